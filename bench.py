@@ -1,0 +1,309 @@
+#!/usr/bin/env python3
+"""bench.py — BASELINE.json metric: "GiB/s device-resident fp32 bucket reduce
+per GPU; % of HBM3E peak".
+
+  python bench.py [--gpus N --steps K --warmup W]
+  (N > 1: launched by torch.distributed.run, one rank per GPU)
+
+N = 1 (BASELINE.json configs[1], C2): one step = one launch of the HIP bucket
+reduce z = x + y over a device-resident 256 MiB fp32 bucket (67,108,864
+elements; the reference's recvOnto step, session.go:255-264, at bucket
+granularity). value = bucket GiB/s = S / t.
+
+N > 1: one step = the S-SGD all-reduce of a 256 MiB fp32 gradient bucket per
+rank: RCCL reduce-scatter(sum) -> HIP /np epilogue on the shard -> RCCL
+all-gather over xGMI (kungfu_amd.collective). Per-GPU work is fixed
+(scaling "weak"); value = N * S / t (whole job). The local-reduce kernel is
+also timed on every rank so the roofline object always describes the HIP
+reduce kernel.
+
+Roofline: algorithmic bytes per launch = 3 * S (read x, read y, write z)
+(SURVEY.md §8d), achieved = 3S / (average launch duration from HIP events on
+the launch stream), peak = 8.0 TB/s HBM3E (MI355X_MICROARCH.md). `traffic` is
+the PMC-measured HBM bytes per launch from profiles/ (rocprofv3 FETCH_SIZE x2
++ WRITE_SIZE, gfx950 correction), null if not recorded.
+
+cpu_baseline: the oracle's restatement of KungFu's std_transform_2 (compiled
+with the reference's -O2 -mavx -mf16c), 1 thread, on the same 256 MiB sum
+repeated for about --cpu-seconds; rank 0 at N = 1 only.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "GiB/s device-resident fp32 bucket reduce per GPU; % of HBM3E peak"
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec, MI355X_MICROARCH.md
+BUCKET_ELEMS = 64 << 20  # 256 MiB of fp32
+KF_FLOAT = 0x20408
+KF_SUM = 0
+REDUCE_KERNEL = "reduce_kernel<float, SUM, NONE, 2>"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--elems", type=int, default=BUCKET_ELEMS)
+    ap.add_argument("--buckets", type=int, default=4,
+                    help="N>1: split the bucket into this many pipelined buckets")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-staged", action="store_true")
+    ap.add_argument("--profile-only", action="store_true",
+                    help="only the timed kernel loop (for rocprofv3 runs)")
+    return ap.parse_args()
+
+
+def load_traffic():
+    """PMC HBM bytes per launch of the reduce kernel, if profiled (profiles/)."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        d = json.load(f)
+    return d.get("hbm_bytes_per_launch"), d.get("source")
+
+
+def time_local_reduce(lib, x, y, z, steps, warmup, world):
+    """Average duration of one reduce launch over `steps` back-to-back launches,
+    from HIP events on the launch stream; plus wall time per step."""
+    from kungfu_amd import _lib
+    stream = torch.cuda.current_stream()
+    sp = stream.cuda_stream
+    ptrs = _lib.ptr_array([x.data_ptr(), y.data_ptr()])
+    n = z.numel()
+    zp = z.data_ptr()
+    fn = lib.kf_bucket_reduce
+    for _ in range(warmup):
+        rc = fn(ptrs, 2, zp, n, KF_FLOAT, KF_SUM, sp)
+    if warmup:
+        _lib.check(rc, "kf_bucket_reduce")
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(steps):
+        fn(ptrs, 2, zp, n, KF_FLOAT, KF_SUM, sp)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    err = lib.kf_last_error()
+    kernel_s = ev0.elapsed_time(ev1) / 1e3 / steps
+    return kernel_s, wall, err
+
+
+def cpu_baseline(x, y, seconds):
+    from oracle import oracle
+    oracle.build()
+    xh = x.cpu().numpy()
+    yh = y.cpu().numpy()
+    zh = np.empty_like(xh)
+    t1 = oracle.bench_transform2(xh, yh, zh, "f32", "sum", 1, threads=1)
+    reps = max(1, min(1000, int(seconds / max(t1, 1e-6))))
+    t = oracle.bench_transform2(xh, yh, zh, "f32", "sum", reps, threads=1)
+    s_bytes = xh.nbytes
+    cpu_model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu_model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {
+        "value": round(reps * s_bytes / t / 2**30, 3),
+        "unit": "GiB/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": "%d x std_transform_2(f32, SUM) over the same 256 MiB bucket, "
+                  "1 thread, oracle restatement built -O2 -mavx -mf16c, %.1f s, %s"
+                  % (reps, t, cpu_model),
+    }
+
+
+def host_staged(lib, x, y):
+    """Copy-inclusive rate of the drop-in: pageable host x,y -> HBM -> kernel
+    -> host z (std_transform_2's path). Not `value`."""
+    xh = x.cpu().numpy()
+    yh = y.cpu().numpy()
+    zh = np.empty_like(xh)
+    n = xh.size
+    rc = lib.kf_transform2_host(xh.ctypes.data, yh.ctypes.data, zh.ctypes.data, n,
+                                KF_FLOAT, KF_SUM)
+    if rc != 0:
+        return {"error": lib.kf_last_error().decode()}
+    reps = 3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        lib.kf_transform2_host(xh.ctypes.data, yh.ctypes.data, zh.ctypes.data, n,
+                               KF_FLOAT, KF_SUM)
+    t = (time.perf_counter() - t0) / reps
+    ok = bool(np.array_equal(zh, xh + yh))
+    return {"value": round(xh.nbytes / t / 2**30, 3), "unit": "GiB/s",
+            "ms_per_call": round(t * 1e3, 3), "correct": ok,
+            "path": "pageable host -> HBM -> HIP kernel -> pageable host"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from kungfu_amd import _lib
+    lib = _lib.load()
+    if lib.kf_device_count() < 1:
+        raise SystemExit("kungfu_amd: no HIP device visible")
+
+    n = args.elems
+    g0 = torch.Generator(device=dev).manual_seed(2 * rank)
+    g1 = torch.Generator(device=dev).manual_seed(2 * rank + 1)
+    x = torch.randn(n, device=dev, generator=g0)
+    y = torch.randn(n, device=dev, generator=g1)
+    z = torch.empty_like(x)
+    s_bytes = x.numel() * x.element_size()
+
+    kernel_s, wall_local, _ = time_local_reduce(lib, x, y, z, args.steps,
+                                                args.warmup, world)
+    if args.profile_only:
+        if rank == 0:
+            print(json.dumps({"kernel_us": kernel_s * 1e6}))
+        return
+
+    out = {}
+    if world == 1:
+        step_s = wall_local / args.steps
+        value = s_bytes / kernel_s / 2**30
+        # parity spot check of the timed output (full check: tests/)
+        zz = z[:1 << 20].cpu().numpy()
+        assert np.array_equal(zz, x[:1 << 20].cpu().numpy() + y[:1 << 20].cpu().numpy())
+        workload = "C2: device-resident z = x + y, one 256 MiB fp32 bucket"
+        parallelism = "single GPU"
+    else:
+        from kungfu_amd.collective import Exchange, GradBuckets
+        ex = Exchange()
+        gb = GradBuckets([n], torch.float32, dev, world, n_buckets=1)
+        # split the one bucket into --buckets pipelined pieces
+        pieces = [gb.buckets[0][b:e] for b, e in
+                  _even_aligned(gb.buckets[0].numel(), args.buckets, world)]
+        gb.buckets[0].copy_(torch.cat([x, torch.zeros(gb.buckets[0].numel() - n, device=dev)]))
+        for _ in range(args.warmup):
+            ex.all_reduce_(pieces, average=True)
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            ex.all_reduce_(pieces, average=True)
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        step_s = t.item() / args.steps
+        value = world * s_bytes / step_s / 2**30
+        busbw = 2 * (world - 1) / world * s_bytes / step_s / 1e9
+        out["collective"] = {
+            "busbw_GBps": round(busbw, 2),
+            "algbw_GiBps_per_gpu": round(s_bytes / step_s / 2**30, 3),
+            "xgmi_bound_GBps": round(153.0 * (world - 1), 1),
+            "frac_of_xgmi": round(busbw / (153.0 * (world - 1)), 4),
+            "buckets": args.buckets,
+        }
+        workload = ("S-SGD all-reduce of a 256 MiB fp32 bucket per rank: RCCL "
+                    "reduce-scatter -> HIP /np -> RCCL all-gather")
+        parallelism = "dp%d" % world
+        kt = torch.tensor([kernel_s], dtype=torch.float64, device=dev)
+        dist.all_reduce(kt, op=dist.ReduceOp.MAX)
+        kernel_s = kt.item()
+
+    traffic, tsrc = load_traffic()
+    achieved = 3 * s_bytes / kernel_s / 1e9
+    res = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(step_s * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic: N(0,1) fp32 from torch.Generator seeds (2r, 2r+1)",
+        "config": {
+            "workload": workload,
+            "bucket_bytes": s_bytes,
+            "elements": n,
+            "parallelism": parallelism,
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": REDUCE_KERNEL,
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 4),
+            "traffic": traffic,
+            "traffic_source": tsrc,
+            "bytes_per_launch": 3 * s_bytes,
+            "kernel_us": round(kernel_s * 1e6, 2),
+        },
+    }
+    res.update(out)
+    if rank == 0 and world == 1:
+        if not args.no_host_staged:
+            res["host_staged"] = host_staged(lib, x, y)
+        if not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(x, y, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def _even_aligned(total, k, world):
+    """k contiguous ranges over [0, total), each divisible by world*64."""
+    unit = world * 64
+    units = total // unit
+    out, off = [], 0
+    q, r = divmod(units, k)
+    for i in range(k):
+        c = (q + (1 if i < r else 0)) * unit
+        if c:
+            out.append((off, off + c))
+        off += c
+    if off < total:
+        out[-1] = (out[-1][0], total)
+    return out
+
+
+if __name__ == "__main__":
+    main()

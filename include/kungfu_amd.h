@@ -1,0 +1,142 @@
+/*
+ * kungfu_amd.h — C-ABI of the MI355X gradient-bucket reduce.
+ *
+ * Two layers live behind this header (libkungfu_amd.so, built from
+ * kungfu_amd/csrc/ for gfx950):
+ *
+ *  B1  drop-in element kernel. Link-compatible with KungFu's base package:
+ *        std_transform_2   replaces /root/reference/srcs/go/kungfu/base/op.cpp:57-93
+ *                          (declared in srcs/cpp/include/kungfu/op.h:17-19)
+ *        kungfu_type_size  replaces srcs/go/kungfu/base/dtype.c:7-35
+ *                          (declared in srcs/cpp/include/kungfu/dtype.h:46)
+ *        float16_sum       replaces srcs/go/kungfu/base/f16.c:25-50
+ *                          (declared in srcs/go/kungfu/base/f16.h:7)
+ *      These take HOST pointers, run the reduce on the GPU (pageable host
+ *      memory -> HBM -> HIP kernel -> host) and return only when the output
+ *      is written, as cgo requires (srcs/go/kungfu/base/op.go:27-35). Bad
+ *      dtype/op -> exit(1), exactly like op.cpp:41,52,89 and dtype.c:31-33.
+ *
+ *  B2  bucket-level device API (the real fast path). Device
+ *      pointers, a hipStream_t passed as void*, no allocation, no host sync,
+ *      error codes instead of exit(). Safe to capture into a hipGraph.
+ *
+ * Enum values are bit-identical to the reference ABI:
+ *      KungFu_Datatype  srcs/cpp/include/kungfu/dtype.h:21-39  ((cat<<16)|(bytes<<8)|8)
+ *      KungFu_Op        srcs/cpp/include/kungfu/op.h:8-13
+ * KungFu_BFLOAT16 is an extension (category 2, 2 bytes, bits-per-byte field 9
+ * so it cannot collide with FLOAT16); the reference has no bf16 type and maps
+ * TF bf16 onto FLOAT16 (srcs/cpp/include/kungfu/tensorflow/ops.h:21-22).
+ */
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- reference-compatible enums ---------------------------------------- */
+
+enum KungFu_Datatype {
+    KungFu_UINT8   = 0x00108,
+    KungFu_UINT16  = 0x00208,
+    KungFu_UINT32  = 0x00408,
+    KungFu_UINT64  = 0x00808,
+    KungFu_INT8    = 0x10108,
+    KungFu_INT16   = 0x10208,
+    KungFu_INT32   = 0x10408,
+    KungFu_INT64   = 0x10808,
+    KungFu_FLOAT16 = 0x20208,
+    KungFu_FLOAT   = 0x20408,
+    KungFu_DOUBLE  = 0x20808,
+    KungFu_BOOL    = 0x30108,
+    /* extension, not in the reference */
+    KungFu_BFLOAT16 = 0x20209,
+};
+typedef enum KungFu_Datatype KungFu_Datatype;
+
+enum KungFu_Op {
+    KungFu_SUM  = 0,
+    KungFu_MIN  = 1,
+    KungFu_MAX  = 2,
+    KungFu_PROD = 3,
+};
+typedef enum KungFu_Op KungFu_Op;
+
+/* ---- B1: drop-in host-pointer entry points ------------------------------ */
+
+/* out[i] = o(input1[i], input2[i]) for i < n. out may alias input1 or input2
+ * exactly. Replaces srcs/go/kungfu/base/op.cpp:57-93. */
+void std_transform_2(const void *input1, const void *input2, void *output,
+                     const int n, const KungFu_Datatype dt, const KungFu_Op o);
+
+/* sizeof one element; unknown dtype -> message + exit(1).
+ * Replaces srcs/go/kungfu/base/dtype.c:7-35. */
+uint32_t kungfu_type_size(KungFu_Datatype dt);
+
+/* z[i] = fp16(fp32(x[i]) + fp32(y[i])), round-to-nearest-even.
+ * Replaces srcs/go/kungfu/base/f16.c:25-50. */
+void float16_sum(void *z, const void *x, const void *y, int len);
+
+/* ---- B2: bucket-level device API ---------------------------------------- */
+
+enum KF_Status {
+    KF_OK              = 0,
+    KF_ERR_DTYPE       = 1, /* unsupported dtype                      */
+    KF_ERR_OP          = 2, /* unsupported op for this dtype          */
+    KF_ERR_ARG         = 3, /* null pointer with n>0, k out of range  */
+    KF_ERR_HIP         = 4, /* a HIP runtime call failed              */
+    KF_ERR_NO_DEVICE   = 5, /* no usable gfx950 device                */
+};
+
+/* Largest k accepted by kf_bucket_reduce*. */
+#define KF_MAX_INPUTS 16
+
+/* out[i] = (((in[0][i] o in[1][i]) o in[2][i]) ... o in[k-1][i])
+ * Left fold in the given order: pass the peers in the reference's arrival or
+ * ring order to reproduce its accumulation order bit for bit
+ * (session.go:255-264 applies Transform2(recv, acc, peer) per hop).
+ * fp16 rounds to fp16 after every hop, as the reference chain does; bf16
+ * accumulates in fp32 and rounds once (build-defined, parity unpinned).
+ * k == 1 is a copy. out may alias any input exactly. */
+int kf_bucket_reduce(const void *const *inputs, int k, void *out, size_t n,
+                     KungFu_Datatype dt, KungFu_Op op, void *stream);
+
+/* S-SGD epilogue fused into the reduce: out[i] = fold_SUM(in[*][i]) / np,
+ * a true IEEE division (TF's g / np, sync_sgd.py:103-104), so it is bit-exact
+ * against "reduce, then divide" for every np. float types only. */
+int kf_bucket_reduce_avg(const void *const *inputs, int k, void *out, size_t n,
+                         KungFu_Datatype dt, int np, void *stream);
+
+/* In-place scale of an already-summed shard: x[i] = x[i] / np (the step
+ * between RCCL reduce-scatter and all-gather). float types only. */
+int kf_bucket_div(void *x, size_t n, KungFu_Datatype dt, int np, void *stream);
+
+/* SMA epilogue (sma_sgd.py:60-65):
+ *   v[i] = fl(fl(c1 * v[i]) + fl(c2 * fl(sum[i] / np)))
+ * with c1 = (float)(1 - alpha), c2 = (float)alpha computed in double first,
+ * as TF converts the Python constants. No FMA contraction. float types only. */
+int kf_sma_blend(void *v, const void *sum, size_t n, KungFu_Datatype dt,
+                 int np, double alpha, void *stream);
+
+/* ---- runtime / diagnostics ---------------------------------------------- */
+
+/* HIP device count visible to the library (0 on a GPU-less host). */
+int kf_device_count(void);
+
+/* Library/ABI version string. */
+const char *kf_version(void);
+
+/* Last HIP error string recorded by the library on this thread. */
+const char *kf_last_error(void);
+
+/* Host-staged variant of std_transform_2 with an explicit chunked pipeline:
+ * pageable host x,y -> pinned staging -> HBM -> kernel -> host out, double
+ * buffered over two HIP streams. Returns KF_Status. Used by the copy-inclusive
+ * measurement. */
+int kf_transform2_host(const void *x, const void *y, void *out, size_t n,
+                       KungFu_Datatype dt, KungFu_Op op);
+
+#ifdef __cplusplus
+}
+#endif

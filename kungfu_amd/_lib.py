@@ -1,0 +1,104 @@
+"""ctypes binding of libkungfu_amd.so (include/kungfu_amd.h).
+
+The shared library is built in-tree by ``kungfu_amd/csrc/Makefile``
+(``__graft_entry__.build()``). There is deliberately no fallback: if the
+library is missing, or the process has no GPU, the product path raises.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libkungfu_amd.so")
+
+# Every symbol include/kungfu_amd.h declares (checked by tests/test_capi.py).
+EXPORTED = (
+    "std_transform_2",
+    "kungfu_type_size",
+    "float16_sum",
+    "kf_bucket_reduce",
+    "kf_bucket_reduce_avg",
+    "kf_bucket_div",
+    "kf_sma_blend",
+    "kf_device_count",
+    "kf_version",
+    "kf_last_error",
+    "kf_transform2_host",
+)
+
+STATUS = {
+    0: "KF_OK",
+    1: "KF_ERR_DTYPE",
+    2: "KF_ERR_OP",
+    3: "KF_ERR_ARG",
+    4: "KF_ERR_HIP",
+    5: "KF_ERR_NO_DEVICE",
+}
+
+MAX_INPUTS = 16
+
+_lib = None
+
+
+class KungFuAMDError(RuntimeError):
+    pass
+
+
+def load():
+    """Load (once) and return the ctypes handle of libkungfu_amd.so."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise KungFuAMDError(
+            "libkungfu_amd.so not built (%s); run __graft_entry__.build() or "
+            "make -C kungfu_amd/csrc" % LIB_PATH)
+    # torch (if present) must bring its HIP runtime first so both resolve the
+    # same libamdhip64.so.7 (same SONAME, one runtime per process).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    c_void_p, c_size_t, c_int = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+    lib.std_transform_2.argtypes = [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int]
+    lib.std_transform_2.restype = None
+    lib.kungfu_type_size.argtypes = [c_int]
+    lib.kungfu_type_size.restype = ctypes.c_uint32
+    lib.float16_sum.argtypes = [c_void_p, c_void_p, c_void_p, c_int]
+    lib.float16_sum.restype = None
+    lib.kf_bucket_reduce.argtypes = [ctypes.POINTER(c_void_p), c_int, c_void_p,
+                                     c_size_t, c_int, c_int, c_void_p]
+    lib.kf_bucket_reduce.restype = c_int
+    lib.kf_bucket_reduce_avg.argtypes = [ctypes.POINTER(c_void_p), c_int, c_void_p,
+                                         c_size_t, c_int, c_int, c_void_p]
+    lib.kf_bucket_reduce_avg.restype = c_int
+    lib.kf_bucket_div.argtypes = [c_void_p, c_size_t, c_int, c_int, c_void_p]
+    lib.kf_bucket_div.restype = c_int
+    lib.kf_sma_blend.argtypes = [c_void_p, c_void_p, c_size_t, c_int, c_int,
+                                 ctypes.c_double, c_void_p]
+    lib.kf_sma_blend.restype = c_int
+    lib.kf_device_count.argtypes = []
+    lib.kf_device_count.restype = c_int
+    lib.kf_version.argtypes = []
+    lib.kf_version.restype = ctypes.c_char_p
+    lib.kf_last_error.argtypes = []
+    lib.kf_last_error.restype = ctypes.c_char_p
+    lib.kf_transform2_host.argtypes = [c_void_p, c_void_p, c_void_p, c_size_t,
+                                       c_int, c_int]
+    lib.kf_transform2_host.restype = c_int
+    _lib = lib
+    return lib
+
+
+def check(rc, what):
+    if rc != 0:
+        lib = load()
+        raise KungFuAMDError("%s failed: %s (%s)" % (
+            what, STATUS.get(rc, rc), lib.kf_last_error().decode()))
+
+
+def ptr_array(ptrs):
+    arr = (ctypes.c_void_p * len(ptrs))()
+    for i, p in enumerate(ptrs):
+        arr[i] = p
+    return arr

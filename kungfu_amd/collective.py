@@ -1,0 +1,219 @@
+"""Bucketed data-parallel all-reduce across the GPUs of a node.
+
+What the reference does (per gradient tensor, on the host):
+  AllReduce op -> Session.AllReduce -> 1 MiB chunks -> strategy graphs ->
+  std_transform_2 per received chunk (session.go:231-326), then the optimizer
+  divides by np in a separate TF op (sync_sgd.py:103-104) or blends
+  (sma_sgd.py:60-65).
+
+What this module does instead: gradients live in a few large
+flat device buckets; each bucket is split evenly into one shard per rank and
+  1. RCCL reduce-scatter (sum)  — each rank receives the sum of its shard
+  2. HIP epilogue on the shard  — /np (S-SGD) via kf_bucket_div, bit-exact
+                                  against "sum, then g / np"
+  3. RCCL all-gather            — every rank gets the full reduced bucket
+over xGMI, one process per GPU. Buckets are issued back to back so the
+epilogue of bucket i overlaps the reduce-scatter of bucket i+1 (all RS on the
+RCCL stream first, each AG queued behind its own epilogue).
+
+The epilogue runs through ``kungfu_amd.ops`` (HIP kernels). It is injectable
+only so the orchestration can be exercised over gloo on CPU in tests; the
+product default is the HIP path and it raises on CPU tensors.
+"""
+import torch
+import torch.distributed as dist
+
+from . import ops
+from .base import OP_NAMES, OP, EvenPartition
+
+# Shards start on 256-byte boundaries so every shard pointer is 16-B aligned
+# for the vector path and RCCL's preferred alignment.
+ALIGN_BYTES = 256
+
+_RED_OPS = {
+    OP.SUM: dist.ReduceOp.SUM,
+    OP.MIN: dist.ReduceOp.MIN,
+    OP.MAX: dist.ReduceOp.MAX,
+    OP.PROD: dist.ReduceOp.PRODUCT,
+}
+
+
+class HipEpilogue:
+    """The shard epilogues as HIP kernels (default, product path)."""
+
+    def div_(self, x, np_):
+        return ops.bucket_div_(x, np_)
+
+    def sma_blend_(self, v, summed, np_, alpha):
+        return ops.sma_blend_(v, summed, np_, alpha)
+
+
+def padded_count(count, world, itemsize):
+    """Smallest length >= count that splits into `world` aligned shards."""
+    unit = world * max(1, ALIGN_BYTES // itemsize)
+    return ((count + unit - 1) // unit) * unit
+
+
+class Exchange:
+    """One process group, its shard workspaces and the epilogue."""
+
+    def __init__(self, group=None, epilogue=None):
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.epilogue = epilogue if epilogue is not None else HipEpilogue()
+        self._ws = {}
+
+    def _workspace(self, key, n, like):
+        t = self._ws.get(key)
+        if t is None or t.numel() < n or t.dtype != like.dtype or t.device != like.device:
+            t = torch.empty(n, dtype=like.dtype, device=like.device)
+            self._ws[key] = t
+        return t[:n]
+
+    def _check(self, buf):
+        if buf.dim() != 1 or not buf.is_contiguous():
+            raise ValueError("bucket must be a flat contiguous tensor")
+        if buf.numel() % self.world:
+            raise ValueError("bucket length %d not divisible by world %d; use "
+                             "padded_count()" % (buf.numel(), self.world))
+
+    def all_reduce_(self, buckets, op="sum", average=False):
+        """In-place all-reduce of flat padded buckets. average=True applies the
+        S-SGD epilogue (sum, then / np) on each shard."""
+        red = OP_NAMES[op] if isinstance(op, str) else OP(op)
+        if average and red != OP.SUM:
+            raise ValueError("average requires op='sum'")
+        for b in buckets:
+            self._check(b)
+        if self.world == 1:
+            # a single peer: the reduce is the identity; g / 1 == g exactly
+            return buckets
+        shards = []
+        works = []
+        for i, b in enumerate(buckets):
+            shard = self._workspace(("rs", i), b.numel() // self.world, b)
+            works.append(dist.reduce_scatter_tensor(shard, b, op=_RED_OPS[red],
+                                                    group=self.group, async_op=True))
+            shards.append(shard)
+        gathers = []
+        for b, shard, w in zip(buckets, shards, works):
+            w.wait()
+            if average:
+                self.epilogue.div_(shard, self.world)
+            gathers.append(dist.all_gather_into_tensor(b, shard, group=self.group,
+                                                       async_op=True))
+        for g in gathers:
+            g.wait()
+        return buckets
+
+    def sma_(self, buckets, alpha):
+        """SMA over flat variable buckets (sma_sgd.py:60-65): each rank's v
+        becomes (1-alpha) v + alpha * (sum_ranks v) / np."""
+        for b in buckets:
+            self._check(b)
+        sums = []
+        for i, b in enumerate(buckets):
+            s = self._workspace(("sum", i), b.numel(), b)
+            if self.world == 1:
+                s.copy_(b)
+            else:
+                shard = self._workspace(("rs", i), b.numel() // self.world, b)
+                dist.reduce_scatter_tensor(shard, b, op=dist.ReduceOp.SUM,
+                                           group=self.group)
+                dist.all_gather_into_tensor(s, shard, group=self.group)
+            sums.append(s)
+        for b, s in zip(buckets, sums):
+            self.epilogue.sma_blend_(b, s, self.world, alpha)
+        return buckets
+
+
+class GradBuckets:
+    """Flat, padded device storage for a list of same-dtype tensors.
+
+    Tensors are grouped, in order, into buckets of about ``bucket_bytes`` at
+    tensor boundaries (a tensor larger than that gets a bucket of its own);
+    each bucket is padded to split into `world` aligned shards. ``views[i]``
+    is tensor i's view into the flat storage, so gradients can be written in
+    place and reduced without fuse/defuse copies (the reference's NCCL path
+    concatenates and slices instead, ops/__init__.py:29-46).
+    """
+
+    def __init__(self, numels, dtype, device, world, bucket_bytes=32 << 20,
+                 n_buckets=None):
+        itemsize = torch.empty((), dtype=dtype).element_size()
+        total = sum(numels)
+        if n_buckets is not None:  # EvenPartition of the fused total
+            groups = self._groups_even(numels, total, n_buckets)
+        else:
+            groups = self._groups_greedy(numels, bucket_bytes // itemsize)
+        self.buckets, self.views, self.spans = [], [None] * len(numels), []
+        for g in groups:
+            count = sum(numels[i] for i in g)
+            b = torch.zeros(padded_count(max(count, 1), world, itemsize),
+                            dtype=dtype, device=device)
+            off = 0
+            for i in g:
+                self.views[i] = b[off:off + numels[i]]
+                off += numels[i]
+            self.buckets.append(b)
+            self.spans.append(count)
+
+    @staticmethod
+    def _groups_greedy(numels, cap):
+        groups, cur, size = [], [], 0
+        for i, n in enumerate(numels):
+            if cur and size + n > cap:
+                groups.append(cur)
+                cur, size = [], 0
+            cur.append(i)
+            size += n
+        if cur:
+            groups.append(cur)
+        return groups
+
+    @staticmethod
+    def _groups_even(numels, total, k):
+        # targets from EvenPartition (interval.go:12-27), snapped to tensor ends
+        bounds = [e for _, e in EvenPartition(0, total, k)]
+        groups, cur, acc, bi = [], [], 0, 0
+        for i, n in enumerate(numels):
+            cur.append(i)
+            acc += n
+            if bi < len(bounds) and acc >= bounds[bi]:
+                groups.append(cur)
+                cur = []
+                while bi < len(bounds) and acc >= bounds[bi]:
+                    bi += 1
+        if cur:
+            groups.append(cur)
+        return groups
+
+
+def group_all_reduce(tensors, op="sum", average=False, exchange=None,
+                     bucket_bytes=32 << 20):
+    """Mirror of the reference's group_all_reduce (ops/collective.py:71-73):
+    returns all-reduced copies of `tensors`. Fuses them into flat buckets
+    (copy in, reduce, copy out); optimizers that own their gradient storage
+    use GradBuckets directly and skip the copies."""
+    ex = exchange or Exchange()
+    if not tensors:
+        return []
+    by_dtype = {}
+    for i, t in enumerate(tensors):
+        by_dtype.setdefault((t.dtype, t.device), []).append(i)
+    out = [None] * len(tensors)
+    for (dtype, device), idx in by_dtype.items():
+        gb = GradBuckets([tensors[i].numel() for i in idx], dtype, device,
+                         ex.world, bucket_bytes=bucket_bytes)
+        for j, i in enumerate(idx):
+            gb.views[j].copy_(tensors[i].reshape(-1))
+        ex.all_reduce_(gb.buckets, op=op, average=average)
+        for j, i in enumerate(idx):
+            out[i] = gb.views[j].view_as(tensors[i]).clone()
+    return out
+
+
+def all_reduce(t, op="sum", exchange=None):
+    """Mirror of all_reduce(t, op) (ops/collective.py:22-24)."""
+    return group_all_reduce([t], op=op, exchange=exchange)[0]

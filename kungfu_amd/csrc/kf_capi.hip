@@ -1,0 +1,453 @@
+// kf_capi.hip — C-ABI entry points of libkungfu_amd.so (include/kungfu_amd.h).
+//
+// B2 (device API): dtype/op/epilogue dispatch onto the templated kernels in
+// kf_reduce_kernels.hpp, launch geometry, alignment handling. Never allocates,
+// never synchronises: capture-safe.
+//
+// B1 (drop-in, host pointers): std_transform_2 / float16_sum move the caller's
+// host buffers to HBM, run the same kernels, copy the result back and return
+// when it is written (cgo contract, srcs/go/kungfu/base/op.go:27-35). Each
+// calling OS thread gets its own stream and device scratch (the reference
+// calls this concurrently from one goroutine per chunk, session.go:317-323).
+// There is no CPU fallback: without a device the call prints why and exits,
+// as the reference does for any unusable argument (op.cpp:41,52,89).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "kf_reduce_kernels.hpp"
+#include "kungfu_amd.h"
+
+namespace
+{
+using namespace kf;
+
+constexpr int kBlock = 256;
+
+// Launch geometry for the streaming body. Tuned on MI355X with
+// tools/tune_reduce.py (DESIGN.md "Kernel tuning"); env overrides exist only
+// for that tuning script.
+struct Geometry {
+    int unroll   = 4;     // 16-B vectors per thread per input per tile
+    int grid_cap = 4096;  // blocks; grid-stride beyond
+    int loadnt   = 0;     // non-temporal read streams
+};
+
+Geometry &geometry()
+{
+    static Geometry g = [] {
+        Geometry g;
+        if (const char *s = std::getenv("KF_UNROLL")) g.unroll = std::atoi(s);
+        if (const char *s = std::getenv("KF_GRID_CAP")) g.grid_cap = std::atoi(s);
+        if (const char *s = std::getenv("KF_LOADNT")) g.loadnt = std::atoi(s);
+        if (g.unroll != 2 && g.unroll != 4 && g.unroll != 8) g.unroll = 4;
+        if (g.grid_cap < 1) g.grid_cap = 4096;
+        g.loadnt = g.loadnt ? 1 : 0;
+        return g;
+    }();
+    return g;
+}
+
+thread_local std::string t_last_error;
+
+int hip_fail(hipError_t e, const char *what)
+{
+    t_last_error = std::string(what) + ": " + hipGetErrorString(e);
+    return KF_ERR_HIP;
+}
+
+#define KF_HIP(call)                                                           \
+    do {                                                                       \
+        hipError_t e_ = (call);                                                \
+        if (e_ != hipSuccess) return hip_fail(e_, #call);                      \
+    } while (0)
+
+int type_size(KungFu_Datatype dt)
+{
+    switch (dt) {
+    case KungFu_UINT8: case KungFu_INT8: case KungFu_BOOL: return 1;
+    case KungFu_UINT16: case KungFu_INT16: case KungFu_FLOAT16:
+    case KungFu_BFLOAT16: return 2;
+    case KungFu_UINT32: case KungFu_INT32: case KungFu_FLOAT: return 4;
+    case KungFu_UINT64: case KungFu_INT64: case KungFu_DOUBLE: return 8;
+    default: return 0;
+    }
+}
+
+bool is_float(KungFu_Datatype dt)
+{
+    return dt == KungFu_FLOAT16 || dt == KungFu_BFLOAT16 || dt == KungFu_FLOAT ||
+           dt == KungFu_DOUBLE;
+}
+
+// ---------------------------------------------------------------------------
+// launch helpers
+// ---------------------------------------------------------------------------
+struct Plan {
+    size_t head = 0, nvec = 0;
+    bool vec_ok = false;
+};
+
+// Vector body needs every pointer at the same 16-B residue; the head peels
+// elements until they are aligned.
+Plan make_plan(const void *const *in, int k, const void *out, size_t n, int sz)
+{
+    Plan p;
+    const uintptr_t r = reinterpret_cast<uintptr_t>(out) & 15u;
+    if (r % sz != 0) return p;
+    for (int j = 0; j < k; ++j) {
+        if ((reinterpret_cast<uintptr_t>(in[j]) & 15u) != r) return p;
+    }
+    size_t head = r == 0 ? 0 : (16 - r) / sz;
+    if (head > n) head = n;
+    p.head   = head;
+    p.nvec   = (n - head) / (16 / sz);
+    p.vec_ok = true;
+    return p;
+}
+
+unsigned grid_for(size_t nvec, size_t nedge, int unroll)
+{
+    const size_t tile   = static_cast<size_t>(kBlock) * unroll;
+    size_t blocks       = (nvec + tile - 1) / tile;
+    const size_t eblk   = (nedge + kBlock - 1) / kBlock;
+    if (blocks > static_cast<size_t>(geometry().grid_cap)) {
+        blocks = geometry().grid_cap;
+    }
+    if (blocks < eblk) blocks = eblk;
+    if (blocks < 1) blocks = 1;
+    return static_cast<unsigned>(blocks);
+}
+
+template <typename T, int OP, int EPI, int KC, int UNROLL, int LOADNT>
+void launch_vec(const InPtrs &ptrs, int k, void *out, size_t n, const Plan &p,
+                int np, hipStream_t s)
+{
+    constexpr int V  = Vec<typename Elt<T>::S>::N;
+    const size_t ned = p.head + (n - p.head - p.nvec * V);
+    const unsigned g = grid_for(p.nvec, ned, UNROLL);
+    reduce_kernel<T, OP, EPI, KC, kBlock, UNROLL, LOADNT>
+        <<<g, kBlock, 0, s>>>(ptrs, k, out, n, p.head, p.nvec, np);
+}
+
+template <typename T, int OP, int EPI, int KC>
+void launch_geom(const InPtrs &ptrs, int k, void *out, size_t n, const Plan &p,
+                 int np, hipStream_t s)
+{
+    const Geometry &g = geometry();
+    // The tuned fp32 2-input SUM (the headline path) carries every geometry
+    // variant; every other combination uses the default unroll 4.
+    if constexpr (std::is_same<T, float>::value && OP == OP_SUM && KC == 2) {
+        if (g.loadnt) {
+            switch (g.unroll) {
+            case 2: return launch_vec<T, OP, EPI, KC, 2, 1>(ptrs, k, out, n, p, np, s);
+            case 8: return launch_vec<T, OP, EPI, KC, 8, 1>(ptrs, k, out, n, p, np, s);
+            default: return launch_vec<T, OP, EPI, KC, 4, 1>(ptrs, k, out, n, p, np, s);
+            }
+        }
+        switch (g.unroll) {
+        case 2: return launch_vec<T, OP, EPI, KC, 2, 0>(ptrs, k, out, n, p, np, s);
+        case 8: return launch_vec<T, OP, EPI, KC, 8, 0>(ptrs, k, out, n, p, np, s);
+        default: break;
+        }
+    }
+    launch_vec<T, OP, EPI, KC, 4, 0>(ptrs, k, out, n, p, np, s);
+}
+
+template <typename T, int OP, int EPI>
+int launch_typed(const void *const *in, int k, void *out, size_t n, int np,
+                 hipStream_t s)
+{
+    using S = typename Elt<T>::S;
+    InPtrs ptrs;
+    for (int j = 0; j < kMaxInputs; ++j) ptrs.p[j] = j < k ? in[j] : nullptr;
+    const Plan p = make_plan(in, k, out, n, sizeof(S));
+    if (!p.vec_ok) {
+        size_t blocks = (n + kBlock - 1) / kBlock;
+        if (blocks > 8192) blocks = 8192;
+        reduce_kernel_unaligned<T, OP, EPI, kBlock>
+            <<<static_cast<unsigned>(blocks), kBlock, 0, s>>>(ptrs, k, out, n, np);
+    } else if (k == 2) {
+        launch_geom<T, OP, EPI, 2>(ptrs, k, out, n, p, np, s);
+    } else {
+        launch_geom<T, OP, EPI, 0>(ptrs, k, out, n, p, np, s);
+    }
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "reduce kernel launch");
+    return KF_OK;
+}
+
+template <typename T, int EPI>
+int dispatch_op(const void *const *in, int k, void *out, size_t n, KungFu_Op op,
+                int np, hipStream_t s)
+{
+    if constexpr (std::is_same<T, f16_t>::value) {
+        if (op != KungFu_SUM) return KF_ERR_OP;  // op.cpp:45-54
+        return launch_typed<T, OP_SUM, EPI>(in, k, out, n, np, s);
+    } else {
+        if constexpr (EPI == EPI_DIV) {
+            if (op != KungFu_SUM) return KF_ERR_OP;
+            return launch_typed<T, OP_SUM, EPI>(in, k, out, n, np, s);
+        } else {
+            switch (op) {
+            case KungFu_SUM: return launch_typed<T, OP_SUM, EPI>(in, k, out, n, np, s);
+            case KungFu_MIN: return launch_typed<T, OP_MIN, EPI>(in, k, out, n, np, s);
+            case KungFu_MAX: return launch_typed<T, OP_MAX, EPI>(in, k, out, n, np, s);
+            case KungFu_PROD: return launch_typed<T, OP_PROD, EPI>(in, k, out, n, np, s);
+            default: return KF_ERR_OP;
+            }
+        }
+    }
+}
+
+int dispatch_none(const void *const *in, int k, void *out, size_t n,
+                  KungFu_Datatype dt, KungFu_Op op, hipStream_t s)
+{
+    switch (dt) {
+    case KungFu_UINT8: return dispatch_op<uint8_t, EPI_NONE>(in, k, out, n, op, 1, s);
+    case KungFu_UINT16: return dispatch_op<uint16_t, EPI_NONE>(in, k, out, n, op, 1, s);
+    case KungFu_UINT32: return dispatch_op<uint32_t, EPI_NONE>(in, k, out, n, op, 1, s);
+    case KungFu_UINT64: return dispatch_op<uint64_t, EPI_NONE>(in, k, out, n, op, 1, s);
+    case KungFu_INT8: return dispatch_op<int8_t, EPI_NONE>(in, k, out, n, op, 1, s);
+    case KungFu_INT16: return dispatch_op<int16_t, EPI_NONE>(in, k, out, n, op, 1, s);
+    case KungFu_INT32: return dispatch_op<int32_t, EPI_NONE>(in, k, out, n, op, 1, s);
+    case KungFu_INT64: return dispatch_op<int64_t, EPI_NONE>(in, k, out, n, op, 1, s);
+    case KungFu_FLOAT16: return dispatch_op<f16_t, EPI_NONE>(in, k, out, n, op, 1, s);
+    case KungFu_FLOAT: return dispatch_op<float, EPI_NONE>(in, k, out, n, op, 1, s);
+    case KungFu_DOUBLE: return dispatch_op<double, EPI_NONE>(in, k, out, n, op, 1, s);
+    case KungFu_BFLOAT16: return dispatch_op<bf16_t, EPI_NONE>(in, k, out, n, op, 1, s);
+    default: return KF_ERR_DTYPE;  // BOOL and unknown: op.cpp:88-89
+    }
+}
+
+int dispatch_div(const void *const *in, int k, void *out, size_t n,
+                 KungFu_Datatype dt, int np, hipStream_t s)
+{
+    switch (dt) {
+    case KungFu_FLOAT16: return dispatch_op<f16_t, EPI_DIV>(in, k, out, n, KungFu_SUM, np, s);
+    case KungFu_FLOAT: return dispatch_op<float, EPI_DIV>(in, k, out, n, KungFu_SUM, np, s);
+    case KungFu_DOUBLE: return dispatch_op<double, EPI_DIV>(in, k, out, n, KungFu_SUM, np, s);
+    case KungFu_BFLOAT16: return dispatch_op<bf16_t, EPI_DIV>(in, k, out, n, KungFu_SUM, np, s);
+    default: return KF_ERR_DTYPE;
+    }
+}
+
+int check_args(const void *const *inputs, int k, const void *out, size_t n)
+{
+    if (k < 1 || k > KF_MAX_INPUTS) return KF_ERR_ARG;
+    if (n == 0) return KF_OK;
+    if (!inputs || !out) return KF_ERR_ARG;
+    for (int j = 0; j < k; ++j) {
+        if (!inputs[j]) return KF_ERR_ARG;
+    }
+    return KF_OK;
+}
+
+template <typename T, typename C>
+int launch_sma(void *v, const void *sum, size_t n, int np, C c1, C c2,
+               hipStream_t s)
+{
+    using S              = typename SmaMath<T>::S;
+    const void *ins[1]   = {sum};
+    const Plan p         = make_plan(ins, 1, v, n, sizeof(S));
+    constexpr int V      = Vec<S>::N;
+    size_t blocks;
+    if (p.vec_ok) {
+        const size_t ned = p.head + (n - p.head - p.nvec * V);
+        blocks           = grid_for(p.nvec, ned, 4);
+    } else {
+        blocks = (n + kBlock - 1) / kBlock;
+        if (blocks > 8192) blocks = 8192;
+    }
+    sma_kernel<T, C, kBlock, 4><<<static_cast<unsigned>(blocks), kBlock, 0, s>>>(
+        v, sum, n, p.head, p.nvec, c1, c2, np, p.vec_ok ? 1 : 0);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "sma kernel launch");
+    return KF_OK;
+}
+
+// ---------------------------------------------------------------------------
+// B1 support: per-thread staging context
+// ---------------------------------------------------------------------------
+struct Staging {
+    hipStream_t stream = nullptr;
+    void *dev          = nullptr;  // 3 regions: x | y | z
+    size_t cap         = 0;        // bytes per region
+    int device         = -1;
+
+    ~Staging()
+    {
+        // Process teardown may have unloaded the runtime already; best effort.
+        if (dev) (void)hipFree(dev);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+
+    int ensure(size_t bytes)
+    {
+        if (!stream) {
+            int cnt = 0;
+            if (hipGetDeviceCount(&cnt) != hipSuccess || cnt == 0) {
+                t_last_error = "no HIP device";
+                return KF_ERR_NO_DEVICE;
+            }
+            KF_HIP(hipGetDevice(&device));
+            KF_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        }
+        if (bytes > cap) {
+            if (dev) KF_HIP(hipFree(dev));
+            dev            = nullptr;
+            size_t rounded = (bytes + 255) & ~static_cast<size_t>(255);
+            KF_HIP(hipMalloc(&dev, 3 * rounded));
+            cap = rounded;
+        }
+        return KF_OK;
+    }
+};
+
+thread_local Staging t_staging;
+
+// Host pointers -> HBM -> kernel -> host. Synchronous.
+int transform2_host(const void *x, const void *y, void *out, size_t n,
+                    KungFu_Datatype dt, KungFu_Op op)
+{
+    const int sz = type_size(dt);
+    if (sz == 0 || dt == KungFu_BOOL) return KF_ERR_DTYPE;
+    if (n == 0) return KF_OK;
+    const size_t bytes = n * static_cast<size_t>(sz);
+    int rc             = t_staging.ensure(bytes);
+    if (rc != KF_OK) return rc;
+    char *dx          = static_cast<char *>(t_staging.dev);
+    char *dy          = dx + t_staging.cap;
+    char *dz          = dy + t_staging.cap;
+    hipStream_t s     = t_staging.stream;
+    KF_HIP(hipMemcpyAsync(dx, x, bytes, hipMemcpyHostToDevice, s));
+    KF_HIP(hipMemcpyAsync(dy, y, bytes, hipMemcpyHostToDevice, s));
+    const void *ins[2] = {dx, dy};
+    rc                 = dispatch_none(ins, 2, dz, n, dt, op, s);
+    if (rc != KF_OK) return rc;
+    KF_HIP(hipMemcpyAsync(out, dz, bytes, hipMemcpyDeviceToHost, s));
+    KF_HIP(hipStreamSynchronize(s));
+    return KF_OK;
+}
+
+[[noreturn]] void die(const char *fn, int rc)
+{
+    std::fprintf(stderr, "kungfu_amd: %s failed (status %d): %s\n", fn, rc,
+                 t_last_error.c_str());
+    std::exit(1);
+}
+
+}  // namespace
+
+extern "C" {
+
+uint32_t kungfu_type_size(KungFu_Datatype dt)
+{
+    const int sz = type_size(dt);
+    if (sz == 0) {
+        std::fprintf(stderr, "unknown dtype: %d\n", static_cast<int>(dt));
+        std::exit(1);
+    }
+    return static_cast<uint32_t>(sz);
+}
+
+void std_transform_2(const void *input1, const void *input2, void *output,
+                     const int n, const KungFu_Datatype dt, const KungFu_Op o)
+{
+    if (n <= 0) return;  // std::transform over an empty range
+    const int rc = transform2_host(input1, input2, output,
+                                   static_cast<size_t>(n), dt, o);
+    if (rc != KF_OK) die("std_transform_2", rc);
+}
+
+void float16_sum(void *z, const void *x, const void *y, int len)
+{
+    if (len <= 0) return;
+    const int rc = transform2_host(x, y, z, static_cast<size_t>(len),
+                                   KungFu_FLOAT16, KungFu_SUM);
+    if (rc != KF_OK) die("float16_sum", rc);
+}
+
+int kf_bucket_reduce(const void *const *inputs, int k, void *out, size_t n,
+                     KungFu_Datatype dt, KungFu_Op op, void *stream)
+{
+    int rc = check_args(inputs, k, out, n);
+    if (rc != KF_OK || n == 0) return rc;
+    const int sz = type_size(dt);
+    if (sz == 0 || dt == KungFu_BOOL) return KF_ERR_DTYPE;
+    if (op < KungFu_SUM || op > KungFu_PROD) return KF_ERR_OP;
+    if (dt == KungFu_FLOAT16 && op != KungFu_SUM) return KF_ERR_OP;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (k == 1) {
+        if (out != inputs[0]) {
+            KF_HIP(hipMemcpyAsync(out, inputs[0], n * sz, hipMemcpyDeviceToDevice, s));
+        }
+        return KF_OK;
+    }
+    return dispatch_none(inputs, k, out, n, dt, op, s);
+}
+
+int kf_bucket_reduce_avg(const void *const *inputs, int k, void *out, size_t n,
+                         KungFu_Datatype dt, int np, void *stream)
+{
+    int rc = check_args(inputs, k, out, n);
+    if (rc != KF_OK || n == 0) return rc;
+    if (!is_float(dt)) return KF_ERR_DTYPE;
+    if (np < 1) return KF_ERR_ARG;
+    return dispatch_div(inputs, k, out, n, dt, np, static_cast<hipStream_t>(stream));
+}
+
+int kf_bucket_div(void *x, size_t n, KungFu_Datatype dt, int np, void *stream)
+{
+    if (n == 0) return KF_OK;
+    if (!x) return KF_ERR_ARG;
+    if (!is_float(dt)) return KF_ERR_DTYPE;
+    if (np < 1) return KF_ERR_ARG;
+    const void *ins[1] = {x};
+    return dispatch_div(ins, 1, x, n, dt, np, static_cast<hipStream_t>(stream));
+}
+
+int kf_sma_blend(void *v, const void *sum, size_t n, KungFu_Datatype dt, int np,
+                 double alpha, void *stream)
+{
+    if (n == 0) return KF_OK;
+    if (!v || !sum) return KF_ERR_ARG;
+    if (np < 1) return KF_ERR_ARG;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    // TF converts the Python constants (1 - alpha) and alpha to the tensor
+    // dtype after computing them in double (sma_sgd.py:64-65).
+    const float c1f = static_cast<float>(1.0 - alpha);
+    const float c2f = static_cast<float>(alpha);
+    switch (dt) {
+    case KungFu_FLOAT: return launch_sma<float, float>(v, sum, n, np, c1f, c2f, s);
+    case KungFu_DOUBLE: return launch_sma<double, double>(v, sum, n, np, 1.0 - alpha, alpha, s);
+    case KungFu_FLOAT16: return launch_sma<f16_t, float>(v, sum, n, np, c1f, c2f, s);
+    case KungFu_BFLOAT16: return launch_sma<bf16_t, float>(v, sum, n, np, c1f, c2f, s);
+    default: return KF_ERR_DTYPE;
+    }
+}
+
+int kf_device_count(void)
+{
+    int cnt = 0;
+    if (hipGetDeviceCount(&cnt) != hipSuccess) return 0;
+    return cnt;
+}
+
+const char *kf_version(void) { return "kungfu_amd 0.1.0 (gfx950)"; }
+
+const char *kf_last_error(void) { return t_last_error.c_str(); }
+
+int kf_transform2_host(const void *x, const void *y, void *out, size_t n,
+                       KungFu_Datatype dt, KungFu_Op op)
+{
+    if (n > 0 && (!x || !y || !out)) return KF_ERR_ARG;
+    if (dt == KungFu_FLOAT16 && op != KungFu_SUM) return KF_ERR_OP;
+    return transform2_host(x, y, out, n, dt, op);
+}
+
+}  // extern "C"

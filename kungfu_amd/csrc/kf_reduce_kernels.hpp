@@ -1,0 +1,492 @@
+// kf_reduce_kernels.hpp — gfx950 element-wise bucket reduce kernels.
+//
+// The reduce is a pure streaming element-wise op: (k reads + 1 write) per
+// element and at most a handful of VALU instructions, so it is HBM-bound
+// (0.083 flop/B for the fp32 2-input sum) and never touches MFMA or LDS.
+// What matters on MI355X is keeping enough 16-byte loads in flight per CU:
+//   * every lane moves whole 16-B vectors (global_load_dwordx4 /
+//     global_store_dwordx4): 1 KiB per wave-instruction, fully coalesced;
+//   * each thread issues UNROLL independent vector loads per input before the
+//     first use, so a 256-thread block has UNROLL*4 KiB per input in flight;
+//   * the grid is persistent-ish (capped, grid-stride over tiles) so 256 CUs
+//     stay busy without a 16k-block launch tail;
+//   * stores are non-temporal: the output is not re-read by this kernel and
+//     keeping it out of L2 leaves room for the read streams.
+//
+// Numerics follow the reference's host reduce (op.cpp:22-54, f16.c:16-50):
+//   SUM/PROD on integers wrap (done in the unsigned type of the same width),
+//   MIN/MAX are std::min/std::max as selects ((b < a) ? b : a, (a < b) ? b : a),
+//   fp16 SUM = widen, fp32 add, RNE narrow — per hop, as the reference chain,
+//   no FMA contraction anywhere (#pragma below and explicit _rn intrinsics).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#pragma clang fp contract(off)
+
+namespace kf
+{
+enum Op { OP_SUM = 0, OP_MIN = 1, OP_MAX = 2, OP_PROD = 3 };
+enum Epi { EPI_NONE = 0, EPI_DIV = 1 };
+
+// Storage tags for the two 16-bit float formats (stored as raw u16 bits).
+struct f16_t {
+    uint16_t bits;
+};
+struct bf16_t {
+    uint16_t bits;
+};
+
+// IEEE binary16 via the compiler's native _Float16: the widen is exact and the
+// narrow is v_cvt_f16_f32 in the default round-to-nearest-even mode.
+__device__ __forceinline__ float f16_to_f32(uint16_t h)
+{
+    return static_cast<float>(__builtin_bit_cast(_Float16, h));
+}
+
+__device__ __forceinline__ uint16_t f32_to_f16(float f)
+{
+    return __builtin_bit_cast(uint16_t, static_cast<_Float16>(f));
+}
+
+__device__ __forceinline__ float bf16_to_f32(uint16_t h)
+{
+    return __uint_as_float(static_cast<uint32_t>(h) << 16);
+}
+
+// RNE narrow; a NaN keeps its sign and upper payload and is made quiet. The
+// same bit recipe as the oracle, so bf16 results compare bit for bit.
+__device__ __forceinline__ uint16_t f32_to_bf16(float f)
+{
+    uint32_t u = __float_as_uint(f);
+    if ((u & 0x7fffffffu) > 0x7f800000u) {
+        return static_cast<uint16_t>((u >> 16) | 0x0040u);
+    }
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return static_cast<uint16_t>(u >> 16);
+}
+
+// ---------------------------------------------------------------------------
+// Per-dtype arithmetic. `Acc` is what the fold carries between hops.
+// ---------------------------------------------------------------------------
+template <typename T> struct Elt;
+
+template <typename T> struct IntElt {
+    using S   = T;  // storage
+    using Acc = T;
+    using W   = typename std::conditional<(sizeof(T) <= 4), uint32_t,
+                                        uint64_t>::type;
+    __device__ static Acc load(S s) { return s; }
+    __device__ static S store(Acc a) { return a; }
+    template <int OP> __device__ static Acc combine(Acc a, S b)
+    {
+        if constexpr (OP == OP_SUM) {
+            return static_cast<T>(static_cast<W>(a) + static_cast<W>(b));
+        } else if constexpr (OP == OP_PROD) {
+            using U = typename std::make_unsigned<T>::type;
+            return static_cast<T>(static_cast<W>(static_cast<U>(a)) *
+                                  static_cast<W>(static_cast<U>(b)));
+        } else if constexpr (OP == OP_MIN) {
+            return (b < a) ? b : a;
+        } else {
+            return (a < b) ? b : a;
+        }
+    }
+};
+
+template <> struct Elt<uint8_t> : IntElt<uint8_t> {};
+template <> struct Elt<uint16_t> : IntElt<uint16_t> {};
+template <> struct Elt<uint32_t> : IntElt<uint32_t> {};
+template <> struct Elt<uint64_t> : IntElt<uint64_t> {};
+template <> struct Elt<int8_t> : IntElt<int8_t> {};
+template <> struct Elt<int16_t> : IntElt<int16_t> {};
+template <> struct Elt<int32_t> : IntElt<int32_t> {};
+template <> struct Elt<int64_t> : IntElt<int64_t> {};
+
+template <> struct Elt<float> {
+    using S   = float;
+    using Acc = float;
+    __device__ static Acc load(S s) { return s; }
+    __device__ static S store(Acc a) { return a; }
+    template <int OP> __device__ static Acc combine(Acc a, S b)
+    {
+        if constexpr (OP == OP_SUM) {
+            return __fadd_rn(a, b);
+        } else if constexpr (OP == OP_PROD) {
+            return __fmul_rn(a, b);
+        } else if constexpr (OP == OP_MIN) {
+            return (b < a) ? b : a;
+        } else {
+            return (a < b) ? b : a;
+        }
+    }
+    __device__ static S div(Acc a, int np)
+    {
+        return __fdiv_rn(a, static_cast<float>(np));
+    }
+};
+
+template <> struct Elt<double> {
+    using S   = double;
+    using Acc = double;
+    __device__ static Acc load(S s) { return s; }
+    __device__ static S store(Acc a) { return a; }
+    template <int OP> __device__ static Acc combine(Acc a, S b)
+    {
+        if constexpr (OP == OP_SUM) {
+            return __dadd_rn(a, b);
+        } else if constexpr (OP == OP_PROD) {
+            return __dmul_rn(a, b);
+        } else if constexpr (OP == OP_MIN) {
+            return (b < a) ? b : a;
+        } else {
+            return (a < b) ? b : a;
+        }
+    }
+    __device__ static S div(Acc a, int np)
+    {
+        return __ddiv_rn(a, static_cast<double>(np));
+    }
+};
+
+// fp16: the reference chain rounds to fp16 after every Transform2 hop
+// (f16.c:16-23), so the accumulator is re-quantised per hop. Only SUM exists
+// in the reference (op.cpp:45-54); the host wrapper rejects the other ops.
+template <> struct Elt<f16_t> {
+    using S   = uint16_t;
+    using Acc = uint16_t;
+    __device__ static Acc load(S s) { return s; }
+    __device__ static S store(Acc a) { return a; }
+    template <int OP> __device__ static Acc combine(Acc a, S b)
+    {
+        static_assert(OP == OP_SUM, "fp16 supports SUM only");
+        return f32_to_f16(__fadd_rn(f16_to_f32(a), f16_to_f32(b)));
+    }
+    __device__ static S div(Acc a, int np)
+    {
+        return f32_to_f16(__fdiv_rn(f16_to_f32(a), static_cast<float>(np)));
+    }
+};
+
+// bf16 (build-defined, not in the reference): fp32 accumulation, one RNE
+// rounding at the end. MIN/MAX select an input and keep its bits.
+template <> struct Elt<bf16_t> {
+    using S = uint16_t;
+    struct Acc {
+        float f;
+        uint16_t bits;
+    };
+    __device__ static Acc load(S s) { return Acc{bf16_to_f32(s), s}; }
+    __device__ static S store(Acc a) { return a.bits; }
+    template <int OP> __device__ static Acc combine(Acc a, S b)
+    {
+        const float fb = bf16_to_f32(b);
+        if constexpr (OP == OP_SUM) {
+            return Acc{__fadd_rn(a.f, fb), 0};
+        } else if constexpr (OP == OP_PROD) {
+            return Acc{__fmul_rn(a.f, fb), 0};
+        } else if constexpr (OP == OP_MIN) {
+            return (fb < a.f) ? Acc{fb, b} : a;
+        } else {
+            return (a.f < fb) ? Acc{fb, b} : a;
+        }
+    }
+    template <int OP> __device__ static S finish(Acc a)
+    {
+        if constexpr (OP == OP_SUM || OP == OP_PROD) {
+            return f32_to_bf16(a.f);
+        } else {
+            return a.bits;
+        }
+    }
+    __device__ static S div(Acc a, int np)
+    {
+        return f32_to_bf16(__fdiv_rn(a.f, static_cast<float>(np)));
+    }
+};
+
+template <typename T, int OP>
+__device__ __forceinline__ typename Elt<T>::S finish(typename Elt<T>::Acc a)
+{
+    if constexpr (std::is_same<T, bf16_t>::value) {
+        return Elt<T>::template finish<OP>(a);
+    } else {
+        return Elt<T>::store(a);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Kernel arguments.
+// ---------------------------------------------------------------------------
+constexpr int kMaxInputs = 16;
+
+struct InPtrs {
+    const void *p[kMaxInputs];
+};
+
+// 16-byte vector of storage elements.
+template <typename S> struct Vec {
+    static constexpr int N = 16 / sizeof(S);
+    S e[N];
+};
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// Load policy: LOADNT=1 marks the read streams non-temporal (each byte is read
+// once); chosen by measurement (tools/tune_reduce.py), see DESIGN.md.
+template <typename S, int LOADNT>
+__device__ __forceinline__ Vec<S> ld_vec(const void *base, size_t vi)
+{
+    const u32x4 *p = reinterpret_cast<const u32x4 *>(base) + vi;
+    u32x4 raw;
+    if constexpr (LOADNT) {
+        raw = __builtin_nontemporal_load(p);
+    } else {
+        raw = *p;
+    }
+    Vec<S> v;
+    __builtin_memcpy(&v, &raw, 16);
+    return v;
+}
+
+template <typename S>
+__device__ __forceinline__ void st_vec(void *base, size_t vi, const Vec<S> &v)
+{
+    u32x4 raw;
+    __builtin_memcpy(&raw, &v, 16);
+    u32x4 *p = reinterpret_cast<u32x4 *>(base) + vi;
+    __builtin_nontemporal_store(raw, p);
+}
+
+// Fold one element across the k inputs (runtime k).
+template <typename T, int OP, int EPI>
+__device__ __forceinline__ typename Elt<T>::S
+fold_scalar(const InPtrs &in, int k, size_t i, int np)
+{
+    using S   = typename Elt<T>::S;
+    auto acc  = Elt<T>::load(reinterpret_cast<const S *>(in.p[0])[i]);
+    for (int j = 1; j < k; ++j) {
+        acc = Elt<T>::template combine<OP>(
+            acc, reinterpret_cast<const S *>(in.p[j])[i]);
+    }
+    if constexpr (EPI == EPI_DIV) {
+        return Elt<T>::div(acc, np);
+    } else {
+        return finish<T, OP>(acc);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Main kernel. Elements [0, head) and [head + nvec*V, n) are done one element
+// per thread; [head, head + nvec*V) as 16-B vectors (all pointers offset by
+// `head` elements are 16-B aligned; the host checks this). KC = compile-time
+// input count (2 for the hot path) or 0 = runtime k (pointers are then read
+// from the kernel-argument block with scalar loads, never a local array).
+// ---------------------------------------------------------------------------
+template <typename T, int OP, int EPI, int KC, int BLOCK, int UNROLL, int LOADNT>
+__global__ void __launch_bounds__(BLOCK)
+    reduce_kernel(InPtrs in, int k, void *out, size_t n, size_t head,
+                  size_t nvec, int np)
+{
+    using S         = typename Elt<T>::S;
+    using Acc       = typename Elt<T>::Acc;
+    constexpr int V = Vec<S>::N;
+    const int kk    = KC > 0 ? KC : k;
+
+    // scalar edges: head elements, then the tail after the vector body
+    const size_t tid   = static_cast<size_t>(blockIdx.x) * BLOCK + threadIdx.x;
+    const size_t vend  = head + nvec * V;
+    const size_t nedge = head + (n - vend);
+    if (tid < nedge) {
+        const size_t i = tid < head ? tid : vend + (tid - head);
+        reinterpret_cast<S *>(out)[i] = fold_scalar<T, OP, EPI>(in, kk, i, np);
+    }
+
+    auto src = [&](int j) {
+        return reinterpret_cast<const char *>(in.p[j]) + head * sizeof(S);
+    };
+    char *obase = reinterpret_cast<char *>(out) + head * sizeof(S);
+
+    auto emit = [&](const Acc &a) -> S {
+        if constexpr (EPI == EPI_DIV) {
+            return Elt<T>::div(a, np);
+        } else {
+            return finish<T, OP>(a);
+        }
+    };
+
+    const size_t tile   = static_cast<size_t>(BLOCK) * UNROLL;
+    const size_t ntiles = (nvec + tile - 1) / tile;
+    for (size_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const size_t v0 = t * tile + threadIdx.x;
+        if (v0 + (UNROLL - 1) * BLOCK < nvec) {
+            // full tile: UNROLL loads of inputs 0 and 1 issued before any use
+            Vec<S> a[UNROLL];
+            Vec<S> b[UNROLL];
+            const char *s0 = src(0);
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u) a[u] = ld_vec<S, LOADNT>(s0, v0 + u * BLOCK);
+            if (kk > 1) {
+                const char *s1 = src(1);
+#pragma unroll
+                for (int u = 0; u < UNROLL; ++u) b[u] = ld_vec<S, LOADNT>(s1, v0 + u * BLOCK);
+            }
+            Acc acc[UNROLL][V];
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u) {
+#pragma unroll
+                for (int e = 0; e < V; ++e) {
+                    acc[u][e] = Elt<T>::load(a[u].e[e]);
+                    if (kk > 1) {
+                        acc[u][e] = Elt<T>::template combine<OP>(acc[u][e], b[u].e[e]);
+                    }
+                }
+            }
+            if constexpr (KC != 2) {
+                for (int j = 2; j < kk; ++j) {
+                    const char *sj = src(j);
+#pragma unroll
+                    for (int u = 0; u < UNROLL; ++u) b[u] = ld_vec<S, LOADNT>(sj, v0 + u * BLOCK);
+#pragma unroll
+                    for (int u = 0; u < UNROLL; ++u) {
+#pragma unroll
+                        for (int e = 0; e < V; ++e) {
+                            acc[u][e] = Elt<T>::template combine<OP>(acc[u][e], b[u].e[e]);
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u) {
+                Vec<S> r;
+#pragma unroll
+                for (int e = 0; e < V; ++e) r.e[e] = emit(acc[u][e]);
+                st_vec<S>(obase, v0 + u * BLOCK, r);
+            }
+        } else {
+            // ragged last tile
+            for (int u = 0; u < UNROLL; ++u) {
+                const size_t vi = v0 + u * BLOCK;
+                if (vi >= nvec) break;
+                Vec<S> a = ld_vec<S, LOADNT>(src(0), vi);
+                Acc acc[V];
+#pragma unroll
+                for (int e = 0; e < V; ++e) acc[e] = Elt<T>::load(a.e[e]);
+                for (int j = 1; j < kk; ++j) {
+                    Vec<S> b = ld_vec<S, LOADNT>(src(j), vi);
+#pragma unroll
+                    for (int e = 0; e < V; ++e) {
+                        acc[e] = Elt<T>::template combine<OP>(acc[e], b.e[e]);
+                    }
+                }
+                Vec<S> r;
+#pragma unroll
+                for (int e = 0; e < V; ++e) r.e[e] = emit(acc[e]);
+                st_vec<S>(obase, vi, r);
+            }
+        }
+    }
+}
+
+// Element-at-a-time kernel for inputs whose 16-B alignment residues differ
+// (e.g. host-side chunk slices at odd offsets). Still coalesced per element.
+template <typename T, int OP, int EPI, int BLOCK>
+__global__ void __launch_bounds__(BLOCK)
+    reduce_kernel_unaligned(InPtrs in, int k, void *out, size_t n, int np)
+{
+    using S = typename Elt<T>::S;
+    for (size_t i = static_cast<size_t>(blockIdx.x) * BLOCK + threadIdx.x; i < n;
+         i += static_cast<size_t>(gridDim.x) * BLOCK) {
+        reinterpret_cast<S *>(out)[i] = fold_scalar<T, OP, EPI>(in, k, i, np);
+    }
+}
+
+// SMA blend: v = fl(fl(c1*v) + fl(c2*fl(s/np))) (sma_sgd.py:60-65).
+template <typename T> struct SmaMath;
+template <> struct SmaMath<float> {
+    using S = float;
+    __device__ static S blend(S v, S s, float c1, float c2, int np)
+    {
+        float avg = __fdiv_rn(s, static_cast<float>(np));
+        return __fadd_rn(__fmul_rn(c1, v), __fmul_rn(c2, avg));
+    }
+};
+template <> struct SmaMath<double> {
+    using S = double;
+    __device__ static S blend(S v, S s, double c1, double c2, int np)
+    {
+        double avg = __ddiv_rn(s, static_cast<double>(np));
+        return __dadd_rn(__dmul_rn(c1, v), __dmul_rn(c2, avg));
+    }
+};
+template <> struct SmaMath<f16_t> {
+    using S = uint16_t;
+    __device__ static S blend(S v, S s, float c1, float c2, int np)
+    {
+        float avg = __fdiv_rn(f16_to_f32(s), static_cast<float>(np));
+        return f32_to_f16(__fadd_rn(__fmul_rn(c1, f16_to_f32(v)), __fmul_rn(c2, avg)));
+    }
+};
+template <> struct SmaMath<bf16_t> {
+    using S = uint16_t;
+    __device__ static S blend(S v, S s, float c1, float c2, int np)
+    {
+        float avg = __fdiv_rn(bf16_to_f32(s), static_cast<float>(np));
+        return f32_to_bf16(__fadd_rn(__fmul_rn(c1, bf16_to_f32(v)), __fmul_rn(c2, avg)));
+    }
+};
+
+template <typename T, typename C, int BLOCK, int UNROLL>
+__global__ void __launch_bounds__(BLOCK)
+    sma_kernel(void *v, const void *s, size_t n, size_t head, size_t nvec,
+               C c1, C c2, int np, int vec_ok)
+{
+    using S         = typename SmaMath<T>::S;
+    constexpr int V = Vec<S>::N;
+    S *pv           = reinterpret_cast<S *>(v);
+    const S *ps     = reinterpret_cast<const S *>(s);
+    const size_t tid = static_cast<size_t>(blockIdx.x) * BLOCK + threadIdx.x;
+    if (!vec_ok) {
+        for (size_t i = tid; i < n; i += static_cast<size_t>(gridDim.x) * BLOCK) {
+            pv[i] = SmaMath<T>::blend(pv[i], ps[i], c1, c2, np);
+        }
+        return;
+    }
+    const size_t vend  = head + nvec * V;
+    const size_t nedge = head + (n - vend);
+    if (tid < nedge) {
+        const size_t i = tid < head ? tid : vend + (tid - head);
+        pv[i]          = SmaMath<T>::blend(pv[i], ps[i], c1, c2, np);
+    }
+    char *vb       = reinterpret_cast<char *>(v) + head * sizeof(S);
+    const char *sb = reinterpret_cast<const char *>(s) + head * sizeof(S);
+    const size_t tile   = static_cast<size_t>(BLOCK) * UNROLL;
+    const size_t ntiles = (nvec + tile - 1) / tile;
+    for (size_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const size_t v0 = t * tile + threadIdx.x;
+        Vec<S> a[UNROLL], b[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            if (v0 + u * BLOCK < nvec) a[u] = ld_vec<S, 0>(vb, v0 + u * BLOCK);
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            if (v0 + u * BLOCK < nvec) b[u] = ld_vec<S, 0>(sb, v0 + u * BLOCK);
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            if (v0 + u * BLOCK < nvec) {
+                Vec<S> r;
+#pragma unroll
+                for (int e = 0; e < V; ++e) {
+                    r.e[e] = SmaMath<T>::blend(a[u].e[e], b[u].e[e], c1, c2, np);
+                }
+                st_vec<S>(vb, v0 + u * BLOCK, r);
+            }
+        }
+    }
+}
+
+}  // namespace kf

@@ -1,0 +1,310 @@
+"""GPU parity: the HIP path (through the C-ABI) against the oracle and the
+reference's golden vectors. Integers bit-exact; floats bit-exact where the
+reference is deterministic (any 2-operand op, ring order, fixed fold order),
+NaN-ness equal where payloads may differ (golden_io.same_bits_or_nan)."""
+import zlib
+
+import numpy as np
+import pytest
+
+import golden_io
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda:0")
+
+
+@pytest.fixture(scope="module")
+def lib(dev):
+    from kungfu_amd import _lib
+    l = _lib.load()
+    assert l.kf_device_count() > 0
+    return l
+
+
+@pytest.fixture(scope="module")
+def orc():
+    from oracle import oracle
+    oracle.build()
+    return oracle
+
+
+def to_dev(a, dev):
+    """numpy -> GPU tensor holding the same bytes (unsigned views for u16..)."""
+    a = np.ascontiguousarray(a)
+    t = torch.from_numpy(a.view(np.uint8).copy()).to(dev)
+    return t
+
+
+def from_dev(t, like):
+    return t.cpu().numpy().view(like.dtype).reshape(like.shape)
+
+
+def dev_reduce(lib, arrs, code, op, dev, out_alias=None):
+    from kungfu_amd import _lib
+    ts = [to_dev(a, dev) for a in arrs]
+    out = ts[out_alias] if out_alias is not None else torch.empty_like(ts[0])
+    rc = lib.kf_bucket_reduce(_lib.ptr_array([t.data_ptr() for t in ts]), len(ts),
+                              out.data_ptr(), arrs[0].size, code, op,
+                              torch.cuda.current_stream().cuda_stream)
+    assert rc == 0, lib.kf_last_error()
+    torch.cuda.synchronize()
+    return from_dev(out, arrs[0])
+
+
+# ---- B1: std_transform_2 drop-in against every reference golden vector ----
+
+def test_std_transform_2_golden(lib):
+    n = 0
+    for c, x, y, z in golden_io.stored_cases():
+        xx, yy = x.copy(), y.copy()
+        if c["kind"] == "alias_x":
+            out = xx
+        elif c["kind"] == "alias_y":
+            out = yy
+        else:
+            out = np.empty_like(x)
+        lib.std_transform_2(xx.ctypes.data, yy.ctypes.data, out.ctypes.data,
+                            c["n"], c["code"], c["opcode"])
+        assert golden_io.same_bits_or_nan(out, z), c
+        n += 1
+    assert n > 600
+
+
+def test_std_transform_2_golden_large(lib):
+    for c, x, y in golden_io.large_cases():
+        z = np.empty_like(x)
+        lib.std_transform_2(x.ctypes.data, y.ctypes.data, z.ctypes.data, c["n"],
+                            c["code"], c["opcode"])
+        assert golden_io.sha(z) == c["sha_z"], c
+
+
+def test_float16_sum_entry(lib, orc):
+    rng = np.random.default_rng(3)
+    for n in (1, 5, 8, 13, 100003):
+        x = (rng.standard_normal(n) * 100).astype(np.float16)
+        y = (rng.standard_normal(n) * 100).astype(np.float16)
+        z = np.empty_like(x)
+        lib.float16_sum(z.ctypes.data, x.ctypes.data, y.ctypes.data, n)
+        assert np.array_equal(z.view(np.uint16), orc.transform2(x, y, "f16", "sum").view(np.uint16))
+
+
+def test_base_transform_mirror(lib):
+    # kungfu_amd.base mirrors op.go: Transform2(z, x, y) / Transform(y, x)
+    from kungfu_amd import base
+    x = base.Vector.of(np.array([1.0, 2.0], np.float32))
+    y = base.Vector.of(np.array([2.0, 5.0], np.float32))
+    z = base.Vector.new(2, base.DataType.F32)
+    base.Transform2(z, x, y, base.OP.SUM)
+    assert list(z.Data) == [3.0, 7.0]
+    base.Transform(y, x, base.OP.MAX)
+    assert list(y.Data) == [2.0, 5.0]
+
+
+# ---- B2: device bucket API ------------------------------------------------
+
+INT_DTS = ["u8", "u16", "u32", "u64", "i8", "i16", "i32", "i64"]
+
+
+@pytest.mark.parametrize("dt", INT_DTS + ["f32", "f64", "bf16"])
+@pytest.mark.parametrize("op", ["sum", "min", "max", "prod"])
+def test_device_two_input_vs_oracle(lib, orc, dev, dt, op):
+    from oracle.oracle import DT, NP, OPS
+    rng = np.random.default_rng(zlib.crc32((dt + op).encode()))
+    for n in (1, 3, 17, 4096 + 5, 1 << 20):
+        if dt in INT_DTS:
+            info = np.iinfo(NP[dt])
+            x = rng.integers(info.min, info.max, size=n, dtype=NP[dt], endpoint=True)
+            y = rng.integers(info.min, info.max, size=n, dtype=NP[dt], endpoint=True)
+        elif dt == "bf16":
+            x = orc.f32_to_bf16_bits(rng.standard_normal(n).astype(np.float32))
+            y = orc.f32_to_bf16_bits(rng.standard_normal(n).astype(np.float32))
+        else:
+            x = rng.standard_normal(n).astype(NP[dt])
+            y = rng.standard_normal(n).astype(NP[dt])
+        got = dev_reduce(lib, [x, y], DT[dt], OPS[op], dev)
+        want = orc.transform2(x, y, dt, op)
+        assert golden_io.same_bits_or_nan(got, want), (dt, op, n)
+
+
+def test_device_f16_sum_and_rejects(lib, orc, dev):
+    from kungfu_amd import _lib
+    rng = np.random.default_rng(4)
+    x = (rng.standard_normal(333333) * 1000).astype(np.float16)  # overflows too
+    y = (rng.standard_normal(333333) * 1000).astype(np.float16)
+    got = dev_reduce(lib, [x, y], 0x20208, 0, dev)
+    assert np.array_equal(got.view(np.uint16), orc.transform2(x, y, "f16", "sum").view(np.uint16))
+    t = torch.zeros(16, dtype=torch.float16, device=dev)
+    arr = _lib.ptr_array([t.data_ptr(), t.data_ptr()])
+    for op in (1, 2, 3):  # op.cpp:45-54: fp16 is SUM only
+        assert lib.kf_bucket_reduce(arr, 2, t.data_ptr(), 16, 0x20208, op, None) == 2
+
+
+def test_specials_all_pairs(lib, orc, dev):
+    # every ordered pair of specials, f32/f64 x all ops (NaN, +-0, inf, subnormal)
+    for c, x, y, z in golden_io.stored_cases():
+        if c["kind"] != "special" or c["dtype"] not in ("f32", "f64", "f16", "i32", "i64"):
+            continue
+        got = dev_reduce(lib, [x, y], c["code"], c["opcode"], dev)
+        assert golden_io.same_bits_or_nan(got, z), c
+
+
+def test_denormals_not_flushed(lib, dev):
+    tiny = np.float32(np.finfo(np.float32).tiny)
+    x = np.array([tiny / 4, tiny / 8, -tiny / 2] * 100, np.float32)
+    y = np.array([tiny / 8, 0.0, tiny / 4] * 100, np.float32)
+    got = dev_reduce(lib, [x, y], 0x20408, 0, dev)
+    assert np.array_equal(got, x + y)
+    assert np.all(got[:3] != 0)
+
+
+@pytest.mark.parametrize("k", [3, 4, 5, 8, 16])
+def test_k_input_ring_order_bit_exact(lib, orc, dev, k):
+    # The k-input fused reduce, fed in the reference ring order, reproduces the
+    # reference RING all-reduce of that chunk bit for bit (schedule.py).
+    from oracle import schedule
+    rng = np.random.default_rng(k)
+    n = 262144 + 13
+    xs = [rng.standard_normal(n).astype(np.float32) for _ in range(k)]
+    for r in (0, k - 1):
+        order = schedule.ring_order(k, r)
+        got = dev_reduce(lib, [xs[j] for j in order], 0x20408, 0, dev)
+        want = orc.reduce_k([xs[j] for j in order], "f32", "sum")
+        assert np.array_equal(got, want)
+    # int32 and fp16 (per-hop rounding) chains as well
+    ints = [rng.integers(-2**31, 2**31 - 1, size=n, dtype=np.int32) for _ in range(k)]
+    assert np.array_equal(dev_reduce(lib, ints, 0x10408, 0, dev), orc.reduce_k(ints, "i32"))
+    hs = [(rng.standard_normal(n) * 30).astype(np.float16) for _ in range(k)]
+    assert np.array_equal(dev_reduce(lib, hs, 0x20208, 0, dev).view(np.uint16),
+                          orc.reduce_k(hs, "f16").view(np.uint16))
+    bs = [orc.f32_to_bf16_bits(rng.standard_normal(n).astype(np.float32)) for _ in range(k)]
+    assert np.array_equal(dev_reduce(lib, bs, 0x20209, 0, dev), orc.reduce_k(bs, "bf16"))
+
+
+def test_schedule_all_reduce_matches_device_fold(lib, orc, dev):
+    # Whole reference schedule (RING, np=4, 4 MiB bucket = 4 chunks with
+    # hash-chosen roots): per chunk, the device fold in that chunk's ring order
+    # equals what every rank holds after the reference all-reduce.
+    from oracle import schedule
+    rng = np.random.default_rng(11)
+    k, n = 4, 1 << 20
+    xs = [rng.standard_normal(n).astype(np.float32) for _ in range(k)]
+    ref = schedule.all_reduce(xs, "f32", "sum", strategy="RING")
+    for b, e, r in schedule.chunk_roots(n, 4, k, strategy="RING"):
+        order = schedule.ring_order(k, r)
+        got = dev_reduce(lib, [xs[j][b:e].copy() for j in order], 0x20408, 0, dev)
+        assert np.array_equal(got, ref[0][b:e])
+
+
+def test_alignment_and_aliasing(lib, orc, dev):
+    from kungfu_amd import _lib
+    rng = np.random.default_rng(12)
+    n = 100000
+    x = rng.standard_normal(n + 8).astype(np.float32)
+    y = rng.standard_normal(n + 8).astype(np.float32)
+    tx, ty = torch.from_numpy(x).to(dev), torch.from_numpy(y).to(dev)
+    s = torch.cuda.current_stream().cuda_stream
+    for ox, oy, oz in ((1, 1, 1), (1, 2, 3), (3, 0, 0), (0, 0, 2), (2, 2, 2)):
+        out = torch.zeros(n + 8, dtype=torch.float32, device=dev)
+        ptrs = _lib.ptr_array([tx.data_ptr() + 4 * ox, ty.data_ptr() + 4 * oy])
+        assert lib.kf_bucket_reduce(ptrs, 2, out.data_ptr() + 4 * oz, n, 0x20408, 0, s) == 0
+        torch.cuda.synchronize()
+        got = out.cpu().numpy()[oz:oz + n]
+        assert np.array_equal(got, x[ox:ox + n] + y[oy:oy + n]), (ox, oy, oz)
+        assert np.all(out.cpu().numpy()[:oz] == 0) and np.all(out.cpu().numpy()[oz + n:] == 0)
+    # in place: out aliases input 0 and input 1
+    for alias in (0, 1):
+        got = dev_reduce(lib, [x[:n], y[:n]], 0x20408, 0, dev, out_alias=alias)
+        assert np.array_equal(got, x[:n] + y[:n])
+
+
+def test_k1_copy_and_empty(lib, dev):
+    from kungfu_amd import _lib
+    t = torch.arange(1000, dtype=torch.float32, device=dev)
+    o = torch.zeros_like(t)
+    s = torch.cuda.current_stream().cuda_stream
+    assert lib.kf_bucket_reduce(_lib.ptr_array([t.data_ptr()]), 1, o.data_ptr(), 1000,
+                                0x20408, 0, s) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(o, t)
+    assert lib.kf_bucket_reduce(_lib.ptr_array([t.data_ptr()] * 2), 2, o.data_ptr(), 0,
+                                0x20408, 0, s) == 0
+
+
+# ---- fused S-SGD / SMA epilogues -------------------------------------------
+
+@pytest.mark.parametrize("np_", [1, 2, 3, 4, 7, 8])
+@pytest.mark.parametrize("dt", ["f32", "f64", "f16", "bf16"])
+def test_avg_epilogue(orc, dev, np_, dt):
+    from kungfu_amd import ops
+    rng = np.random.default_rng(np_ * 7)
+    n = 300001
+    tdt = {"f32": torch.float32, "f64": torch.float64, "f16": torch.float16,
+           "bf16": torch.bfloat16}[dt]
+    if dt == "bf16":
+        xs = [orc.f32_to_bf16_bits(rng.standard_normal(n).astype(np.float32)) for _ in range(np_)]
+    else:
+        xs = [rng.standard_normal(n).astype(orc.NP[dt]) for _ in range(np_)]
+    ts = [torch.from_numpy(x.view(np.int16) if x.itemsize == 2 else x).to(dev).view(tdt) for x in xs]
+    out = ops.bucket_reduce_avg(ts, np_)
+    torch.cuda.synchronize()
+    got = out.cpu().view(torch.int16 if out.element_size() == 2 else out.dtype).numpy()
+    want = orc.reduce_avg(xs, dt, np_)
+    assert np.array_equal(got.view(np.uint8), want.view(np.uint8))
+    # reduce-then-divide done in two steps (RS -> div -> AG) gives the same bits
+    if dt in ("f32", "f64"):
+        s = ops.bucket_reduce(ts, op="sum")
+        ops.bucket_div_(s, np_)
+        torch.cuda.synchronize()
+        assert np.array_equal(s.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("dt", ["f32", "f64", "f16", "bf16"])
+def test_sma_blend(orc, dev, dt):
+    from kungfu_amd import ops
+    rng = np.random.default_rng(13)
+    n = 250007
+    tdt = {"f32": torch.float32, "f64": torch.float64, "f16": torch.float16,
+           "bf16": torch.bfloat16}[dt]
+    if dt == "bf16":
+        v = orc.f32_to_bf16_bits(rng.standard_normal(n).astype(np.float32))
+        s = orc.f32_to_bf16_bits(rng.standard_normal(n).astype(np.float32) * 4)
+    else:
+        v = rng.standard_normal(n).astype(orc.NP[dt])
+        s = (rng.standard_normal(n) * 4).astype(orc.NP[dt])
+    view = lambda a: a.view(np.int16) if a.itemsize == 2 else a  # noqa: E731
+    tv = torch.from_numpy(view(v).copy()).to(dev).view(tdt)
+    ts = torch.from_numpy(view(s).copy()).to(dev).view(tdt)
+    for np_, alpha in ((4, 0.1), (3, 0.25), (8, 0.1)):
+        want = orc.sma_blend(view(v).copy(), view(s), dt, np_, alpha)
+        tv2 = tv.clone()
+        ops.sma_blend_(tv2, ts, np_, alpha)
+        torch.cuda.synchronize()
+        got = tv2.cpu().view(torch.int16 if tv2.element_size() == 2 else tv2.dtype).numpy()
+        assert np.array_equal(got.view(np.uint8), want.view(np.uint8)), (np_, alpha)
+
+
+# ---- full BASELINE size (C2: 256 MiB fp32) ---------------------------------
+
+def test_c2_full_size_bit_exact(lib, orc, dev):
+    from kungfu_amd import ops
+    n = 64 << 20  # 67,108,864 fp32 = 256 MiB per input
+    g0 = torch.Generator(device=dev).manual_seed(0)
+    g1 = torch.Generator(device=dev).manual_seed(1)
+    x = torch.randn(n, device=dev, generator=g0)
+    y = torch.randn(n, device=dev, generator=g1)
+    z = ops.bucket_reduce([x, y])
+    torch.cuda.synchronize()
+    xh, yh, zh = x.cpu().numpy(), y.cpu().numpy(), z.cpu().numpy()
+    assert np.array_equal(zh, orc.transform2(xh, yh, "f32", "sum"))
+    # size-independent property: in-place repeat is idempotent on the copy
+    z2 = ops.bucket_reduce([x, y], out=x)  # out aliases input 0
+    torch.cuda.synchronize()
+    assert torch.equal(z2, z)
