@@ -130,6 +130,11 @@ const char *kf_version(void);
 /* Last HIP error string recorded by the library on this thread. */
 const char *kf_last_error(void);
 
+/* Tuning hook (tools/tune_reduce.py only): launch geometry of the fp32 SUM
+ * 2-input path — unroll in {1,2,4,8} vectors per thread, grid cap in blocks,
+ * non-temporal loads, plain stores. Not thread-safe; call before launching. */
+int kf_set_geometry(int unroll, int grid_cap, int loadnt, int stplain);
+
 /* Host-staged variant of std_transform_2 with an explicit chunked pipeline:
  * pageable host x,y -> pinned staging -> HBM -> kernel -> host out, double
  * buffered over two HIP streams. Returns KF_Status. Used by the copy-inclusive

@@ -23,6 +23,7 @@ EXPORTED = (
     "kf_version",
     "kf_last_error",
     "kf_transform2_host",
+    "kf_set_geometry",
 )
 
 STATUS = {
@@ -86,6 +87,8 @@ def load():
     lib.kf_transform2_host.argtypes = [c_void_p, c_void_p, c_void_p, c_size_t,
                                        c_int, c_int]
     lib.kf_transform2_host.restype = c_int
+    lib.kf_set_geometry.argtypes = [c_int, c_int, c_int, c_int]
+    lib.kf_set_geometry.restype = c_int
     _lib = lib
     return lib
 

@@ -28,27 +28,19 @@ using namespace kf;
 
 constexpr int kBlock = 256;
 
-// Launch geometry for the streaming body. Tuned on MI355X with
-// tools/tune_reduce.py (DESIGN.md "Kernel tuning"); env overrides exist only
-// for that tuning script.
+// Launch geometry for the streaming body. Defaults tuned on MI355X with
+// tools/tune_reduce.py (DESIGN.md "Kernel tuning"); kf_set_geometry() exists
+// only for that tuning script.
 struct Geometry {
     int unroll   = 4;     // 16-B vectors per thread per input per tile
     int grid_cap = 4096;  // blocks; grid-stride beyond
     int loadnt   = 0;     // non-temporal read streams
+    int stplain  = 0;     // plain (not non-temporal) stores
 };
 
 Geometry &geometry()
 {
-    static Geometry g = [] {
-        Geometry g;
-        if (const char *s = std::getenv("KF_UNROLL")) g.unroll = std::atoi(s);
-        if (const char *s = std::getenv("KF_GRID_CAP")) g.grid_cap = std::atoi(s);
-        if (const char *s = std::getenv("KF_LOADNT")) g.loadnt = std::atoi(s);
-        if (g.unroll != 2 && g.unroll != 4 && g.unroll != 8) g.unroll = 4;
-        if (g.grid_cap < 1) g.grid_cap = 4096;
-        g.loadnt = g.loadnt ? 1 : 0;
-        return g;
-    }();
+    static Geometry g;
     return g;
 }
 
@@ -123,15 +115,29 @@ unsigned grid_for(size_t nvec, size_t nedge, int unroll)
     return static_cast<unsigned>(blocks);
 }
 
-template <typename T, int OP, int EPI, int KC, int UNROLL, int LOADNT>
+template <typename T, int OP, int EPI, int KC, int UNROLL, int LOADNT, int STPLAIN = 0>
 void launch_vec(const InPtrs &ptrs, int k, void *out, size_t n, const Plan &p,
                 int np, hipStream_t s)
 {
     constexpr int V  = Vec<typename Elt<T>::S>::N;
     const size_t ned = p.head + (n - p.head - p.nvec * V);
     const unsigned g = grid_for(p.nvec, ned, UNROLL);
-    reduce_kernel<T, OP, EPI, KC, kBlock, UNROLL, LOADNT>
+    reduce_kernel<T, OP, EPI, KC, kBlock, UNROLL, LOADNT, STPLAIN>
         <<<g, kBlock, 0, s>>>(ptrs, k, out, n, p.head, p.nvec, np);
+}
+
+// The tuned fp32 2-input SUM (the headline path) carries every geometry
+// variant; every other combination uses unroll 4 with the default policies.
+template <typename T, int OP, int EPI, int KC, int LOADNT, int STPLAIN>
+void launch_unroll(const InPtrs &ptrs, int k, void *out, size_t n, const Plan &p,
+                   int np, hipStream_t s)
+{
+    switch (geometry().unroll) {
+    case 1: return launch_vec<T, OP, EPI, KC, 1, LOADNT, STPLAIN>(ptrs, k, out, n, p, np, s);
+    case 2: return launch_vec<T, OP, EPI, KC, 2, LOADNT, STPLAIN>(ptrs, k, out, n, p, np, s);
+    case 8: return launch_vec<T, OP, EPI, KC, 8, LOADNT, STPLAIN>(ptrs, k, out, n, p, np, s);
+    default: return launch_vec<T, OP, EPI, KC, 4, LOADNT, STPLAIN>(ptrs, k, out, n, p, np, s);
+    }
 }
 
 template <typename T, int OP, int EPI, int KC>
@@ -139,21 +145,12 @@ void launch_geom(const InPtrs &ptrs, int k, void *out, size_t n, const Plan &p,
                  int np, hipStream_t s)
 {
     const Geometry &g = geometry();
-    // The tuned fp32 2-input SUM (the headline path) carries every geometry
-    // variant; every other combination uses the default unroll 4.
-    if constexpr (std::is_same<T, float>::value && OP == OP_SUM && KC == 2) {
-        if (g.loadnt) {
-            switch (g.unroll) {
-            case 2: return launch_vec<T, OP, EPI, KC, 2, 1>(ptrs, k, out, n, p, np, s);
-            case 8: return launch_vec<T, OP, EPI, KC, 8, 1>(ptrs, k, out, n, p, np, s);
-            default: return launch_vec<T, OP, EPI, KC, 4, 1>(ptrs, k, out, n, p, np, s);
-            }
-        }
-        switch (g.unroll) {
-        case 2: return launch_vec<T, OP, EPI, KC, 2, 0>(ptrs, k, out, n, p, np, s);
-        case 8: return launch_vec<T, OP, EPI, KC, 8, 0>(ptrs, k, out, n, p, np, s);
-        default: break;
-        }
+    if constexpr (std::is_same<T, float>::value && OP == OP_SUM && KC == 2 &&
+                  EPI == EPI_NONE) {
+        if (g.loadnt && g.stplain) return launch_unroll<T, OP, EPI, KC, 1, 1>(ptrs, k, out, n, p, np, s);
+        if (g.loadnt) return launch_unroll<T, OP, EPI, KC, 1, 0>(ptrs, k, out, n, p, np, s);
+        if (g.stplain) return launch_unroll<T, OP, EPI, KC, 0, 1>(ptrs, k, out, n, p, np, s);
+        return launch_unroll<T, OP, EPI, KC, 0, 0>(ptrs, k, out, n, p, np, s);
     }
     launch_vec<T, OP, EPI, KC, 4, 0>(ptrs, k, out, n, p, np, s);
 }
@@ -429,6 +426,18 @@ int kf_sma_blend(void *v, const void *sum, size_t n, KungFu_Datatype dt, int np,
     case KungFu_BFLOAT16: return launch_sma<bf16_t, float>(v, sum, n, np, c1f, c2f, s);
     default: return KF_ERR_DTYPE;
     }
+}
+
+int kf_set_geometry(int unroll, int grid_cap, int loadnt, int stplain)
+{
+    if (unroll != 1 && unroll != 2 && unroll != 4 && unroll != 8) return KF_ERR_ARG;
+    if (grid_cap < 1) return KF_ERR_ARG;
+    Geometry &g = geometry();
+    g.unroll    = unroll;
+    g.grid_cap  = grid_cap;
+    g.loadnt    = loadnt ? 1 : 0;
+    g.stplain   = stplain ? 1 : 0;
+    return KF_OK;
 }
 
 int kf_device_count(void)

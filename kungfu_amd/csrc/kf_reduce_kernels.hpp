@@ -251,13 +251,19 @@ __device__ __forceinline__ Vec<S> ld_vec(const void *base, size_t vi)
     return v;
 }
 
-template <typename S>
+// Store policy: STPLAIN=0 (default) writes non-temporally — the output is not
+// re-read by this kernel; STPLAIN=1 uses plain stores (tuning variant).
+template <typename S, int STPLAIN = 0>
 __device__ __forceinline__ void st_vec(void *base, size_t vi, const Vec<S> &v)
 {
     u32x4 raw;
     __builtin_memcpy(&raw, &v, 16);
     u32x4 *p = reinterpret_cast<u32x4 *>(base) + vi;
-    __builtin_nontemporal_store(raw, p);
+    if constexpr (STPLAIN) {
+        *p = raw;
+    } else {
+        __builtin_nontemporal_store(raw, p);
+    }
 }
 
 // Fold one element across the k inputs (runtime k).
@@ -285,7 +291,8 @@ fold_scalar(const InPtrs &in, int k, size_t i, int np)
 // input count (2 for the hot path) or 0 = runtime k (pointers are then read
 // from the kernel-argument block with scalar loads, never a local array).
 // ---------------------------------------------------------------------------
-template <typename T, int OP, int EPI, int KC, int BLOCK, int UNROLL, int LOADNT>
+template <typename T, int OP, int EPI, int KC, int BLOCK, int UNROLL, int LOADNT,
+          int STPLAIN = 0>
 __global__ void __launch_bounds__(BLOCK)
     reduce_kernel(InPtrs in, int k, void *out, size_t n, size_t head,
                   size_t nvec, int np)
@@ -363,7 +370,7 @@ __global__ void __launch_bounds__(BLOCK)
                 Vec<S> r;
 #pragma unroll
                 for (int e = 0; e < V; ++e) r.e[e] = emit(acc[u][e]);
-                st_vec<S>(obase, v0 + u * BLOCK, r);
+                st_vec<S, STPLAIN>(obase, v0 + u * BLOCK, r);
             }
         } else {
             // ragged last tile
@@ -384,7 +391,7 @@ __global__ void __launch_bounds__(BLOCK)
                 Vec<S> r;
 #pragma unroll
                 for (int e = 0; e < V; ++e) r.e[e] = emit(acc[e]);
-                st_vec<S>(obase, vi, r);
+                st_vec<S, STPLAIN>(obase, vi, r);
             }
         }
     }
