@@ -31,11 +31,15 @@ constexpr int kBlock = 256;
 // Launch geometry for the streaming body. Defaults tuned on MI355X with
 // tools/tune_reduce.py (DESIGN.md "Kernel tuning"); kf_set_geometry() exists
 // only for that tuning script.
+// Measured (profiles/r01/tune_c2.jsonl, 256 MiB fp32, 96 variants x 5 rounds):
+// non-temporal loads + non-temporal stores, ONE 16-B vector per thread and a
+// grid of one block per 256 vectors (no grid-stride) is fastest: 114.6 us =
+// 7.03 TB/s; the previous unroll-4 / 4096-block default ran 134 us.
 struct Geometry {
-    int unroll   = 4;     // 16-B vectors per thread per input per tile
-    int grid_cap = 4096;  // blocks; grid-stride beyond
-    int loadnt   = 0;     // non-temporal read streams
-    int stplain  = 0;     // plain (not non-temporal) stores
+    int unroll   = 1;        // 16-B vectors per thread per input per tile
+    int grid_cap = 1 << 20;  // blocks; grid-stride beyond (8 GiB fp32 buckets)
+    int loadnt   = 1;        // non-temporal read streams
+    int stplain  = 0;        // plain (not non-temporal) stores
 };
 
 Geometry &geometry()
@@ -127,7 +131,8 @@ void launch_vec(const InPtrs &ptrs, int k, void *out, size_t n, const Plan &p,
 }
 
 // The tuned fp32 2-input SUM (the headline path) carries every geometry
-// variant; every other combination uses unroll 4 with the default policies.
+// variant; every other combination uses the tuned default (unroll 1,
+// non-temporal loads and stores).
 template <typename T, int OP, int EPI, int KC, int LOADNT, int STPLAIN>
 void launch_unroll(const InPtrs &ptrs, int k, void *out, size_t n, const Plan &p,
                    int np, hipStream_t s)
@@ -152,7 +157,7 @@ void launch_geom(const InPtrs &ptrs, int k, void *out, size_t n, const Plan &p,
         if (g.stplain) return launch_unroll<T, OP, EPI, KC, 0, 1>(ptrs, k, out, n, p, np, s);
         return launch_unroll<T, OP, EPI, KC, 0, 0>(ptrs, k, out, n, p, np, s);
     }
-    launch_vec<T, OP, EPI, KC, 4, 0>(ptrs, k, out, n, p, np, s);
+    launch_vec<T, OP, EPI, KC, 1, 1>(ptrs, k, out, n, p, np, s);
 }
 
 template <typename T, int OP, int EPI>
@@ -255,12 +260,12 @@ int launch_sma(void *v, const void *sum, size_t n, int np, C c1, C c2,
     size_t blocks;
     if (p.vec_ok) {
         const size_t ned = p.head + (n - p.head - p.nvec * V);
-        blocks           = grid_for(p.nvec, ned, 4);
+        blocks           = grid_for(p.nvec, ned, 1);
     } else {
         blocks = (n + kBlock - 1) / kBlock;
         if (blocks > 8192) blocks = 8192;
     }
-    sma_kernel<T, C, kBlock, 4><<<static_cast<unsigned>(blocks), kBlock, 0, s>>>(
+    sma_kernel<T, C, kBlock, 1><<<static_cast<unsigned>(blocks), kBlock, 0, s>>>(
         v, sum, n, p.head, p.nvec, c1, c2, np, p.vec_ok ? 1 : 0);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "sma kernel launch");

@@ -6,12 +6,12 @@
 // What matters on MI355X is keeping enough 16-byte loads in flight per CU:
 //   * every lane moves whole 16-B vectors (global_load_dwordx4 /
 //     global_store_dwordx4): 1 KiB per wave-instruction, fully coalesced;
+//   * loads AND stores are non-temporal: every byte is touched exactly once, so
+//     nothing is worth keeping in L2 / Infinity Cache;
 //   * each thread issues UNROLL independent vector loads per input before the
-//     first use, so a 256-thread block has UNROLL*4 KiB per input in flight;
-//   * the grid is persistent-ish (capped, grid-stride over tiles) so 256 CUs
-//     stay busy without a 16k-block launch tail;
-//   * stores are non-temporal: the output is not re-read by this kernel and
-//     keeping it out of L2 leaves room for the read streams.
+//     first use; measured best is UNROLL = 1 with one block per 256 vectors
+//     (a 65,536-block grid for the 256 MiB bucket): occupancy, not per-thread
+//     ILP, keeps the 256 CUs' memory queues full (DESIGN.md "Kernel tuning").
 //
 // Numerics follow the reference's host reduce (op.cpp:22-54, f16.c:16-50):
 //   SUM/PROD on integers wrap (done in the unsigned type of the same width),
@@ -476,11 +476,11 @@ __global__ void __launch_bounds__(BLOCK)
         Vec<S> a[UNROLL], b[UNROLL];
 #pragma unroll
         for (int u = 0; u < UNROLL; ++u) {
-            if (v0 + u * BLOCK < nvec) a[u] = ld_vec<S, 0>(vb, v0 + u * BLOCK);
+            if (v0 + u * BLOCK < nvec) a[u] = ld_vec<S, 1>(vb, v0 + u * BLOCK);
         }
 #pragma unroll
         for (int u = 0; u < UNROLL; ++u) {
-            if (v0 + u * BLOCK < nvec) b[u] = ld_vec<S, 0>(sb, v0 + u * BLOCK);
+            if (v0 + u * BLOCK < nvec) b[u] = ld_vec<S, 1>(sb, v0 + u * BLOCK);
         }
 #pragma unroll
         for (int u = 0; u < UNROLL; ++u) {
