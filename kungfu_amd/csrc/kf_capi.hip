@@ -31,12 +31,14 @@ constexpr int kBlock = 256;
 // Launch geometry for the streaming body. Defaults tuned on MI355X with
 // tools/tune_reduce.py (DESIGN.md "Kernel tuning"); kf_set_geometry() exists
 // only for that tuning script.
-// Measured (profiles/r01/tune_c2.jsonl, 256 MiB fp32, 96 variants x 5 rounds):
-// non-temporal loads + non-temporal stores, ONE 16-B vector per thread and a
-// grid of one block per 256 vectors (no grid-stride) is fastest: 114.6 us =
-// 7.03 TB/s; the previous unroll-4 / 4096-block default ran 134 us.
+// Measured on MI355X (profiles/r01/tune_c2_rot3.jsonl: 256 MiB fp32, launches
+// cycling over 3 independent bucket sets so no output is still in the 256 MiB
+// Infinity Cache; 5 rounds interleaved in one process): non-temporal loads and
+// stores, 4 vectors per thread, one block per tile (no grid-stride) is
+// fastest at 122.0 us = 6.60 TB/s. With the same buffers every launch
+// (profiles/r01/tune_c2.jsonl) it runs 116.9 us, within 2% of the best there.
 struct Geometry {
-    int unroll   = 1;        // 16-B vectors per thread per input per tile
+    int unroll   = 4;        // 16-B vectors per thread per input per tile
     int grid_cap = 1 << 20;  // blocks; grid-stride beyond (8 GiB fp32 buckets)
     int loadnt   = 1;        // non-temporal read streams
     int stplain  = 0;        // plain (not non-temporal) stores
@@ -131,7 +133,7 @@ void launch_vec(const InPtrs &ptrs, int k, void *out, size_t n, const Plan &p,
 }
 
 // The tuned fp32 2-input SUM (the headline path) carries every geometry
-// variant; every other combination uses the tuned default (unroll 1,
+// variant; every other combination uses the tuned default (unroll 4,
 // non-temporal loads and stores).
 template <typename T, int OP, int EPI, int KC, int LOADNT, int STPLAIN>
 void launch_unroll(const InPtrs &ptrs, int k, void *out, size_t n, const Plan &p,
@@ -157,7 +159,7 @@ void launch_geom(const InPtrs &ptrs, int k, void *out, size_t n, const Plan &p,
         if (g.stplain) return launch_unroll<T, OP, EPI, KC, 0, 1>(ptrs, k, out, n, p, np, s);
         return launch_unroll<T, OP, EPI, KC, 0, 0>(ptrs, k, out, n, p, np, s);
     }
-    launch_vec<T, OP, EPI, KC, 1, 1>(ptrs, k, out, n, p, np, s);
+    launch_vec<T, OP, EPI, KC, 4, 1>(ptrs, k, out, n, p, np, s);
 }
 
 template <typename T, int OP, int EPI>
@@ -260,12 +262,12 @@ int launch_sma(void *v, const void *sum, size_t n, int np, C c1, C c2,
     size_t blocks;
     if (p.vec_ok) {
         const size_t ned = p.head + (n - p.head - p.nvec * V);
-        blocks           = grid_for(p.nvec, ned, 1);
+        blocks           = grid_for(p.nvec, ned, 4);
     } else {
         blocks = (n + kBlock - 1) / kBlock;
         if (blocks > 8192) blocks = 8192;
     }
-    sma_kernel<T, C, kBlock, 1><<<static_cast<unsigned>(blocks), kBlock, 0, s>>>(
+    sma_kernel<T, C, kBlock, 4><<<static_cast<unsigned>(blocks), kBlock, 0, s>>>(
         v, sum, n, p.head, p.nvec, c1, c2, np, p.vec_ok ? 1 : 0);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "sma kernel launch");

@@ -8,10 +8,10 @@
 //     global_store_dwordx4): 1 KiB per wave-instruction, fully coalesced;
 //   * loads AND stores are non-temporal: every byte is touched exactly once, so
 //     nothing is worth keeping in L2 / Infinity Cache;
-//   * each thread issues UNROLL independent vector loads per input before the
-//     first use; measured best is UNROLL = 1 with one block per 256 vectors
-//     (a 65,536-block grid for the 256 MiB bucket): occupancy, not per-thread
-//     ILP, keeps the 256 CUs' memory queues full (DESIGN.md "Kernel tuning").
+//   * each thread issues UNROLL = 4 independent vector loads per input before
+//     the first use, and the grid has one 256-thread block per tile of 1024
+//     vectors (16,384 blocks for the 256 MiB bucket, no grid-stride), so every
+//     CU holds 8 blocks x 32 KiB of loads in flight (DESIGN.md "Kernel tuning").
 //
 // Numerics follow the reference's host reduce (op.cpp:22-54, f16.c:16-50):
 //   SUM/PROD on integers wrap (done in the unsigned type of the same width),

@@ -29,18 +29,22 @@ def main():
     ap.add_argument("--grid", default="1024,2048,4096,8192,16384,65536")
     ap.add_argument("--loadnt", default="0,1")
     ap.add_argument("--stplain", default="0,1")
+    ap.add_argument("--rotate", type=int, default=3,
+                    help="cycle launches over this many independent (x,y,z) sets "
+                         "so no launch finds its buffers in the 256 MiB Infinity Cache")
     args = ap.parse_args()
 
     from kungfu_amd import _lib
     lib = _lib.load()
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
-    x = torch.randn(args.elems, device=dev, generator=g)
-    y = torch.randn(args.elems, device=dev, generator=g)
-    z = torch.empty_like(x)
-    want = x + y
+    sets = []
+    for _ in range(args.rotate):
+        x = torch.randn(args.elems, device=dev, generator=g)
+        y = torch.randn(args.elems, device=dev, generator=g)
+        z = torch.empty_like(x)
+        sets.append((_lib.ptr_array([x.data_ptr(), y.data_ptr()]), z, x, y))
     s = torch.cuda.current_stream()
-    ptrs = _lib.ptr_array([x.data_ptr(), y.data_ptr()])
     ints = lambda v: [int(t) for t in v.split(",")]  # noqa: E731
     variants = list(itertools.product(ints(args.unroll), ints(args.grid),
                                       ints(args.loadnt), ints(args.stplain)))
@@ -49,18 +53,21 @@ def main():
     for r in range(args.rounds):
         for v in variants:
             _lib.check(lib.kf_set_geometry(*v), "kf_set_geometry")
-            for _ in range(3):
-                lib.kf_bucket_reduce(ptrs, 2, z.data_ptr(), z.numel(), 0x20408, 0, s.cuda_stream)
+            for i in range(3):
+                p, z, _, _ = sets[i % len(sets)]
+                lib.kf_bucket_reduce(p, 2, z.data_ptr(), z.numel(), 0x20408, 0, s.cuda_stream)
             e0.record(s)
-            for _ in range(args.launches):
-                lib.kf_bucket_reduce(ptrs, 2, z.data_ptr(), z.numel(), 0x20408, 0, s.cuda_stream)
+            for i in range(args.launches):
+                p, z, _, _ = sets[i % len(sets)]
+                lib.kf_bucket_reduce(p, 2, z.data_ptr(), z.numel(), 0x20408, 0, s.cuda_stream)
             e1.record(s)
             torch.cuda.synchronize()
             samples[v].append(e0.elapsed_time(e1) * 1e3 / args.launches)
             if r == 0:
-                assert torch.equal(z, want), v
-                z.zero_()
-    bytes_ = 3 * x.numel() * 4
+                for _, z, x, y in sets:
+                    assert torch.equal(z, x + y), v
+                    z.zero_()
+    bytes_ = 3 * args.elems * 4
     rows = []
     for v, ts in samples.items():
         med = statistics.median(ts)
