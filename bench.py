@@ -10,9 +10,10 @@ reduce z = x + y over a device-resident 256 MiB fp32 bucket (67,108,864
 elements; the reference's recvOnto step, session.go:255-264, at bucket
 granularity). value = bucket GiB/s = S / t.
 
-N > 1: one step = the S-SGD all-reduce of a 256 MiB fp32 gradient bucket per
-rank: RCCL reduce-scatter(sum) -> HIP /np epilogue on the shard -> RCCL
-all-gather over xGMI (kungfu_amd.collective). Per-GPU work is fixed
+N > 1 (configs[2], C3 geometry): one step = the S-SGD all-reduce of 64 x 4 MiB
+fp32 gradient buckets (256 MiB) per rank: per bucket RCCL reduce-scatter(sum)
+-> HIP /np epilogue on the shard -> RCCL all-gather over xGMI, buckets
+pipelined (kungfu_amd.collective). Per-GPU work is fixed
 (scaling "weak"); value = N * S / t (whole job). The local-reduce kernel is
 also timed on every rank so the roofline object always describes the HIP
 reduce kernel.
@@ -55,8 +56,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--elems", type=int, default=BUCKET_ELEMS)
-    ap.add_argument("--buckets", type=int, default=4,
-                    help="N>1: split the bucket into this many pipelined buckets")
+    ap.add_argument("--buckets", type=int, default=64,
+                    help="N>1: the 256 MiB gradient set as this many pipelined "
+                         "buckets (64 x 4 MiB = BASELINE.json configs[2], C3)")
     ap.add_argument("--rotate", type=int, default=3,
                     help="independent bucket sets cycled by the timed launches, so "
                          "no launch finds its 256 MiB output still in the 256 MiB "
@@ -225,6 +227,22 @@ def main():
         pieces = [gb.buckets[0][b:e] for b, e in
                   _even_aligned(gb.buckets[0].numel(), args.buckets, world)]
         gb.buckets[0].copy_(torch.cat([x, torch.zeros(gb.buckets[0].numel() - n, device=dev)]))
+        # correctness of the timed path before timing it: every rank's x is
+        # regenerated from its seed and reduced locally by the HIP k-input
+        # fold (rank order) -> must match the RCCL result (bit-exact at N=2)
+        from kungfu_amd import ops
+        ex.all_reduce_(pieces, average=True)
+        allx = [torch.randn(n, device=dev, generator=torch.Generator(device=dev).manual_seed(2 * r))
+                for r in range(world)]
+        want = ops.bucket_reduce_avg(allx, world)
+        got = gb.buckets[0][:n]
+        if world == 2:
+            assert torch.equal(got, want), "N=2 all-reduce not bit-exact"
+        else:
+            bound = (world - 1) * 2.0 ** -24 * sum(a.abs() for a in allx) / world + 1e-30
+            assert bool(((got - want).abs() <= 2 * bound).all()), "all-reduce out of bound"
+        del allx, want
+        gb.buckets[0][:n].copy_(x)
         for _ in range(args.warmup):
             ex.all_reduce_(pieces, average=True)
         torch.cuda.synchronize()
@@ -248,8 +266,8 @@ def main():
             "frac_of_xgmi": round(busbw / (153.0 * (world - 1)), 4),
             "buckets": args.buckets,
         }
-        workload = ("S-SGD all-reduce of a 256 MiB fp32 bucket per rank: RCCL "
-                    "reduce-scatter -> HIP /np -> RCCL all-gather")
+        workload = ("C3: S-SGD all-reduce of %d fp32 buckets (256 MiB) per rank: "
+                    "RCCL reduce-scatter -> HIP /np -> RCCL all-gather" % len(pieces))
         parallelism = "dp%d" % world
         kt = torch.tensor([kernel_s], dtype=torch.float64, device=dev)
         dist.all_reduce(kt, op=dist.ReduceOp.MAX)

@@ -135,10 +135,10 @@ const char *kf_last_error(void);
  * non-temporal loads, plain stores. Not thread-safe; call before launching. */
 int kf_set_geometry(int unroll, int grid_cap, int loadnt, int stplain);
 
-/* Host-staged variant of std_transform_2 with an explicit chunked pipeline:
- * pageable host x,y -> pinned staging -> HBM -> kernel -> host out, double
- * buffered over two HIP streams. Returns KF_Status. Used by the copy-inclusive
- * measurement. */
+/* Host-pointer reduce with a status code instead of exit(): the path
+ * std_transform_2 takes (pageable host x,y -> HBM -> HIP kernel -> host out,
+ * synchronous, per-thread stream and device scratch). Used by the
+ * copy-inclusive measurement (bench.py host_staged). */
 int kf_transform2_host(const void *x, const void *y, void *out, size_t n,
                        KungFu_Datatype dt, KungFu_Op op);
 

@@ -1,0 +1,123 @@
+"""Synchronous data-parallel optimizers whose gradient/variable reduction runs on
+the MI355X bucket path (RCCL reduce-scatter + HIP epilogue + RCCL all-gather).
+
+Operator surface kept from the reference:
+
+* ``SynchronousSGDOptimizer(optimizer, named_parameters=None, op=None, ...)``
+  — torch signature of srcs/python/kungfu/torch/optimizers/sync_sgd.py:31-34
+  (wraps an optimizer instance, reduces every gradient in ``step()``). The
+  arithmetic is that of the TF S-SGD (sync_sgd.py:78-109): all-reduce-sum of
+  each gradient, then ``g / np`` — here fused into the shard epilogue and
+  bit-exact against "sum, then divide". ``average=False`` gives the torch
+  reference's sum-only behaviour (torch/optimizers/sync_sgd.py:12-22).
+* ``SynchronousAveragingOptimizer(optimizer, named_parameters=None, alpha=0.1)``
+  — SMA (sma_sgd.py:9-74): before the local update every variable with a
+  gradient becomes ``(1 - alpha) * v + alpha * allreduce_sum(v) / np``.
+
+Buckets: parameters are grouped (in registration order, per dtype/device) into
+flat padded device buckets (``collective.GradBuckets``); ``p.grad`` (S-SGD) or
+``p.data`` (SMA) are made views into them so the reduction needs no fuse /
+defuse copies. If a training loop replaces ``p.grad`` (``zero_grad`` with
+``set_to_none=True``), the new gradient is copied into the bucket view once.
+"""
+import torch
+
+from .collective import Exchange, GradBuckets
+
+
+def _wrap(optimizer, mixin):
+    # same trick as the reference (torch/optimizers/sync_sgd.py:31-34): a
+    # subclass of the user's optimizer class, sharing its param_groups/state
+    cls = type(optimizer.__class__.__name__, (mixin, optimizer.__class__), {})
+    obj = cls.__new__(cls)
+    obj.__dict__.update(optimizer.__dict__)
+    return obj
+
+
+class _Bucketed:
+    def _kf_setup(self, named_parameters, exchange, bucket_bytes):
+        if named_parameters is None:
+            params = [p for g in self.param_groups for p in g["params"]]
+        else:
+            params = [p for _, p in named_parameters]
+        self._kf_params = [p for p in params if p.requires_grad]
+        self._kf_ex = exchange if exchange is not None else Exchange()
+        self._kf_bucket_bytes = bucket_bytes
+        self._kf_groups = None
+
+    def _kf_build(self, tensors_of):
+        groups = {}
+        for p in self._kf_params:
+            groups.setdefault((p.dtype, p.device), []).append(p)
+        self._kf_groups = []
+        for (dtype, device), ps in groups.items():
+            gb = GradBuckets([p.numel() for p in ps], dtype, device,
+                             self._kf_ex.world, bucket_bytes=self._kf_bucket_bytes)
+            self._kf_groups.append((ps, gb))
+
+
+class _SyncSGD(_Bucketed):
+    def sync_gradients(self):
+        if self._kf_groups is None:
+            self._kf_build(None)
+        for ps, gb in self._kf_groups:
+            for p, view in zip(ps, gb.views):
+                g = p.grad
+                v = view.view_as(p)
+                if g is None:
+                    v.zero_()
+                    p.grad = v
+                elif g.data_ptr() != v.data_ptr():
+                    v.copy_(g)
+                    p.grad = v
+            self._kf_ex.all_reduce_(gb.buckets, op=self._kf_op,
+                                    average=self._kf_average)
+
+    def step(self, closure=None):
+        self.sync_gradients()
+        return super().step(closure)
+
+
+def SynchronousSGDOptimizer(optimizer, named_parameters=None, op=None,
+                            average=True, exchange=None, bucket_bytes=32 << 20):
+    """S-SGD: all-reduce gradients (sum, then / np when average) before each
+    step. Returns the wrapped optimizer (reference: sync_sgd.py:81-84)."""
+    opt = _wrap(optimizer, _SyncSGD)
+    opt._kf_setup(named_parameters, exchange, bucket_bytes)
+    opt._kf_op = op if op is not None else "sum"
+    opt._kf_average = bool(average)
+    if opt._kf_average and opt._kf_op != "sum":
+        raise ValueError("average=True needs op='sum'")
+    return opt
+
+
+class _SMA(_Bucketed):
+    def sync_variables(self):
+        if self._kf_groups is None:
+            self._kf_build(None)
+            for ps, gb in self._kf_groups:  # move the variables into buckets
+                for p, view in zip(ps, gb.views):
+                    v = view.view_as(p)
+                    v.copy_(p.data)
+                    p.data = v
+        for ps, gb in self._kf_groups:
+            # sma_sgd.py:53-57: only variables that have a gradient take part;
+            # others are restored after the blend
+            saved = [(p, p.data.clone()) for p in ps if p.grad is None]
+            self._kf_ex.sma_(gb.buckets, self._kf_alpha)
+            for p, d in saved:
+                p.data.copy_(d)
+
+    def step(self, closure=None):
+        self.sync_variables()
+        return super().step(closure)
+
+
+def SynchronousAveragingOptimizer(optimizer, named_parameters=None, alpha=0.1,
+                                  exchange=None, bucket_bytes=32 << 20):
+    """SMA: v <- (1 - alpha) v + alpha * mean_ranks(v) before each local step
+    (sma_sgd.py:50-74)."""
+    opt = _wrap(optimizer, _SMA)
+    opt._kf_setup(named_parameters, exchange, bucket_bytes)
+    opt._kf_alpha = float(alpha)
+    return opt

@@ -1,0 +1,52 @@
+"""Test-only CPU stand-in for collective.HipEpilogue, so the N>1 orchestration
+(bucketing, sharding, RS -> epilogue -> AG) runs over gloo on CPU tensors. It
+delegates to the oracle, i.e. the exact semantics the HIP kernels are
+parity-tested against on the GPU (tests/test_gpu_parity.py)."""
+import numpy as np
+import torch
+
+from oracle import oracle
+
+_DT = {torch.float32: "f32", torch.float64: "f64", torch.float16: "f16",
+       torch.bfloat16: "bf16"}
+
+
+def _np(t):
+    if t.dtype in (torch.float16, torch.bfloat16):
+        return t.view(torch.int16).numpy().view(np.uint16 if t.dtype == torch.bfloat16 else np.float16)
+    return t.numpy()
+
+
+class CpuEpilogue:
+    def div_(self, x, np_):
+        a = _np(x)
+        a[...] = oracle.reduce_avg([np.ascontiguousarray(a)], _DT[x.dtype], np_)
+        return x
+
+    def sma_blend_(self, v, summed, np_, alpha):
+        a = _np(v)
+        a[...] = oracle.sma_blend(np.ascontiguousarray(a), np.ascontiguousarray(_np(summed)),
+                                  _DT[v.dtype], np_, alpha)
+        return v
+
+
+class GpuShardEpilogue:
+    """Runs the REAL HIP epilogue on a GPU copy of each CPU shard (used by the
+    gpu-marked multi-process test: gloo moves the data, HIP does the math)."""
+
+    def __init__(self, device):
+        from kungfu_amd.collective import HipEpilogue
+        self.hip = HipEpilogue()
+        self.device = device
+
+    def div_(self, x, np_):
+        g = x.to(self.device)
+        self.hip.div_(g, np_)
+        x.copy_(g.cpu())
+        return x
+
+    def sma_blend_(self, v, summed, np_, alpha):
+        g = v.to(self.device)
+        self.hip.sma_blend_(g, summed.to(self.device), np_, alpha)
+        v.copy_(g.cpu())
+        return v

@@ -1,0 +1,249 @@
+"""N>1 path over gloo on CPU (world sizes 2 and 3): bucketing, sharding,
+reduce-scatter -> epilogue -> all-gather, the optimizer wrappers. Expected
+values come from the oracle / the reference's known answers."""
+import json
+import os
+import socket
+import sys
+import traceback
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _entry(rank, world, port, fn_name, errq, use_gpu):
+    sys.path[:0] = [ROOT, HERE]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import test_collective_gloo as mod
+        getattr(mod, fn_name)(rank, world, use_gpu)
+        dist.barrier()
+    except Exception:
+        errq.put("rank %d: %s" % (rank, traceback.format_exc()))
+        raise
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def run_world(fn_name, world, use_gpu=False):
+    ctx = mp.get_context("spawn")
+    errq = ctx.SimpleQueue()
+    port = free_port()
+    procs = [ctx.Process(target=_entry, args=(r, world, port, fn_name, errq, use_gpu))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=600)
+    errs = []
+    while not errq.empty():
+        errs.append(errq.get())
+    assert not errs, "\n".join(errs)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+
+
+def _epilogue(use_gpu):
+    import cpu_epilogue
+    if use_gpu:
+        return cpu_epilogue.GpuShardEpilogue(torch.device("cuda:0"))
+    return cpu_epilogue.CpuEpilogue()
+
+
+def _inputs(rank, n, dtype=np.float32):
+    rng = np.random.default_rng(100 + rank)
+    return rng.standard_normal(n).astype(dtype)
+
+
+# ---- per-rank bodies ---------------------------------------------------------
+
+def body_all_reduce(rank, world, use_gpu):
+    from kungfu_amd.collective import Exchange, padded_count
+    from oracle import oracle
+    ex = Exchange(epilogue=_epilogue(use_gpu))
+    n = 100003
+    L = padded_count(n, world, 4)
+    xs = [_inputs(r, n) for r in range(world)]
+    b = torch.zeros(L)
+    b[:n] = torch.from_numpy(xs[rank])
+    ex.all_reduce_([b], average=True)
+    got = b[:n].numpy()
+    if world == 2:  # two operands: commutative, so bit-exact
+        assert np.array_equal(got, oracle.reduce_avg(xs, "f32", 2))
+    else:
+        exact = np.sum(np.array(xs, np.float64), axis=0) / world
+        bound = (world - 1) * 2.0 ** -24 * np.sum(np.abs(np.array(xs, np.float64)), axis=0) / world
+        assert np.all(np.abs(got - exact) <= bound + 2.0 ** -24 * np.abs(exact))
+    # sum only, int32: bit-exact for every world size and order
+    ints = [np.random.default_rng(r).integers(-2**31, 2**31 - 1, n, dtype=np.int32)
+            for r in range(world)]
+    bi = torch.zeros(L, dtype=torch.int32)
+    bi[:n] = torch.from_numpy(ints[rank])
+    ex.all_reduce_([bi], op="sum")
+    assert np.array_equal(bi[:n].numpy(), oracle.reduce_k(ints, "i32"))
+    # MAX
+    bm = torch.zeros(L)
+    bm[:n] = torch.from_numpy(xs[rank])
+    ex.all_reduce_([bm], op="max")
+    assert np.array_equal(bm[:n].numpy(), np.max(np.array(xs), axis=0))
+
+
+def body_resnet50_buckets(rank, world, use_gpu):
+    # C4 layout: ResNet-50 gradient set fused into 16 buckets (EvenPartition)
+    from kungfu_amd.collective import Exchange, GradBuckets
+    sizes = json.load(open(os.path.join(HERE, "golden", "models.json")))["resnet50-imagenet"]
+    ex = Exchange(epilogue=_epilogue(use_gpu))
+    gb = GradBuckets(sizes, torch.float32, torch.device("cpu"), world, n_buckets=16)
+    assert len(gb.buckets) <= 16 and sum(gb.spans) == 25583592
+    for i, v in enumerate(gb.views):
+        assert v.numel() == sizes[i]
+        v.fill_(float((rank + 1) * (i % 7 + 1)))
+    for b in gb.buckets:
+        assert b.numel() % world == 0 and (b.numel() // world) * 4 % 256 == 0
+    ex.all_reduce_(gb.buckets, average=True)
+    tot = world * (world + 1) / 2
+    for i, v in enumerate(gb.views):
+        want = np.float32(np.float32(tot * (i % 7 + 1)) / np.float32(world))
+        assert torch.all(v == want), i
+
+
+def body_group_all_reduce(rank, world, use_gpu):
+    # ops/collective.py:71-73 mirror; KAT of fake_agent.cpp:15-44 (iota * np)
+    from kungfu_amd.collective import Exchange, group_all_reduce
+    ex = Exchange(epilogue=_epilogue(use_gpu))
+    ts = [torch.arange(world * 4, dtype=torch.int32),
+          torch.ones(1 << 20, dtype=torch.int32),
+          torch.full((3, 5), float(rank + 1))]
+    out = group_all_reduce(ts, exchange=ex)
+    assert torch.equal(out[0], torch.arange(world * 4, dtype=torch.int32) * world)
+    assert torch.all(out[1] == world)  # kungfu-test-public-apis.go:87-104
+    assert torch.all(out[2] == world * (world + 1) / 2)
+    assert out[2].shape == (3, 5)
+
+
+def _model(seed=0):
+    torch.manual_seed(seed)
+    return torch.nn.Sequential(torch.nn.Linear(17, 9), torch.nn.Tanh(), torch.nn.Linear(9, 3))
+
+
+def _loss(m, rank):
+    g = torch.Generator().manual_seed(rank)
+    x = torch.randn(8, 17, generator=g)
+    return (m(x) ** 2).mean()
+
+
+def body_sync_sgd(rank, world, use_gpu):
+    from kungfu_amd.collective import Exchange
+    from kungfu_amd.optimizers import SynchronousSGDOptimizer
+    m = _model()
+    opt = SynchronousSGDOptimizer(torch.optim.SGD(m.parameters(), lr=0.1),
+                                  named_parameters=m.named_parameters(),
+                                  exchange=Exchange(epilogue=_epilogue(use_gpu)))
+    # expected: every rank's gradients, summed, / np, then SGD
+    grads = []
+    for r in range(world):
+        mr = _model()
+        _loss(mr, r).backward()
+        grads.append([p.grad.clone() for p in mr.parameters()])
+    ref = _model()
+    for steps in range(2):
+        opt.zero_grad()
+        _loss(m, rank).backward()
+        opt.step()
+        if steps == 0:
+            with torch.no_grad():
+                for j, p in enumerate(ref.parameters()):
+                    s = grads[0][j].clone()
+                    for r in range(1, world):
+                        s = s + grads[r][j]
+                    p -= 0.1 * (s / world)
+            for p, q in zip(m.parameters(), ref.parameters()):
+                assert torch.allclose(p, q, rtol=0, atol=1e-6)
+    # all ranks hold identical parameters after synchronous steps
+    flat = torch.cat([p.detach().reshape(-1) for p in m.parameters()])
+    allf = [torch.empty_like(flat) for _ in range(world)]
+    dist.all_gather(allf, flat)
+    for f in allf:
+        assert torch.equal(f, flat)
+
+
+def body_sma(rank, world, use_gpu):
+    from kungfu_amd.collective import Exchange
+    from kungfu_amd.optimizers import SynchronousAveragingOptimizer
+    alpha = 0.1
+    m = _model(seed=rank)  # replicas start different
+    before = [p.detach().clone() for p in m.parameters()]
+    allp = []
+    for r in range(world):
+        allp.append([p.detach().clone() for p in _model(seed=r).parameters()])
+    opt = SynchronousAveragingOptimizer(torch.optim.SGD(m.parameters(), lr=0.0),
+                                        alpha=alpha,
+                                        exchange=Exchange(epilogue=_epilogue(use_gpu)))
+    _loss(m, rank).backward()
+    opt.step()  # lr 0: only the model averaging acts
+    for j, p in enumerate(m.parameters()):
+        s = allp[0][j].clone()
+        for r in range(1, world):
+            s = s + allp[r][j]
+        avg = s / world
+        want = np.float32(1 - alpha) * before[j] + np.float32(alpha) * avg
+        assert torch.allclose(p.detach(), want, rtol=0, atol=2e-7), j
+
+
+# ---- tests -------------------------------------------------------------------
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_all_reduce(world):
+    run_world("body_all_reduce", world)
+
+
+def test_resnet50_16_buckets():
+    run_world("body_resnet50_buckets", 2)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_group_all_reduce(world):
+    run_world("body_group_all_reduce", world)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sync_sgd_optimizer(world):
+    run_world("body_sync_sgd", world)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sma_optimizer(world):
+    run_world("body_sma", world)
+
+
+def test_world1_identity():
+    from kungfu_amd.collective import Exchange
+    ex = Exchange()
+    b = torch.arange(64, dtype=torch.float32)
+    ex.all_reduce_([b], average=True)
+    assert torch.equal(b, torch.arange(64, dtype=torch.float32))
+
+
+@pytest.mark.gpu
+def test_all_reduce_with_hip_epilogue():
+    # gloo moves the shards, the real HIP /np epilogue runs on the GPU
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    run_world("body_all_reduce", 2, use_gpu=True)
+    run_world("body_sync_sgd", 3, use_gpu=True)
+    run_world("body_sma", 2, use_gpu=True)
