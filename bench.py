@@ -125,7 +125,8 @@ def cpu_baseline(x, y, seconds):
     xh = x.cpu().numpy()
     yh = y.cpu().numpy()
     zh = np.empty_like(xh)
-    t1 = oracle.bench_transform2(xh, yh, zh, "f32", "sum", 1, threads=1)
+    oracle.bench_transform2(xh, yh, zh, "f32", "sum", 1, threads=1)  # page in
+    t1 = oracle.bench_transform2(xh, yh, zh, "f32", "sum", 2, threads=1) / 2
     reps = max(1, min(1000, int(seconds / max(t1, 1e-6))))
     t = oracle.bench_transform2(xh, yh, zh, "f32", "sum", reps, threads=1)
     s_bytes = xh.nbytes
