@@ -113,17 +113,31 @@ class Exchange:
         for b in buckets:
             self._check(b)
         sums = []
-        for i, b in enumerate(buckets):
-            s = self._workspace(("sum", i), b.numel(), b)
-            if self.world == 1:
+        if self.world == 1:
+            for i, b in enumerate(buckets):
+                s = self._workspace(("sum", i), b.numel(), b)
                 s.copy_(b)
-            else:
-                shard = self._workspace(("rs", i), b.numel() // self.world, b)
-                dist.reduce_scatter_tensor(shard, b, op=dist.ReduceOp.SUM,
-                                           group=self.group)
-                dist.all_gather_into_tensor(s, shard, group=self.group)
-            sums.append(s)
-        for b, s in zip(buckets, sums):
+                sums.append(s)
+            for b, s in zip(buckets, sums):
+                self.epilogue.sma_blend_(b, s, self.world, alpha)
+            return buckets
+        # pipelined: every reduce-scatter is queued first, each all-gather
+        # right behind its reduce-scatter, and each bucket's blend waits only
+        # for its own all-gather, so blends overlap later buckets' transfers.
+        # The reduce-scatter reads v before any blend of that bucket runs.
+        rs = []
+        for i, b in enumerate(buckets):
+            shard = self._workspace(("rs", i), b.numel() // self.world, b)
+            rs.append((shard, dist.reduce_scatter_tensor(
+                shard, b, op=dist.ReduceOp.SUM, group=self.group, async_op=True)))
+        ags = []
+        for i, (b, (shard, w)) in enumerate(zip(buckets, rs)):
+            w.wait()
+            s = self._workspace(("sum", i), b.numel(), b)
+            ags.append((s, dist.all_gather_into_tensor(s, shard, group=self.group,
+                                                       async_op=True)))
+        for b, (s, w) in zip(buckets, ags):
+            w.wait()
             self.epilogue.sma_blend_(b, s, self.world, alpha)
         return buckets
 
