@@ -145,24 +145,43 @@ class Exchange:
 class GradBuckets:
     """Flat, padded device storage for a list of same-dtype tensors.
 
-    Tensors are grouped, in order, into buckets of about ``bucket_bytes`` at
-    tensor boundaries (a tensor larger than that gets a bucket of its own);
-    each bucket is padded to split into `world` aligned shards. ``views[i]``
-    is tensor i's view into the flat storage, so gradients can be written in
-    place and reduced without fuse/defuse copies (the reference's NCCL path
-    concatenates and slices instead, ops/__init__.py:29-46).
+    Two layouts:
+      * ``bucket_bytes`` (default): tensors are grouped, in order, into buckets
+        of about that size at tensor boundaries (a larger tensor gets a bucket
+        of its own); each bucket is its own flat buffer, padded to split into
+        ``world`` aligned shards.
+      * ``n_buckets=k``: all tensors are laid out back to back in ONE flat
+        buffer, which is cut into k contiguous buckets by EvenPartition
+        (interval.go:12-27) of its aligned units — tensors may straddle bucket
+        boundaries (the reduce is element-wise). This is SURVEY §8(a) C4:
+        ResNet-50's 25,583,592 fp32 in 16 buckets of ~1.6 M elements.
+    ``views[i]`` is tensor i's view into the flat storage, so gradients can be
+    written in place and reduced without fuse/defuse copies (the reference's
+    NCCL path concatenates and slices instead, ops/__init__.py:29-46).
+    ``spans[j]`` is the number of real (non-padding) elements of bucket j,
+    which always precede its padding.
     """
 
     def __init__(self, numels, dtype, device, world, bucket_bytes=32 << 20,
                  n_buckets=None):
         itemsize = torch.empty((), dtype=dtype).element_size()
-        total = sum(numels)
-        if n_buckets is not None:  # EvenPartition of the fused total
-            groups = self._groups_even(numels, total, n_buckets)
-        else:
-            groups = self._groups_greedy(numels, bucket_bytes // itemsize)
-        self.buckets, self.views, self.spans = [], [None] * len(numels), []
-        for g in groups:
+        self.buckets, self.views, self.spans, self.flats = [], [None] * len(numels), [], []
+        if n_buckets is not None:
+            total = sum(numels)
+            unit = world * max(1, ALIGN_BYTES // itemsize)
+            units = max(1, (total + unit - 1) // unit)
+            flat = torch.zeros(units * unit, dtype=dtype, device=device)
+            self.flats.append(flat)
+            off = 0
+            for i, n in enumerate(numels):
+                self.views[i] = flat[off:off + n]
+                off += n
+            for ub, ue in EvenPartition(0, units, min(n_buckets, units)):
+                b, e = ub * unit, ue * unit
+                self.buckets.append(flat[b:e])
+                self.spans.append(max(0, min(e, total) - b))
+            return
+        for g in self._groups_greedy(numels, max(1, bucket_bytes // itemsize)):
             count = sum(numels[i] for i in g)
             b = torch.zeros(padded_count(max(count, 1), world, itemsize),
                             dtype=dtype, device=device)
@@ -170,6 +189,7 @@ class GradBuckets:
             for i in g:
                 self.views[i] = b[off:off + numels[i]]
                 off += numels[i]
+            self.flats.append(b)
             self.buckets.append(b)
             self.spans.append(count)
 
@@ -182,23 +202,6 @@ class GradBuckets:
                 cur, size = [], 0
             cur.append(i)
             size += n
-        if cur:
-            groups.append(cur)
-        return groups
-
-    @staticmethod
-    def _groups_even(numels, total, k):
-        # targets from EvenPartition (interval.go:12-27), snapped to tensor ends
-        bounds = [e for _, e in EvenPartition(0, total, k)]
-        groups, cur, acc, bi = [], [], 0, 0
-        for i, n in enumerate(numels):
-            cur.append(i)
-            acc += n
-            if bi < len(bounds) and acc >= bounds[bi]:
-                groups.append(cur)
-                cur = []
-                while bi < len(bounds) and acc >= bounds[bi]:
-                    bi += 1
         if cur:
             groups.append(cur)
         return groups

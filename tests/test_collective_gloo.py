@@ -109,7 +109,9 @@ def body_resnet50_buckets(rank, world, use_gpu):
     sizes = json.load(open(os.path.join(HERE, "golden", "models.json")))["resnet50-imagenet"]
     ex = Exchange(epilogue=_epilogue(use_gpu))
     gb = GradBuckets(sizes, torch.float32, torch.device("cpu"), world, n_buckets=16)
-    assert len(gb.buckets) <= 16 and sum(gb.spans) == 25583592
+    assert len(gb.buckets) == 16 and sum(gb.spans) == 25583592
+    lens = [b.numel() for b in gb.buckets]
+    assert max(lens) - min(lens) <= world * 64  # EvenPartition of aligned units
     for i, v in enumerate(gb.views):
         assert v.numel() == sizes[i]
         v.fill_(float((rank + 1) * (i % 7 + 1)))

@@ -308,3 +308,35 @@ def test_c2_full_size_bit_exact(lib, orc, dev):
     z2 = ops.bucket_reduce([x, y], out=x)  # out aliases input 0
     torch.cuda.synchronize()
     assert torch.equal(z2, z)
+
+
+# ---- optimizer surface on the GPU (world 1: default HIP epilogue) ---------
+
+def test_optimizers_world1_on_gpu(orc, dev):
+    from kungfu_amd.optimizers import (SynchronousAveragingOptimizer,
+                                       SynchronousSGDOptimizer)
+    torch.manual_seed(0)
+    m = torch.nn.Linear(300, 70).to(dev)
+    ref = torch.nn.Linear(300, 70).to(dev)
+    ref.load_state_dict(m.state_dict())
+    x = torch.randn(16, 300, device=dev)
+    opt = SynchronousSGDOptimizer(torch.optim.SGD(m.parameters(), lr=0.05),
+                                  named_parameters=m.named_parameters())
+    ropt = torch.optim.SGD(ref.parameters(), lr=0.05)
+    for _ in range(3):
+        for mm, oo in ((m, opt), (ref, ropt)):
+            oo.zero_grad()
+            (mm(x) ** 2).mean().backward()
+            oo.step()
+    for p, q in zip(m.parameters(), ref.parameters()):
+        assert torch.equal(p, q)  # np = 1: g / 1 == g, identical updates
+    # SMA at np = 1 still applies (1-a) v + a (v / 1), rounded per TF op order
+    v_before = [p.detach().clone() for p in m.parameters()]
+    sma = SynchronousAveragingOptimizer(torch.optim.SGD(m.parameters(), lr=0.0), alpha=0.1)
+    sma.zero_grad()
+    (m(x) ** 2).mean().backward()
+    sma.step()
+    for p, v in zip(m.parameters(), v_before):
+        vh = v.cpu().numpy().reshape(-1)
+        want = orc.sma_blend(vh, vh, "f32", 1, 0.1)
+        assert np.array_equal(p.detach().cpu().numpy().reshape(-1), want)
