@@ -72,6 +72,13 @@ def parse():
                     help="rehearsal only: put every rank on this GPU")
     ap.add_argument("--no-extra", action="store_true",
                     help="N>1: skip the C4/C5 sub-benchmarks")
+    ap.add_argument("--config", default="default", choices=["default", "c1"],
+                    help="c1: BASELINE configs[0], np=2 localhost all-reduce of "
+                         "one 4 MiB fp32 bucket over the rchannel wire format")
+    ap.add_argument("--c1-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--c1-rank", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--c1-mode", default="device", help=argparse.SUPPRESS)
+    ap.add_argument("--c1-dir", default="", help=argparse.SUPPRESS)
     ap.add_argument("--profile-only", action="store_true",
                     help="only the timed kernel loop (for rocprofv3 runs)")
     return ap.parse_args()
@@ -157,30 +164,121 @@ def cpu_baseline(x, y, seconds):
 
 
 def host_staged(lib, x, y):
-    """Copy-inclusive rate of the drop-in: pageable host x,y -> HBM -> kernel
-    -> host z (std_transform_2's path). Not `value`."""
-    xh = x.cpu().numpy()
-    yh = y.cpu().numpy()
-    zh = np.empty_like(xh)
-    n = xh.size
-    rc = lib.kf_transform2_host(xh.ctypes.data, yh.ctypes.data, zh.ctypes.data, n,
-                                KF_FLOAT, KF_SUM)
-    if rc != 0:
-        return {"error": lib.kf_last_error().decode()}
-    reps = 3
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        lib.kf_transform2_host(xh.ctypes.data, yh.ctypes.data, zh.ctypes.data, n,
-                               KF_FLOAT, KF_SUM)
-    t = (time.perf_counter() - t0) / reps
-    ok = bool(np.array_equal(zh, xh + yh))
-    return {"value": round(xh.nbytes / t / 2**30, 3), "unit": "GiB/s",
-            "ms_per_call": round(t * 1e3, 3), "correct": ok,
-            "path": "pageable host -> HBM -> HIP kernel -> pageable host"}
+    """Copy-inclusive rate of the drop-in: host x,y -> HBM -> kernel -> host z
+    (std_transform_2's path), from pageable buffers and from pinned buffers
+    (16 MiB chunks over two streams). Never `value`."""
+    res = {}
+    for kind in ("pageable", "pinned"):
+        xh, yh = x.cpu(), y.cpu()
+        zh = torch.empty_like(xh)
+        if kind == "pinned":
+            xh, yh, zh = xh.pin_memory(), yh.pin_memory(), zh.pin_memory()
+        n = xh.numel()
+        args = (xh.data_ptr(), yh.data_ptr(), zh.data_ptr(), n, KF_FLOAT, KF_SUM)
+        rc = lib.kf_transform2_host(*args)
+        if rc != 0:
+            res[kind] = {"error": lib.kf_last_error().decode()}
+            continue
+        reps = 5
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            lib.kf_transform2_host(*args)
+        t = (time.perf_counter() - t0) / reps
+        ok = bool(torch.equal(zh, xh + yh))
+        res[kind] = {"value": round(xh.numel() * 4 / t / 2**30, 3), "unit": "GiB/s",
+                     "ms_per_call": round(t * 1e3, 3), "correct": ok}
+    res["path"] = "host x,y -> HBM -> HIP kernel -> host z (PCIe incl.), 256 MiB fp32"
+    return res
+
+
+# ---- C1: np = 2 plumbing over the rchannel wire format ----------------------
+
+C1_ELEMS = 1 << 20  # one 4 MiB fp32 bucket (SURVEY §8d)
+
+
+def c1_child(args):
+    """One peer of the C1 run. Rank 0 (the star root) reduces with:
+    device   — page-locked ingest + HIP fold, bucket resident in HBM;
+    dropin   — host buffers, std_transform_2 of libkungfu_amd.so per chunk;
+    cpu      — host buffers, the oracle's restatement of the reference reduce
+               (this is bench.py's CPU-baseline leg)."""
+    from kungfu_amd.session import Session
+    r = args.c1_rank
+    x = ((r + 1) * (np.arange(C1_ELEMS) % 1024) / 1024).astype(np.float32)
+    want = (3 * (np.arange(C1_ELEMS) % 1024) / 1024).astype(np.float32)
+    if args.c1_mode == "device":
+        dev = torch.device("cuda", 0)
+        xs, ys = torch.from_numpy(x).to(dev), torch.zeros(C1_ELEMS, device=dev)
+        sess = Session(r, 2, args.c1_dir, mode="device")
+        result = lambda: ys.cpu().numpy()  # noqa: E731
+    else:
+        xs, ys = x, np.zeros_like(x)
+        fn = None
+        if args.c1_mode == "cpu":
+            from oracle import oracle
+            olib = oracle.lib()
+
+            def fn(a, b, out, n, dt, op):
+                olib.oracle_transform2(a, b, out, n, dt, op)
+        sess = Session(r, 2, args.c1_dir, mode="host", reduce_fn=fn)
+        result = lambda: ys  # noqa: E731
+    name = "NegotiatedGrad_0/AllReduce"
+    for _ in range(args.warmup):
+        sess.all_reduce(xs, ys, name)
+    ok = bool(np.array_equal(result(), want))
+    ts = []
+    for _ in range(args.steps):
+        t0 = time.perf_counter()
+        sess.all_reduce(xs, ys, name)
+        ts.append(time.perf_counter() - t0)
+    ok = ok and bool(np.array_equal(result(), want))
+    sess.close()
+    if r == 0:
+        ts.sort()
+        med = ts[len(ts) // 2]
+        nbytes = C1_ELEMS * 4
+        print(json.dumps({"mode": args.c1_mode, "correct": ok,
+                          "latency_ms_median": round(med * 1e3, 4),
+                          "latency_ms_min": round(ts[0] * 1e3, 4),
+                          "rate_GiBps": round(4 * (2 - 1) * nbytes / med / 2**30, 3)}),
+              flush=True)
+
+
+def c1_parent(args):
+    """Launch the two peers per mode (subprocesses, one unix socket each)."""
+    import subprocess
+    import tempfile
+    res = {}
+    for mode in ("device", "dropin", "cpu"):
+        with tempfile.TemporaryDirectory() as d:
+            cmd = [sys.executable, os.path.abspath(__file__), "--c1-child",
+                   "--c1-mode", mode, "--c1-dir", d, "--steps", str(args.steps),
+                   "--warmup", str(args.warmup)]
+            procs = [subprocess.Popen(cmd + ["--c1-rank", str(r)], stdout=subprocess.PIPE,
+                                      text=True, cwd=ROOT) for r in range(2)]
+            outs = [p.communicate(timeout=600)[0] for p in procs]
+            if any(p.returncode for p in procs):
+                res[mode] = {"error": "peer exit codes %s" % [p.returncode for p in procs]}
+                continue
+            res[mode] = json.loads(outs[0].strip().splitlines()[-1])
+    line = {
+        "metric": "C1 all-reduce rate 4(np-1)*bytes/t (kungfu-bench-allreduce.go:73-80)",
+        "unit": "GiB/s",
+        "config": {"workload": "C1: np=2 localhost, one 4 MiB fp32 bucket, 4 x 1 MiB "
+                               "chunks, STAR at rank 0, rchannel framing over unix "
+                               "sockets", "elements": C1_ELEMS},
+        "steps": args.steps, "warmup": args.warmup,
+        "modes": res,
+    }
+    print(json.dumps(line), flush=True)
 
 
 def main():
     args = parse()
+    if args.c1_child:
+        return c1_child(args)
+    if args.config == "c1":
+        return c1_parent(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

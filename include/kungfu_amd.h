@@ -87,6 +87,8 @@ enum KF_Status {
     KF_ERR_ARG         = 3, /* null pointer with n>0, k out of range  */
     KF_ERR_HIP         = 4, /* a HIP runtime call failed              */
     KF_ERR_NO_DEVICE   = 5, /* no usable gfx950 device                */
+    KF_ERR_IO          = 6, /* socket read/write failed               */
+    KF_ERR_PROTO       = 7, /* rchannel framing/length/token mismatch  */
 };
 
 /* Largest k accepted by kf_bucket_reduce*. */
@@ -130,17 +132,78 @@ const char *kf_version(void);
 /* Last HIP error string recorded by the library on this thread. */
 const char *kf_last_error(void);
 
+/* Page-lock / release a host range so std_transform_2 and
+ * kf_transform2_host can DMA it directly (e.g. a receive-buffer pool the
+ * transport reuses, srcs/go/rchannel/connection/byte_slice_pool.go:28-60). */
+int kf_host_register(void *p, size_t bytes);
+int kf_host_unregister(void *p);
+
 /* Tuning hook (tools/tune_reduce.py only): launch geometry of the fp32 SUM
  * 2-input path — unroll in {1,2,4,8} vectors per thread, grid cap in blocks,
  * non-temporal loads, plain stores. Not thread-safe; call before launching. */
 int kf_set_geometry(int unroll, int grid_cap, int loadnt, int stplain);
 
 /* Host-pointer reduce with a status code instead of exit(): the path
- * std_transform_2 takes (pageable host x,y -> HBM -> HIP kernel -> host out,
- * synchronous, per-thread stream and device scratch). Used by the
- * copy-inclusive measurement (bench.py host_staged). */
+ * std_transform_2 takes. Synchronous, per-thread streams and device scratch.
+ * If x, y and out are all page-locked (hipHostMalloc or kf_host_register)
+ * the bucket moves in 16 MiB chunks alternating over two streams (H2D of
+ * chunk i+1 overlaps kernel + D2H of chunk i); otherwise pageable copies
+ * through the runtime's staging. Used by the copy-inclusive measurement
+ * (bench.py host_staged). */
 int kf_transform2_host(const void *x, const void *y, void *out, size_t n,
                        KungFu_Datatype dt, KungFu_Op op);
+
+/* ---- host ingestion: rchannel wire format + device recvOnto ----------- */
+
+/* rchannel constants (srcs/go/rchannel/connection/message.go:10-17, 71-78) */
+#define KF_RCH_CONN_COLLECTIVE 2
+#define KF_RCH_NO_FLAG 0u
+#define KF_RCH_WAIT_RECV_BUF 1u
+
+/* Connection handshake: client sends {u16 type, u16 src_port, u32 src_ipv4},
+ * server answers {u32 token}; a token mismatch on a collective connection is
+ * an error (srcs/go/rchannel/connection/connection.go:28-101). */
+int kf_rch_client_handshake(int fd, uint16_t conn_type, uint16_t src_port,
+                            uint32_t src_ipv4, uint32_t expect_token);
+int kf_rch_server_handshake(int fd, uint32_t token, uint16_t *conn_type,
+                            uint16_t *src_port, uint32_t *src_ipv4);
+
+/* One named message: {u32 name_len, name, u32 flags} {u32 len, payload}
+ * (message.go:90-198; tcpConnection.Send, connection.go:149-165). */
+int kf_rch_send(int fd, const char *name, uint32_t flags, const void *data,
+                uint32_t len);
+/* Reads a message header; name is NUL-terminated into name[cap]. */
+int kf_rch_recv_header(int fd, char *name, uint32_t cap, uint32_t *name_len,
+                       uint32_t *flags);
+/* Reads a message body into dst; its length must equal expect_len
+ * (Message.ReadInto, message.go:184-198). */
+int kf_rch_recv_body(int fd, void *dst, uint32_t expect_len);
+
+/* Page-locked landing slots + device slots for peer chunks. */
+typedef struct kf_ingest kf_ingest_t;
+kf_ingest_t *kf_ingest_create(size_t slot_bytes, int nslots);
+void kf_ingest_destroy(kf_ingest_t *g);
+
+/* recvOnto on the device (session.go:255-264): read the body of the message
+ * whose header was just read (len bytes) from fd into the next page-locked
+ * slot, then on `stream`: copy it to HBM and fold dev_acc = own o peer, with
+ * own = dev_own (SendBuf before the first receive) or dev_acc if NULL.
+ * Returns after the socket read; the device work stays queued on `stream`. */
+int kf_ingest_recv_onto(kf_ingest_t *g, int fd, uint32_t len, void *dev_acc,
+                        const void *dev_own, size_t count, KungFu_Datatype dt,
+                        KungFu_Op op, void *stream);
+/* recvInto on the device (session.go:266-270): read the body into the next
+ * page-locked slot and queue its copy into dev_dst on `stream`. */
+int kf_ingest_recv_into(kf_ingest_t *g, int fd, uint32_t len, void *dev_dst,
+                        void *stream);
+/* sendOnto/sendInto from the device: copy bytes of dev_src (after the work
+ * queued on `stream`) to a page-locked slot and send it as one message. */
+int kf_ingest_send_from_device(kf_ingest_t *g, int fd, const char *name,
+                               uint32_t flags, const void *dev_src, size_t bytes,
+                               void *stream);
+/* Wait for every queued slot copy. */
+int kf_ingest_sync(kf_ingest_t *g);
+const char *kf_ingest_last_error(void);
 
 #ifdef __cplusplus
 }

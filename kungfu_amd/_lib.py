@@ -24,6 +24,20 @@ EXPORTED = (
     "kf_last_error",
     "kf_transform2_host",
     "kf_set_geometry",
+    "kf_host_register",
+    "kf_host_unregister",
+    "kf_rch_client_handshake",
+    "kf_rch_server_handshake",
+    "kf_rch_send",
+    "kf_rch_recv_header",
+    "kf_rch_recv_body",
+    "kf_ingest_create",
+    "kf_ingest_destroy",
+    "kf_ingest_recv_onto",
+    "kf_ingest_recv_into",
+    "kf_ingest_send_from_device",
+    "kf_ingest_sync",
+    "kf_ingest_last_error",
 )
 
 STATUS = {
@@ -33,6 +47,8 @@ STATUS = {
     3: "KF_ERR_ARG",
     4: "KF_ERR_HIP",
     5: "KF_ERR_NO_DEVICE",
+    6: "KF_ERR_IO",
+    7: "KF_ERR_PROTO",
 }
 
 MAX_INPUTS = 16
@@ -89,6 +105,39 @@ def load():
     lib.kf_transform2_host.restype = c_int
     lib.kf_set_geometry.argtypes = [c_int, c_int, c_int, c_int]
     lib.kf_set_geometry.restype = c_int
+    lib.kf_host_register.argtypes = [c_void_p, c_size_t]
+    lib.kf_host_register.restype = c_int
+    lib.kf_host_unregister.argtypes = [c_void_p]
+    lib.kf_host_unregister.restype = c_int
+    u16, u32 = ctypes.c_uint16, ctypes.c_uint32
+    lib.kf_rch_client_handshake.argtypes = [c_int, u16, u16, u32, u32]
+    lib.kf_rch_client_handshake.restype = c_int
+    lib.kf_rch_server_handshake.argtypes = [c_int, u32, ctypes.POINTER(u16),
+                                            ctypes.POINTER(u16), ctypes.POINTER(u32)]
+    lib.kf_rch_server_handshake.restype = c_int
+    lib.kf_rch_send.argtypes = [c_int, ctypes.c_char_p, u32, c_void_p, u32]
+    lib.kf_rch_send.restype = c_int
+    lib.kf_rch_recv_header.argtypes = [c_int, ctypes.c_char_p, u32, ctypes.POINTER(u32),
+                                       ctypes.POINTER(u32)]
+    lib.kf_rch_recv_header.restype = c_int
+    lib.kf_rch_recv_body.argtypes = [c_int, c_void_p, u32]
+    lib.kf_rch_recv_body.restype = c_int
+    lib.kf_ingest_create.argtypes = [c_size_t, c_int]
+    lib.kf_ingest_create.restype = c_void_p
+    lib.kf_ingest_destroy.argtypes = [c_void_p]
+    lib.kf_ingest_destroy.restype = None
+    lib.kf_ingest_recv_onto.argtypes = [c_void_p, c_int, u32, c_void_p, c_void_p,
+                                        c_size_t, c_int, c_int, c_void_p]
+    lib.kf_ingest_recv_onto.restype = c_int
+    lib.kf_ingest_recv_into.argtypes = [c_void_p, c_int, u32, c_void_p, c_void_p]
+    lib.kf_ingest_recv_into.restype = c_int
+    lib.kf_ingest_send_from_device.argtypes = [c_void_p, c_int, ctypes.c_char_p, u32,
+                                               c_void_p, c_size_t, c_void_p]
+    lib.kf_ingest_send_from_device.restype = c_int
+    lib.kf_ingest_sync.argtypes = [c_void_p]
+    lib.kf_ingest_sync.restype = c_int
+    lib.kf_ingest_last_error.argtypes = []
+    lib.kf_ingest_last_error.restype = ctypes.c_char_p
     _lib = lib
     return lib
 
@@ -96,8 +145,8 @@ def load():
 def check(rc, what):
     if rc != 0:
         lib = load()
-        raise KungFuAMDError("%s failed: %s (%s)" % (
-            what, STATUS.get(rc, rc), lib.kf_last_error().decode()))
+        detail = lib.kf_last_error().decode() or lib.kf_ingest_last_error().decode()
+        raise KungFuAMDError("%s failed: %s (%s)" % (what, STATUS.get(rc, rc), detail))
 
 
 def ptr_array(ptrs):

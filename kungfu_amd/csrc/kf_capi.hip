@@ -277,29 +277,33 @@ int launch_sma(void *v, const void *sum, size_t n, int np, C c1, C c2,
 // ---------------------------------------------------------------------------
 // B1 support: per-thread staging context
 // ---------------------------------------------------------------------------
+constexpr int kSlots = 2;                        // pipeline depth (streams)
+constexpr size_t kChunkBytes = size_t(16) << 20;  // per input per slot
+
 struct Staging {
-    hipStream_t stream = nullptr;
-    void *dev          = nullptr;  // 3 regions: x | y | z
-    size_t cap         = 0;        // bytes per region
-    int device         = -1;
+    hipStream_t stream[kSlots] = {nullptr, nullptr};
+    void *dev                  = nullptr;  // 3 regions: x | y | z
+    size_t cap                 = 0;        // bytes per region
+    int device                 = -1;
 
     ~Staging()
     {
         // Process teardown may have unloaded the runtime already; best effort.
         if (dev) (void)hipFree(dev);
-        if (stream) (void)hipStreamDestroy(stream);
+        for (auto &s : stream)
+            if (s) (void)hipStreamDestroy(s);
     }
 
     int ensure(size_t bytes)
     {
-        if (!stream) {
+        if (!stream[0]) {
             int cnt = 0;
             if (hipGetDeviceCount(&cnt) != hipSuccess || cnt == 0) {
                 t_last_error = "no HIP device";
                 return KF_ERR_NO_DEVICE;
             }
             KF_HIP(hipGetDevice(&device));
-            KF_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+            for (auto &s : stream) KF_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
         }
         if (bytes > cap) {
             if (dev) KF_HIP(hipFree(dev));
@@ -314,7 +318,31 @@ struct Staging {
 
 thread_local Staging t_staging;
 
+// True when the whole range is page-locked host memory the GPU can DMA
+// (hipHostMalloc'ed, or registered with kf_host_register).
+bool is_pinned(const void *p, size_t bytes)
+{
+    if (!p) return false;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    if (a.type != hipMemoryTypeHost) return false;
+    const void *last = static_cast<const char *>(p) + bytes - 1;
+    hipPointerAttribute_t b;
+    if (hipPointerGetAttributes(&b, last) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return b.type == hipMemoryTypeHost;
+}
+
 // Host pointers -> HBM -> kernel -> host. Synchronous.
+//  * pinned x, y, out: 16 MiB chunks alternate over two streams, so the H2D
+//    of chunk i+1 overlaps the kernel + D2H of chunk i (the SDMA engines for
+//    the two directions run concurrently);
+//  * pageable: whole-buffer copies through the runtime's staging.
 int transform2_host(const void *x, const void *y, void *out, size_t n,
                     KungFu_Datatype dt, KungFu_Op op)
 {
@@ -322,19 +350,45 @@ int transform2_host(const void *x, const void *y, void *out, size_t n,
     if (sz == 0 || dt == KungFu_BOOL) return KF_ERR_DTYPE;
     if (n == 0) return KF_OK;
     const size_t bytes = n * static_cast<size_t>(sz);
-    int rc             = t_staging.ensure(bytes);
+    const bool pinned  = bytes > kChunkBytes && is_pinned(x, bytes) &&
+                        is_pinned(y, bytes) && is_pinned(out, bytes);
+    int rc = t_staging.ensure(pinned ? kSlots * kChunkBytes : bytes);
     if (rc != KF_OK) return rc;
-    char *dx          = static_cast<char *>(t_staging.dev);
-    char *dy          = dx + t_staging.cap;
-    char *dz          = dy + t_staging.cap;
-    hipStream_t s     = t_staging.stream;
-    KF_HIP(hipMemcpyAsync(dx, x, bytes, hipMemcpyHostToDevice, s));
-    KF_HIP(hipMemcpyAsync(dy, y, bytes, hipMemcpyHostToDevice, s));
-    const void *ins[2] = {dx, dy};
-    rc                 = dispatch_none(ins, 2, dz, n, dt, op, s);
-    if (rc != KF_OK) return rc;
-    KF_HIP(hipMemcpyAsync(out, dz, bytes, hipMemcpyDeviceToHost, s));
-    KF_HIP(hipStreamSynchronize(s));
+    char *dx = static_cast<char *>(t_staging.dev);
+    char *dy = dx + t_staging.cap;
+    char *dz = dy + t_staging.cap;
+    if (!pinned) {
+        hipStream_t s = t_staging.stream[0];
+        KF_HIP(hipMemcpyAsync(dx, x, bytes, hipMemcpyHostToDevice, s));
+        KF_HIP(hipMemcpyAsync(dy, y, bytes, hipMemcpyHostToDevice, s));
+        const void *ins[2] = {dx, dy};
+        rc                 = dispatch_none(ins, 2, dz, n, dt, op, s);
+        if (rc != KF_OK) return rc;
+        KF_HIP(hipMemcpyAsync(out, dz, bytes, hipMemcpyDeviceToHost, s));
+        KF_HIP(hipStreamSynchronize(s));
+        return KF_OK;
+    }
+    const size_t chunk_elems = kChunkBytes / sz;
+    const char *hx = static_cast<const char *>(x);
+    const char *hy = static_cast<const char *>(y);
+    char *hz       = static_cast<char *>(out);
+    size_t i       = 0;
+    for (size_t b = 0; b < n; b += chunk_elems, ++i) {
+        const size_t m   = n - b < chunk_elems ? n - b : chunk_elems;
+        const size_t off = b * sz, len = m * sz;
+        const int slot   = static_cast<int>(i % kSlots);
+        hipStream_t s    = t_staging.stream[slot];
+        char *sx = dx + slot * kChunkBytes, *sy = dy + slot * kChunkBytes,
+             *sz_ = dz + slot * kChunkBytes;
+        // slot reuse is ordered by its own stream
+        KF_HIP(hipMemcpyAsync(sx, hx + off, len, hipMemcpyHostToDevice, s));
+        KF_HIP(hipMemcpyAsync(sy, hy + off, len, hipMemcpyHostToDevice, s));
+        const void *ins[2] = {sx, sy};
+        rc                 = dispatch_none(ins, 2, sz_, m, dt, op, s);
+        if (rc != KF_OK) return rc;
+        KF_HIP(hipMemcpyAsync(hz + off, sz_, len, hipMemcpyDeviceToHost, s));
+    }
+    for (auto &s : t_staging.stream) KF_HIP(hipStreamSynchronize(s));
     return KF_OK;
 }
 
@@ -444,6 +498,20 @@ int kf_set_geometry(int unroll, int grid_cap, int loadnt, int stplain)
     g.grid_cap  = grid_cap;
     g.loadnt    = loadnt ? 1 : 0;
     g.stplain   = stplain ? 1 : 0;
+    return KF_OK;
+}
+
+int kf_host_register(void *p, size_t bytes)
+{
+    if (!p || bytes == 0) return KF_ERR_ARG;
+    KF_HIP(hipHostRegister(p, bytes, hipHostRegisterDefault));
+    return KF_OK;
+}
+
+int kf_host_unregister(void *p)
+{
+    if (!p) return KF_ERR_ARG;
+    KF_HIP(hipHostUnregister(p));
     return KF_OK;
 }
 

@@ -1,0 +1,343 @@
+// kf_ingest.hip — host ingestion: KungFu's rchannel wire format and the
+// device-side recvOnto / sendInto steps of Session.runGraphs.
+//
+// Wire format (little-endian), restated from the reference:
+//   connection header  {u16 type, u16 src_port, u32 src_ipv4}   connection.go:73-80,
+//                                                               message.go:44-56
+//   connection ack     {u32 token}                              connection.go:28-40, 81-92
+//   message header     {u32 name_len, name bytes, u32 flags}    message.go:90-128
+//   message body       {u32 len, payload}                       message.go:160-198
+//   flags: WaitRecvBuf = 1 (receiver reads straight into its registered
+//   RecvBuf, handler/collective.go:43-61)
+//
+// Ingest: a peer chunk is read from the socket straight into a page-locked
+// slot, copied to HBM by the SDMA engine and folded onto the device-resident
+// accumulator by the same HIP kernel as kf_bucket_reduce — replacing
+// "Recv into a pooled Go []byte, then std_transform_2 on the host"
+// (session.go:255-264). Slots are reused round-robin; a slot is refilled only
+// after its previous H2D completed (per-slot event), so the socket read of
+// chunk i+1 overlaps the copy + fold of chunk i.
+#include <errno.h>
+#include <hip/hip_runtime.h>
+#include <sys/socket.h>
+#include <sys/uio.h>
+#include <unistd.h>
+
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "kungfu_amd.h"
+
+extern "C" const char *kf_last_error(void);
+
+namespace
+{
+thread_local std::string t_ingest_error;
+
+int io_fail(const char *what)
+{
+    t_ingest_error = std::string(what) + ": " + std::strerror(errno);
+    return KF_ERR_IO;
+}
+
+int proto_fail(const std::string &what)
+{
+    t_ingest_error = what;
+    return KF_ERR_PROTO;
+}
+
+int hip_fail(hipError_t e, const char *what)
+{
+    t_ingest_error = std::string(what) + ": " + hipGetErrorString(e);
+    return KF_ERR_HIP;
+}
+
+#define ING_HIP(call)                                                          \
+    do {                                                                       \
+        hipError_t e_ = (call);                                                \
+        if (e_ != hipSuccess) return hip_fail(e_, #call);                      \
+    } while (0)
+
+// readN (message.go:204-213): loop until exactly n bytes arrived
+int read_full(int fd, void *buf, size_t n)
+{
+    char *p = static_cast<char *>(buf);
+    while (n > 0) {
+        ssize_t r = ::read(fd, p, n);
+        if (r < 0) {
+            if (errno == EINTR) continue;
+            return io_fail("read");
+        }
+        if (r == 0) return proto_fail("unexpected end of stream");
+        p += r;
+        n -= static_cast<size_t>(r);
+    }
+    return KF_OK;
+}
+
+int write_full(int fd, struct iovec *iov, int cnt)
+{
+    while (cnt > 0) {
+        ssize_t w = ::writev(fd, iov, cnt);
+        if (w < 0) {
+            if (errno == EINTR) continue;
+            return io_fail("writev");
+        }
+        size_t left = static_cast<size_t>(w);
+        while (cnt > 0 && left >= iov->iov_len) {
+            left -= iov->iov_len;
+            ++iov;
+            --cnt;
+        }
+        if (cnt > 0) {
+            iov->iov_base = static_cast<char *>(iov->iov_base) + left;
+            iov->iov_len -= left;
+        }
+    }
+    return KF_OK;
+}
+
+inline void put_u32(unsigned char *p, uint32_t v)
+{
+    p[0] = v & 0xff;
+    p[1] = (v >> 8) & 0xff;
+    p[2] = (v >> 16) & 0xff;
+    p[3] = (v >> 24) & 0xff;
+}
+
+inline uint32_t get_u32(const unsigned char *p)
+{
+    return uint32_t(p[0]) | (uint32_t(p[1]) << 8) | (uint32_t(p[2]) << 16) |
+           (uint32_t(p[3]) << 24);
+}
+
+}  // namespace
+
+struct kf_ingest {
+    size_t slot_bytes = 0;
+    int nslots        = 0;
+    int next          = 0;
+    std::vector<void *> host;   // page-locked slots
+    std::vector<void *> dev;    // device slots
+    std::vector<hipEvent_t> done;
+    std::vector<bool> armed;
+    std::mutex mu;  // slot bookkeeping; callers may share one ingest object
+
+    ~kf_ingest()
+    {
+        for (auto e : done)
+            if (e) (void)hipEventDestroy(e);
+        for (auto p : dev)
+            if (p) (void)hipFree(p);
+        for (auto p : host)
+            if (p) (void)hipHostFree(p);
+    }
+
+    // next free slot: wait until its previous H2D has finished
+    int take(int *slot)
+    {
+        std::lock_guard<std::mutex> lock(mu);
+        const int s = next;
+        next        = (next + 1) % nslots;
+        if (armed[s]) {
+            ING_HIP(hipEventSynchronize(done[s]));
+            armed[s] = false;
+        }
+        *slot = s;
+        return KF_OK;
+    }
+};
+
+extern "C" {
+
+int kf_rch_client_handshake(int fd, uint16_t conn_type, uint16_t src_port,
+                            uint32_t src_ipv4, uint32_t expect_token)
+{
+    unsigned char h[8];
+    h[0] = conn_type & 0xff;
+    h[1] = conn_type >> 8;
+    h[2] = src_port & 0xff;
+    h[3] = src_port >> 8;
+    put_u32(h + 4, src_ipv4);
+    struct iovec iov = {h, sizeof(h)};
+    int rc           = write_full(fd, &iov, 1);
+    if (rc != KF_OK) return rc;
+    unsigned char a[4];
+    rc = read_full(fd, a, 4);
+    if (rc != KF_OK) return rc;
+    // connection.go:93-99: a token mismatch is fatal on collective connections
+    if (get_u32(a) != expect_token && conn_type == KF_RCH_CONN_COLLECTIVE) {
+        return proto_fail("invalid token");
+    }
+    return KF_OK;
+}
+
+int kf_rch_server_handshake(int fd, uint32_t token, uint16_t *conn_type,
+                            uint16_t *src_port, uint32_t *src_ipv4)
+{
+    unsigned char h[8];
+    int rc = read_full(fd, h, 8);
+    if (rc != KF_OK) return rc;
+    if (conn_type) *conn_type = uint16_t(h[0] | (h[1] << 8));
+    if (src_port) *src_port = uint16_t(h[2] | (h[3] << 8));
+    if (src_ipv4) *src_ipv4 = get_u32(h + 4);
+    unsigned char a[4];
+    put_u32(a, token);
+    struct iovec iov = {a, 4};
+    return write_full(fd, &iov, 1);
+}
+
+int kf_rch_send(int fd, const char *name, uint32_t flags, const void *data,
+                uint32_t len)
+{
+    if (!name || (len > 0 && !data)) return KF_ERR_ARG;
+    const uint32_t nl = static_cast<uint32_t>(std::strlen(name));
+    unsigned char a[4], b[4], c[4];
+    put_u32(a, nl);
+    put_u32(b, flags);
+    put_u32(c, len);
+    // tcpConnection.Send: header then message, one logical write (connection.go:149-165)
+    struct iovec iov[5] = {{a, 4},
+                           {const_cast<char *>(name), nl},
+                           {b, 4},
+                           {c, 4},
+                           {const_cast<void *>(data), len}};
+    return write_full(fd, iov, len > 0 ? 5 : 4);
+}
+
+int kf_rch_recv_header(int fd, char *name, uint32_t cap, uint32_t *name_len,
+                       uint32_t *flags)
+{
+    unsigned char a[4];
+    int rc = read_full(fd, a, 4);
+    if (rc != KF_OK) return rc;
+    const uint32_t nl = get_u32(a);
+    if (nl + 1 > cap || !name) return proto_fail("message name longer than buffer");
+    rc = read_full(fd, name, nl);
+    if (rc != KF_OK) return rc;
+    name[nl] = 0;
+    rc       = read_full(fd, a, 4);
+    if (rc != KF_OK) return rc;
+    if (name_len) *name_len = nl;
+    if (flags) *flags = get_u32(a);
+    return KF_OK;
+}
+
+int kf_rch_recv_body(int fd, void *dst, uint32_t expect_len)
+{
+    unsigned char a[4];
+    int rc = read_full(fd, a, 4);
+    if (rc != KF_OK) return rc;
+    // Message.ReadInto (message.go:184-198): the length must match the buffer
+    if (get_u32(a) != expect_len) return proto_fail("unexpected message length");
+    if (expect_len == 0) return KF_OK;
+    if (!dst) return KF_ERR_ARG;
+    return read_full(fd, dst, expect_len);
+}
+
+kf_ingest_t *kf_ingest_create(size_t slot_bytes, int nslots)
+{
+    if (slot_bytes == 0 || nslots < 1) return nullptr;
+    auto *g       = new kf_ingest;
+    g->slot_bytes = slot_bytes;
+    g->nslots     = nslots;
+    g->host.assign(nslots, nullptr);
+    g->dev.assign(nslots, nullptr);
+    g->done.assign(nslots, nullptr);
+    g->armed.assign(nslots, false);
+    for (int i = 0; i < nslots; ++i) {
+        if (hipHostMalloc(&g->host[i], slot_bytes, hipHostMallocDefault) != hipSuccess ||
+            hipMalloc(&g->dev[i], slot_bytes) != hipSuccess ||
+            hipEventCreateWithFlags(&g->done[i], hipEventDisableTiming) != hipSuccess) {
+            t_ingest_error = "kf_ingest_create: HIP allocation failed";
+            delete g;
+            return nullptr;
+        }
+    }
+    return g;
+}
+
+void kf_ingest_destroy(kf_ingest_t *g) { delete g; }
+
+int kf_ingest_recv_onto(kf_ingest_t *g, int fd, uint32_t len, void *dev_acc,
+                        const void *dev_own, size_t count, KungFu_Datatype dt,
+                        KungFu_Op op, void *stream)
+{
+    if (!g || !dev_acc) return KF_ERR_ARG;
+    if (len > g->slot_bytes) return proto_fail("chunk larger than ingest slot");
+    const uint32_t sz = kungfu_type_size(dt);
+    if (static_cast<size_t>(len) != count * sz) return proto_fail("chunk length != count * type size");
+    int slot;
+    int rc = g->take(&slot);
+    if (rc != KF_OK) return rc;
+    rc = kf_rch_recv_body(fd, g->host[slot], len);
+    if (rc != KF_OK) return rc;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    ING_HIP(hipMemcpyAsync(g->dev[slot], g->host[slot], len, hipMemcpyHostToDevice, s));
+    // Transform2(RecvBuf, effective, peer): own is SendBuf before the first
+    // receive, RecvBuf afterwards (session.go:241-264)
+    const void *ins[2] = {dev_own ? dev_own : dev_acc, g->dev[slot]};
+    rc                 = kf_bucket_reduce(ins, 2, dev_acc, count, dt, op, stream);
+    if (rc != KF_OK) return rc;
+    // the slot is free again once both the copy and the fold have run
+    ING_HIP(hipEventRecord(g->done[slot], s));
+    {
+        std::lock_guard<std::mutex> lock(g->mu);
+        g->armed[slot] = true;
+    }
+    return KF_OK;
+}
+
+int kf_ingest_recv_into(kf_ingest_t *g, int fd, uint32_t len, void *dev_dst,
+                        void *stream)
+{
+    if (!g || (!dev_dst && len > 0)) return KF_ERR_ARG;
+    if (len > g->slot_bytes) return proto_fail("chunk larger than ingest slot");
+    int slot;
+    int rc = g->take(&slot);
+    if (rc != KF_OK) return rc;
+    rc = kf_rch_recv_body(fd, g->host[slot], len);
+    if (rc != KF_OK || len == 0) return rc;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    ING_HIP(hipMemcpyAsync(dev_dst, g->host[slot], len, hipMemcpyHostToDevice, s));
+    ING_HIP(hipEventRecord(g->done[slot], s));
+    {
+        std::lock_guard<std::mutex> lock(g->mu);
+        g->armed[slot] = true;
+    }
+    return KF_OK;
+}
+
+int kf_ingest_send_from_device(kf_ingest_t *g, int fd, const char *name,
+                               uint32_t flags, const void *dev_src, size_t bytes,
+                               void *stream)
+{
+    if (!g || !dev_src || !name) return KF_ERR_ARG;
+    if (bytes > g->slot_bytes) return proto_fail("chunk larger than ingest slot");
+    int slot;
+    int rc = g->take(&slot);
+    if (rc != KF_OK) return rc;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    ING_HIP(hipMemcpyAsync(g->host[slot], dev_src, bytes, hipMemcpyDeviceToHost, s));
+    ING_HIP(hipStreamSynchronize(s));
+    return kf_rch_send(fd, name, flags, g->host[slot], static_cast<uint32_t>(bytes));
+}
+
+int kf_ingest_sync(kf_ingest_t *g)
+{
+    if (!g) return KF_ERR_ARG;
+    std::lock_guard<std::mutex> lock(g->mu);
+    for (int i = 0; i < g->nslots; ++i) {
+        if (g->armed[i]) {
+            ING_HIP(hipEventSynchronize(g->done[i]));
+            g->armed[i] = false;
+        }
+    }
+    return KF_OK;
+}
+
+const char *kf_ingest_last_error(void) { return t_ingest_error.c_str(); }
+
+}  // extern "C"

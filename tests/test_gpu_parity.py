@@ -340,3 +340,33 @@ def test_optimizers_world1_on_gpu(orc, dev):
         vh = v.cpu().numpy().reshape(-1)
         want = orc.sma_blend(vh, vh, "f32", 1, 0.1)
         assert np.array_equal(p.detach().cpu().numpy().reshape(-1), want)
+
+
+def test_host_paths_pageable_and_pinned(lib, orc):
+    # kf_transform2_host: pageable (runtime staging) and pinned (16 MiB
+    # chunks over two streams, ragged last chunk) give the oracle's bits
+    rng = np.random.default_rng(21)
+    n = (40 << 20) // 4 + 12345  # 40 MiB + ragged
+    x = rng.standard_normal(n).astype(np.float32)
+    y = rng.standard_normal(n).astype(np.float32)
+    want = orc.transform2(x, y, "f32", "sum")
+    z = np.empty_like(x)
+    assert lib.kf_transform2_host(x.ctypes.data, y.ctypes.data, z.ctypes.data, n,
+                                  0x20408, 0) == 0
+    assert np.array_equal(z, want)
+    tx = torch.from_numpy(x).pin_memory()
+    ty = torch.from_numpy(y).pin_memory()
+    tz = torch.empty_like(tx).pin_memory()
+    assert lib.kf_transform2_host(tx.data_ptr(), ty.data_ptr(), tz.data_ptr(), n,
+                                  0x20408, 0) == 0
+    assert np.array_equal(tz.numpy(), want)
+    # registered (not hipHostMalloc'ed) numpy memory also takes the DMA path
+    z2 = np.zeros_like(x)
+    for a in (x, y, z2):
+        assert lib.kf_host_register(a.ctypes.data, a.nbytes) == 0
+    try:
+        lib.std_transform_2(x.ctypes.data, y.ctypes.data, z2.ctypes.data, n, 0x20408, 0)
+        assert np.array_equal(z2, want)
+    finally:
+        for a in (x, y, z2):
+            lib.kf_host_unregister(a.ctypes.data)

@@ -1,0 +1,126 @@
+"""Single-host Session (kungfu_amd/session.py) over the rchannel wire format:
+np peers as processes on unix sockets, STAR strategy, chunked by 1 MiB.
+Host mode runs on CPU with the oracle as the injected fold; device mode
+(pinned ingest + HIP fold) is the -m gpu variant. Expected values: the
+reference KATs and the oracle folded in every possible arrival order."""
+import itertools
+import os
+import sys
+import tempfile
+import traceback
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+
+def oracle_reduce_fn(x, y, out, n, dt, op):
+    from oracle import oracle
+    rc = oracle.lib().oracle_transform2(x, y, out, n, dt, op)
+    assert rc == 0
+
+
+def inputs(rank, n, kind):
+    if kind == "iota":  # fake_agent.cpp:15-44
+        return np.arange(n, dtype=np.int32)
+    if kind == "c1":  # x_r[i] = (r+1) * (i mod 1024) / 1024
+        return ((rank + 1) * (np.arange(n) % 1024) / 1024).astype(np.float32)
+    return np.random.default_rng(40 + rank).standard_normal(n).astype(np.float32)
+
+
+def _body(rank, size, sock_dir, mode, kind, n, errq):
+    sys.path[:0] = [ROOT, HERE]
+    try:
+        from kungfu_amd.session import Session
+        if mode == "device":
+            import torch
+            dev = torch.device("cuda:0")
+            x = torch.from_numpy(inputs(rank, n, kind)).to(dev)
+            y = torch.zeros_like(x)
+            s = Session(rank, size, sock_dir, mode="device")
+            s.all_reduce(x, y, "NegotiatedGrad_0/AllReduce")
+            got = y.cpu().numpy()
+            z = x.clone()
+            s.all_reduce(z, z, "inplace")  # in place: SendBuf is RecvBuf
+            got_inplace = z.cpu().numpy()
+        else:
+            x = inputs(rank, n, kind)
+            y = np.zeros_like(x)
+            s = Session(rank, size, sock_dir, mode="host", reduce_fn=oracle_reduce_fn)
+            s.all_reduce(x, y, "NegotiatedGrad_0/AllReduce")
+            got = y
+            z = x.copy()
+            s.all_reduce(z, z, "inplace")
+            got_inplace = z
+        s.close()
+        check(rank, size, kind, n, got)
+        check(rank, size, kind, n, got_inplace)
+    except Exception:
+        errq.put("rank %d: %s" % (rank, traceback.format_exc()))
+
+
+def check(rank, size, kind, n, got):
+    from oracle import oracle
+    xs = [inputs(r, n, kind) for r in range(size)]
+    if kind == "iota":
+        assert np.array_equal(got, np.arange(n, dtype=np.int32) * size)
+        return
+    if kind == "c1":
+        assert np.array_equal(got, sum(xs))  # exact in fp32
+        return
+    # arrival order may differ per chunk: each chunk must equal the root's
+    # fold x0 o x_a o x_b ... for SOME order of the peers
+    k = (n * 4 + (1 << 20) - 1) >> 20
+    from kungfu_amd.base import EvenPartition
+    for b, e in EvenPartition(0, n, k):
+        opts = [oracle.reduce_k([xs[0][b:e]] + [xs[p][b:e] for p in perm], "f32")
+                for perm in itertools.permutations(range(1, size))]
+        assert any(np.array_equal(got[b:e], o) for o in opts), (rank, b, e)
+
+
+def run(size, mode, kind, n):
+    ctx = mp.get_context("spawn")
+    errq = ctx.SimpleQueue()
+    with tempfile.TemporaryDirectory() as d:
+        ps = [ctx.Process(target=_body, args=(r, size, d, mode, kind, n, errq))
+              for r in range(size)]
+        for p in ps:
+            p.start()
+        for p in ps:
+            p.join(timeout=300)
+    errs = []
+    while not errq.empty():
+        errs.append(errq.get())
+    assert not errs, "\n".join(errs)
+    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+
+
+@pytest.mark.parametrize("size,kind,n", [(2, "iota", 8), (3, "iota", 12),
+                                         (2, "c1", 1 << 20), (2, "rand", 300007),
+                                         (3, "rand", 600011)])
+def test_session_host_mode(size, kind, n):
+    run(size, "host", kind, n)
+
+
+def test_session_single_peer_forward():
+    from kungfu_amd.session import Session
+    with tempfile.TemporaryDirectory() as d:
+        s = Session(0, 1, d, mode="host", reduce_fn=oracle_reduce_fn)
+        x = np.arange(10, dtype=np.int32) + 1
+        y = np.zeros_like(x)
+        s.all_reduce(x, y, "t")
+        assert np.array_equal(y, x)  # test_operations.cpp:3-26
+        s.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("size,kind,n", [(2, "c1", 1 << 20), (2, "rand", 300007),
+                                         (3, "rand", 600011), (2, "iota", 8)])
+def test_session_device_mode(size, kind, n):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    run(size, "device", kind, n)
