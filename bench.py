@@ -216,11 +216,8 @@ def c1_child(args):
         fn = None
         if args.c1_mode == "cpu":
             from oracle import oracle
-            olib = oracle.lib()
-
-            def fn(a, b, out, n, dt, op):
-                olib.oracle_transform2(a, b, out, n, dt, op)
-        sess = Session(r, 2, args.c1_dir, mode="host", reduce_fn=fn)
+            fn = ctypes.cast(oracle.lib().oracle_transform2, ctypes.c_void_p)
+        sess = Session(r, 2, args.c1_dir, mode="host", host_reduce_fn=fn)
         result = lambda: ys  # noqa: E731
     name = "NegotiatedGrad_0/AllReduce"
     for _ in range(args.warmup):

@@ -205,6 +205,33 @@ int kf_ingest_send_from_device(kf_ingest_t *g, int fd, const char *name,
 int kf_ingest_sync(kf_ingest_t *g);
 const char *kf_ingest_last_error(void);
 
+/* ---- single-host session engine (collective boundary) ---- */
+
+/* Host-mode fold callback: out = x op y over n elements; 0 = ok. */
+typedef int (*kf_host_reduce_fn)(const void *x, const void *y, void *out,
+                                 int64_t n, int dt, int op);
+
+typedef struct kf_session kf_session_t;
+
+/* Peer `rank` of `size` on this host: listens on
+ * <sock_dir>/kungfu-amd-<10000+rank>.sock and connects to the peers the STAR
+ * strategy needs (rchannel handshake with `token`). device_mode = 1: buffers
+ * passed to kf_session_all_reduce are HBM pointers; 0: host pointers. NULL on
+ * failure (kf_session_last_error). */
+kf_session_t *kf_session_create(int rank, int size, const char *sock_dir,
+                                uint32_t token, int device_mode);
+/* Host mode only: fold with `fn` instead of std_transform_2. */
+int kf_session_set_host_reduce(kf_session_t *s, kf_host_reduce_fn fn);
+/* Synchronous all-reduce of one bucket: the counterpart of
+ * GoKungfuAllReduce(sendBuf, recvBuf, count, dtype, op, name, done = nil)
+ * (srcs/go/libkungfu-comm/collective.go:34-45). send == recv is in place.
+ * Every peer must call it with the same name, count, dtype and op. */
+int kf_session_all_reduce(kf_session_t *s, const void *send, void *recv,
+                          size_t count, KungFu_Datatype dt, KungFu_Op op,
+                          const char *name, void *stream);
+void kf_session_destroy(kf_session_t *s);
+const char *kf_session_last_error(void);
+
 #ifdef __cplusplus
 }
 #endif

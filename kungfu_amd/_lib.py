@@ -38,6 +38,11 @@ EXPORTED = (
     "kf_ingest_send_from_device",
     "kf_ingest_sync",
     "kf_ingest_last_error",
+    "kf_session_create",
+    "kf_session_set_host_reduce",
+    "kf_session_all_reduce",
+    "kf_session_destroy",
+    "kf_session_last_error",
 )
 
 STATUS = {
@@ -138,6 +143,17 @@ def load():
     lib.kf_ingest_sync.restype = c_int
     lib.kf_ingest_last_error.argtypes = []
     lib.kf_ingest_last_error.restype = ctypes.c_char_p
+    lib.kf_session_create.argtypes = [c_int, c_int, ctypes.c_char_p, u32, c_int]
+    lib.kf_session_create.restype = c_void_p
+    lib.kf_session_set_host_reduce.argtypes = [c_void_p, c_void_p]
+    lib.kf_session_set_host_reduce.restype = c_int
+    lib.kf_session_all_reduce.argtypes = [c_void_p, c_void_p, c_void_p, c_size_t, c_int,
+                                          c_int, ctypes.c_char_p, c_void_p]
+    lib.kf_session_all_reduce.restype = c_int
+    lib.kf_session_destroy.argtypes = [c_void_p]
+    lib.kf_session_destroy.restype = None
+    lib.kf_session_last_error.argtypes = []
+    lib.kf_session_last_error.restype = ctypes.c_char_p
     _lib = lib
     return lib
 
@@ -145,7 +161,8 @@ def load():
 def check(rc, what):
     if rc != 0:
         lib = load()
-        detail = lib.kf_last_error().decode() or lib.kf_ingest_last_error().decode()
+        detail = (lib.kf_session_last_error().decode() or lib.kf_last_error().decode()
+                  or lib.kf_ingest_last_error().decode())
         raise KungFuAMDError("%s failed: %s (%s)" % (what, STATUS.get(rc, rc), detail))
 
 

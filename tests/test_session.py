@@ -17,10 +17,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 
 
-def oracle_reduce_fn(x, y, out, n, dt, op):
+def oracle_reduce_fn():
+    """C address of the oracle's transform2 (kf_host_reduce_fn signature)."""
+    import ctypes
     from oracle import oracle
-    rc = oracle.lib().oracle_transform2(x, y, out, n, dt, op)
-    assert rc == 0
+    return ctypes.cast(oracle.lib().oracle_transform2, ctypes.c_void_p)
 
 
 def inputs(rank, n, kind):
@@ -49,7 +50,7 @@ def _body(rank, size, sock_dir, mode, kind, n, errq):
         else:
             x = inputs(rank, n, kind)
             y = np.zeros_like(x)
-            s = Session(rank, size, sock_dir, mode="host", reduce_fn=oracle_reduce_fn)
+            s = Session(rank, size, sock_dir, mode="host", host_reduce_fn=oracle_reduce_fn())
             s.all_reduce(x, y, "NegotiatedGrad_0/AllReduce")
             got = y
             z = x.copy()
@@ -108,7 +109,7 @@ def test_session_host_mode(size, kind, n):
 def test_session_single_peer_forward():
     from kungfu_amd.session import Session
     with tempfile.TemporaryDirectory() as d:
-        s = Session(0, 1, d, mode="host", reduce_fn=oracle_reduce_fn)
+        s = Session(0, 1, d, mode="host", host_reduce_fn=oracle_reduce_fn())
         x = np.arange(10, dtype=np.int32) + 1
         y = np.zeros_like(x)
         s.all_reduce(x, y, "t")
