@@ -63,6 +63,20 @@ enum KungFu_Op {
 };
 typedef enum KungFu_Op KungFu_Op;
 
+/* srcs/cpp/include/kungfu/strategy.h:7-17 */
+enum KungFu_Strategy {
+    KungFu_Tree                = 0,
+    KungFu_BinaryTree          = 1,
+    KungFu_Ring                = 2,
+    KungFu_Star                = 3,
+    KungFu_MultiStar           = 4,
+    KungFu_Clique              = 5,
+    KungFu_BinaryTreeStar      = 6,
+    KungFu_MultiBinaryTreeStar = 7,
+    KungFu_AUTO                = 8,
+};
+typedef enum KungFu_Strategy KungFu_Strategy;
+
 /* ---- B1: drop-in host-pointer entry points ------------------------------ */
 
 /* out[i] = o(input1[i], input2[i]) for i < n. out may alias input1 or input2
@@ -201,6 +215,14 @@ int kf_ingest_recv_into(kf_ingest_t *g, int fd, uint32_t len, void *dev_dst,
 int kf_ingest_send_from_device(kf_ingest_t *g, int fd, const char *name,
                                uint32_t flags, const void *dev_src, size_t bytes,
                                void *stream);
+/* The same two steps for a chunk already in host memory (a message read
+ * ahead of its all-reduce and kept, as the reference's per-name mailbox
+ * does, handler/collective.go:27-41). */
+int kf_ingest_fold_host(kf_ingest_t *g, const void *host, uint32_t len,
+                        void *dev_acc, const void *dev_own, size_t count,
+                        KungFu_Datatype dt, KungFu_Op op, void *stream);
+int kf_ingest_copy_host(kf_ingest_t *g, const void *host, uint32_t len,
+                        void *dev_dst, void *stream);
 /* Wait for every queued slot copy. */
 int kf_ingest_sync(kf_ingest_t *g);
 const char *kf_ingest_last_error(void);
@@ -214,12 +236,17 @@ typedef int (*kf_host_reduce_fn)(const void *x, const void *y, void *out,
 typedef struct kf_session kf_session_t;
 
 /* Peer `rank` of `size` on this host: listens on
- * <sock_dir>/kungfu-amd-<10000+rank>.sock and connects to the peers the STAR
- * strategy needs (rchannel handshake with `token`). device_mode = 1: buffers
- * passed to kf_session_all_reduce are HBM pointers; 0: host pointers. NULL on
+ * <sock_dir>/kungfu-amd-<10000+rank>.sock and connects to every other peer
+ * (rchannel handshake with `token`). The strategy and chunk hash come from
+ * KUNGFU_ALLREDUCE_STRATEGY / KUNGFU_CONFIG_STRATEGY_HASH_METHOD as in the
+ * reference (default BINARY_TREE_STAR, NAME). device_mode = 1: buffers passed
+ * to kf_session_all_reduce are HBM pointers; 0: host pointers. NULL on
  * failure (kf_session_last_error). */
 kf_session_t *kf_session_create(int rank, int size, const char *sock_dir,
                                 uint32_t token, int device_mode);
+/* Override the strategy (KungFu_Strategy) and chunk hash (1 = NAME,
+ * 0 = SIMPLE); every peer must use the same. */
+int kf_session_set_strategy(kf_session_t *s, int strategy, int hash_by_name);
 /* Host mode only: fold with `fn` instead of std_transform_2. */
 int kf_session_set_host_reduce(kf_session_t *s, kf_host_reduce_fn fn);
 /* Synchronous all-reduce of one bucket: the counterpart of

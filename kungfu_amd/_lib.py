@@ -36,9 +36,12 @@ EXPORTED = (
     "kf_ingest_recv_onto",
     "kf_ingest_recv_into",
     "kf_ingest_send_from_device",
+    "kf_ingest_fold_host",
+    "kf_ingest_copy_host",
     "kf_ingest_sync",
     "kf_ingest_last_error",
     "kf_session_create",
+    "kf_session_set_strategy",
     "kf_session_set_host_reduce",
     "kf_session_all_reduce",
     "kf_session_destroy",
@@ -145,6 +148,13 @@ def load():
     lib.kf_ingest_last_error.restype = ctypes.c_char_p
     lib.kf_session_create.argtypes = [c_int, c_int, ctypes.c_char_p, u32, c_int]
     lib.kf_session_create.restype = c_void_p
+    lib.kf_session_set_strategy.argtypes = [c_void_p, c_int, c_int]
+    lib.kf_session_set_strategy.restype = c_int
+    lib.kf_ingest_fold_host.argtypes = [c_void_p, c_void_p, u32, c_void_p, c_void_p,
+                                        c_size_t, c_int, c_int, c_void_p]
+    lib.kf_ingest_fold_host.restype = c_int
+    lib.kf_ingest_copy_host.argtypes = [c_void_p, c_void_p, u32, c_void_p, c_void_p]
+    lib.kf_ingest_copy_host.restype = c_int
     lib.kf_session_set_host_reduce.argtypes = [c_void_p, c_void_p]
     lib.kf_session_set_host_reduce.restype = c_int
     lib.kf_session_all_reduce.argtypes = [c_void_p, c_void_p, c_void_p, c_size_t, c_int,

@@ -82,6 +82,17 @@ bool is_float(KungFu_Datatype dt)
            dt == KungFu_DOUBLE;
 }
 
+Div make_div(int np)
+{
+    Div d;
+    d.f    = static_cast<float>(np);
+    d.d    = static_cast<double>(np);
+    d.pow2 = np > 0 && (np & (np - 1)) == 0;
+    d.fi   = 1.0f / d.f;  // exact for powers of two
+    d.di   = 1.0 / d.d;
+    return d;
+}
+
 // ---------------------------------------------------------------------------
 // launch helpers
 // ---------------------------------------------------------------------------
@@ -123,7 +134,7 @@ unsigned grid_for(size_t nvec, size_t nedge, int unroll)
 
 template <typename T, int OP, int EPI, int KC, int UNROLL, int LOADNT, int STPLAIN = 0>
 void launch_vec(const InPtrs &ptrs, int k, void *out, size_t n, const Plan &p,
-                int np, hipStream_t s)
+                const Div &np, hipStream_t s)
 {
     constexpr int V  = Vec<typename Elt<T>::S>::N;
     const size_t ned = p.head + (n - p.head - p.nvec * V);
@@ -137,7 +148,7 @@ void launch_vec(const InPtrs &ptrs, int k, void *out, size_t n, const Plan &p,
 // non-temporal loads and stores).
 template <typename T, int OP, int EPI, int KC, int LOADNT, int STPLAIN>
 void launch_unroll(const InPtrs &ptrs, int k, void *out, size_t n, const Plan &p,
-                   int np, hipStream_t s)
+                   const Div &np, hipStream_t s)
 {
     switch (geometry().unroll) {
     case 1: return launch_vec<T, OP, EPI, KC, 1, LOADNT, STPLAIN>(ptrs, k, out, n, p, np, s);
@@ -149,7 +160,7 @@ void launch_unroll(const InPtrs &ptrs, int k, void *out, size_t n, const Plan &p
 
 template <typename T, int OP, int EPI, int KC>
 void launch_geom(const InPtrs &ptrs, int k, void *out, size_t n, const Plan &p,
-                 int np, hipStream_t s)
+                 const Div &np, hipStream_t s)
 {
     const Geometry &g = geometry();
     if constexpr (std::is_same<T, float>::value && OP == OP_SUM && KC == 2 &&
@@ -159,13 +170,41 @@ void launch_geom(const InPtrs &ptrs, int k, void *out, size_t n, const Plan &p,
         if (g.stplain) return launch_unroll<T, OP, EPI, KC, 0, 1>(ptrs, k, out, n, p, np, s);
         return launch_unroll<T, OP, EPI, KC, 0, 0>(ptrs, k, out, n, p, np, s);
     }
-    launch_vec<T, OP, EPI, KC, 4, 1>(ptrs, k, out, n, p, np, s);
+    // about 8 16-B loads in flight per thread whatever k is
+    constexpr int U = KC == 0 || KC <= 2 ? 4 : KC <= 4 ? 2 : 1;
+    launch_vec<T, OP, EPI, KC, U, 1>(ptrs, k, out, n, p, np, s);
+}
+
+// SUM folds of the gradient dtypes get a compile-time input count for
+// k = 3..8 (all k loads in flight); everything else runs the runtime-k loop.
+template <typename T, int OP, int EPI>
+void launch_k(const InPtrs &ptrs, int k, void *out, size_t n, const Plan &p,
+              const Div &np, hipStream_t s)
+{
+    if (k == 2) return launch_geom<T, OP, EPI, 2>(ptrs, k, out, n, p, np, s);
+    constexpr bool fast = OP == OP_SUM && (std::is_same<T, float>::value ||
+                                           std::is_same<T, f16_t>::value ||
+                                           std::is_same<T, bf16_t>::value);
+    if constexpr (fast) {
+        switch (k) {
+        case 1: return launch_geom<T, OP, EPI, 1>(ptrs, k, out, n, p, np, s);
+        case 3: return launch_geom<T, OP, EPI, 3>(ptrs, k, out, n, p, np, s);
+        case 4: return launch_geom<T, OP, EPI, 4>(ptrs, k, out, n, p, np, s);
+        case 5: return launch_geom<T, OP, EPI, 5>(ptrs, k, out, n, p, np, s);
+        case 6: return launch_geom<T, OP, EPI, 6>(ptrs, k, out, n, p, np, s);
+        case 7: return launch_geom<T, OP, EPI, 7>(ptrs, k, out, n, p, np, s);
+        case 8: return launch_geom<T, OP, EPI, 8>(ptrs, k, out, n, p, np, s);
+        default: break;
+        }
+    }
+    launch_geom<T, OP, EPI, 0>(ptrs, k, out, n, p, np, s);
 }
 
 template <typename T, int OP, int EPI>
-int launch_typed(const void *const *in, int k, void *out, size_t n, int np,
+int launch_typed(const void *const *in, int k, void *out, size_t n, int npi,
                  hipStream_t s)
 {
+    const Div np = make_div(npi);
     using S = typename Elt<T>::S;
     InPtrs ptrs;
     for (int j = 0; j < kMaxInputs; ++j) ptrs.p[j] = j < k ? in[j] : nullptr;
@@ -175,10 +214,8 @@ int launch_typed(const void *const *in, int k, void *out, size_t n, int np,
         if (blocks > 8192) blocks = 8192;
         reduce_kernel_unaligned<T, OP, EPI, kBlock>
             <<<static_cast<unsigned>(blocks), kBlock, 0, s>>>(ptrs, k, out, n, np);
-    } else if (k == 2) {
-        launch_geom<T, OP, EPI, 2>(ptrs, k, out, n, p, np, s);
     } else {
-        launch_geom<T, OP, EPI, 0>(ptrs, k, out, n, p, np, s);
+        launch_k<T, OP, EPI>(ptrs, k, out, n, p, np, s);
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "reduce kernel launch");
@@ -268,7 +305,7 @@ int launch_sma(void *v, const void *sum, size_t n, int np, C c1, C c2,
         if (blocks > 8192) blocks = 8192;
     }
     sma_kernel<T, C, kBlock, 4><<<static_cast<unsigned>(blocks), kBlock, 0, s>>>(
-        v, sum, n, p.head, p.nvec, c1, c2, np, p.vec_ok ? 1 : 0);
+        v, sum, n, p.head, p.nvec, c1, c2, make_div(np), p.vec_ok ? 1 : 0);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "sma kernel launch");
     return KF_OK;

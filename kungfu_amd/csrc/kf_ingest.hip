@@ -30,8 +30,6 @@
 
 #include "kungfu_amd.h"
 
-extern "C" const char *kf_last_error(void);
-
 namespace
 {
 thread_local std::string t_ingest_error;
@@ -323,6 +321,48 @@ int kf_ingest_send_from_device(kf_ingest_t *g, int fd, const char *name,
     ING_HIP(hipMemcpyAsync(g->host[slot], dev_src, bytes, hipMemcpyDeviceToHost, s));
     ING_HIP(hipStreamSynchronize(s));
     return kf_rch_send(fd, name, flags, g->host[slot], static_cast<uint32_t>(bytes));
+}
+
+int kf_ingest_fold_host(kf_ingest_t *g, const void *host, uint32_t len, void *dev_acc,
+                        const void *dev_own, size_t count, KungFu_Datatype dt, KungFu_Op op,
+                        void *stream)
+{
+    if (!g || !dev_acc || (!host && len > 0)) return KF_ERR_ARG;
+    if (len > g->slot_bytes) return proto_fail("chunk larger than ingest slot");
+    int slot;
+    int rc = g->take(&slot);
+    if (rc != KF_OK) return rc;
+    std::memcpy(g->host[slot], host, len);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    ING_HIP(hipMemcpyAsync(g->dev[slot], g->host[slot], len, hipMemcpyHostToDevice, s));
+    const void *ins[2] = {dev_own ? dev_own : dev_acc, g->dev[slot]};
+    rc                 = kf_bucket_reduce(ins, 2, dev_acc, count, dt, op, stream);
+    if (rc != KF_OK) return rc;
+    ING_HIP(hipEventRecord(g->done[slot], s));
+    {
+        std::lock_guard<std::mutex> lock(g->mu);
+        g->armed[slot] = true;
+    }
+    return KF_OK;
+}
+
+int kf_ingest_copy_host(kf_ingest_t *g, const void *host, uint32_t len, void *dev_dst,
+                        void *stream)
+{
+    if (!g || (!dev_dst && len > 0) || (!host && len > 0)) return KF_ERR_ARG;
+    if (len > g->slot_bytes) return proto_fail("chunk larger than ingest slot");
+    int slot;
+    int rc = g->take(&slot);
+    if (rc != KF_OK || len == 0) return rc;
+    std::memcpy(g->host[slot], host, len);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    ING_HIP(hipMemcpyAsync(dev_dst, g->host[slot], len, hipMemcpyHostToDevice, s));
+    ING_HIP(hipEventRecord(g->done[slot], s));
+    {
+        std::lock_guard<std::mutex> lock(g->mu);
+        g->armed[slot] = true;
+    }
+    return KF_OK;
 }
 
 int kf_ingest_sync(kf_ingest_t *g)

@@ -31,6 +31,15 @@ namespace kf
 enum Op { OP_SUM = 0, OP_MIN = 1, OP_MAX = 2, OP_PROD = 3 };
 enum Epi { EPI_NONE = 0, EPI_DIV = 1 };
 
+// The 1/np epilogue divisor. For np a power of two, x * 2^-k and x / 2^k are
+// the same correctly rounded value, so the multiply is used (bit-identical,
+// no software division); otherwise a true IEEE division (TF's g / np).
+struct Div {
+    float f, fi;
+    double d, di;
+    int pow2;
+};
+
 // Storage tags for the two 16-bit float formats (stored as raw u16 bits).
 struct f16_t {
     uint16_t bits;
@@ -122,9 +131,9 @@ template <> struct Elt<float> {
             return (a < b) ? b : a;
         }
     }
-    __device__ static S div(Acc a, int np)
+    __device__ static S div(Acc a, const Div &dv)
     {
-        return __fdiv_rn(a, static_cast<float>(np));
+        return dv.pow2 ? __fmul_rn(a, dv.fi) : __fdiv_rn(a, dv.f);
     }
 };
 
@@ -145,9 +154,9 @@ template <> struct Elt<double> {
             return (a < b) ? b : a;
         }
     }
-    __device__ static S div(Acc a, int np)
+    __device__ static S div(Acc a, const Div &dv)
     {
-        return __ddiv_rn(a, static_cast<double>(np));
+        return dv.pow2 ? __dmul_rn(a, dv.di) : __ddiv_rn(a, dv.d);
     }
 };
 
@@ -164,9 +173,10 @@ template <> struct Elt<f16_t> {
         static_assert(OP == OP_SUM, "fp16 supports SUM only");
         return f32_to_f16(__fadd_rn(f16_to_f32(a), f16_to_f32(b)));
     }
-    __device__ static S div(Acc a, int np)
+    __device__ static S div(Acc a, const Div &dv)
     {
-        return f32_to_f16(__fdiv_rn(f16_to_f32(a), static_cast<float>(np)));
+        const float x = f16_to_f32(a);
+        return f32_to_f16(dv.pow2 ? __fmul_rn(x, dv.fi) : __fdiv_rn(x, dv.f));
     }
 };
 
@@ -201,9 +211,9 @@ template <> struct Elt<bf16_t> {
             return a.bits;
         }
     }
-    __device__ static S div(Acc a, int np)
+    __device__ static S div(Acc a, const Div &dv)
     {
-        return f32_to_bf16(__fdiv_rn(a.f, static_cast<float>(np)));
+        return f32_to_bf16(dv.pow2 ? __fmul_rn(a.f, dv.fi) : __fdiv_rn(a.f, dv.f));
     }
 };
 
@@ -269,7 +279,7 @@ __device__ __forceinline__ void st_vec(void *base, size_t vi, const Vec<S> &v)
 // Fold one element across the k inputs (runtime k).
 template <typename T, int OP, int EPI>
 __device__ __forceinline__ typename Elt<T>::S
-fold_scalar(const InPtrs &in, int k, size_t i, int np)
+fold_scalar(const InPtrs &in, int k, size_t i, const Div &np)
 {
     using S   = typename Elt<T>::S;
     auto acc  = Elt<T>::load(reinterpret_cast<const S *>(in.p[0])[i]);
@@ -295,7 +305,7 @@ template <typename T, int OP, int EPI, int KC, int BLOCK, int UNROLL, int LOADNT
           int STPLAIN = 0>
 __global__ void __launch_bounds__(BLOCK)
     reduce_kernel(InPtrs in, int k, void *out, size_t n, size_t head,
-                  size_t nvec, int np)
+                  size_t nvec, Div np)
 {
     using S         = typename Elt<T>::S;
     using Acc       = typename Elt<T>::Acc;
@@ -329,29 +339,49 @@ __global__ void __launch_bounds__(BLOCK)
     for (size_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const size_t v0 = t * tile + threadIdx.x;
         if (v0 + (UNROLL - 1) * BLOCK < nvec) {
-            // full tile: UNROLL loads of inputs 0 and 1 issued before any use
-            Vec<S> a[UNROLL];
-            Vec<S> b[UNROLL];
-            const char *s0 = src(0);
-#pragma unroll
-            for (int u = 0; u < UNROLL; ++u) a[u] = ld_vec<S, LOADNT>(s0, v0 + u * BLOCK);
-            if (kk > 1) {
-                const char *s1 = src(1);
-#pragma unroll
-                for (int u = 0; u < UNROLL; ++u) b[u] = ld_vec<S, LOADNT>(s1, v0 + u * BLOCK);
-            }
             Acc acc[UNROLL][V];
+            if constexpr (KC > 0) {
+                // compile-time k: all KC x UNROLL loads issued before any use
+                Vec<S> v[KC][UNROLL];
 #pragma unroll
-            for (int u = 0; u < UNROLL; ++u) {
+                for (int j = 0; j < KC; ++j) {
+                    const char *sj = src(j);
 #pragma unroll
-                for (int e = 0; e < V; ++e) {
-                    acc[u][e] = Elt<T>::load(a[u].e[e]);
-                    if (kk > 1) {
-                        acc[u][e] = Elt<T>::template combine<OP>(acc[u][e], b[u].e[e]);
+                    for (int u = 0; u < UNROLL; ++u) v[j][u] = ld_vec<S, LOADNT>(sj, v0 + u * BLOCK);
+                }
+#pragma unroll
+                for (int u = 0; u < UNROLL; ++u) {
+#pragma unroll
+                    for (int e = 0; e < V; ++e) {
+                        acc[u][e] = Elt<T>::load(v[0][u].e[e]);
+#pragma unroll
+                        for (int j = 1; j < KC; ++j) {
+                            acc[u][e] = Elt<T>::template combine<OP>(acc[u][e], v[j][u].e[e]);
+                        }
                     }
                 }
-            }
-            if constexpr (KC != 2) {
+            } else {
+                // runtime k: inputs 0 and 1 up front, then one input at a time
+                Vec<S> a[UNROLL];
+                Vec<S> b[UNROLL];
+                const char *s0 = src(0);
+#pragma unroll
+                for (int u = 0; u < UNROLL; ++u) a[u] = ld_vec<S, LOADNT>(s0, v0 + u * BLOCK);
+                if (kk > 1) {
+                    const char *s1 = src(1);
+#pragma unroll
+                    for (int u = 0; u < UNROLL; ++u) b[u] = ld_vec<S, LOADNT>(s1, v0 + u * BLOCK);
+                }
+#pragma unroll
+                for (int u = 0; u < UNROLL; ++u) {
+#pragma unroll
+                    for (int e = 0; e < V; ++e) {
+                        acc[u][e] = Elt<T>::load(a[u].e[e]);
+                        if (kk > 1) {
+                            acc[u][e] = Elt<T>::template combine<OP>(acc[u][e], b[u].e[e]);
+                        }
+                    }
+                }
                 for (int j = 2; j < kk; ++j) {
                     const char *sj = src(j);
 #pragma unroll
@@ -401,7 +431,7 @@ __global__ void __launch_bounds__(BLOCK)
 // (e.g. host-side chunk slices at odd offsets). Still coalesced per element.
 template <typename T, int OP, int EPI, int BLOCK>
 __global__ void __launch_bounds__(BLOCK)
-    reduce_kernel_unaligned(InPtrs in, int k, void *out, size_t n, int np)
+    reduce_kernel_unaligned(InPtrs in, int k, void *out, size_t n, Div np)
 {
     using S = typename Elt<T>::S;
     for (size_t i = static_cast<size_t>(blockIdx.x) * BLOCK + threadIdx.x; i < n;
@@ -414,33 +444,35 @@ __global__ void __launch_bounds__(BLOCK)
 template <typename T> struct SmaMath;
 template <> struct SmaMath<float> {
     using S = float;
-    __device__ static S blend(S v, S s, float c1, float c2, int np)
+    __device__ static S blend(S v, S s, float c1, float c2, const Div &dv)
     {
-        float avg = __fdiv_rn(s, static_cast<float>(np));
+        float avg = dv.pow2 ? __fmul_rn(s, dv.fi) : __fdiv_rn(s, dv.f);
         return __fadd_rn(__fmul_rn(c1, v), __fmul_rn(c2, avg));
     }
 };
 template <> struct SmaMath<double> {
     using S = double;
-    __device__ static S blend(S v, S s, double c1, double c2, int np)
+    __device__ static S blend(S v, S s, double c1, double c2, const Div &dv)
     {
-        double avg = __ddiv_rn(s, static_cast<double>(np));
+        double avg = dv.pow2 ? __dmul_rn(s, dv.di) : __ddiv_rn(s, dv.d);
         return __dadd_rn(__dmul_rn(c1, v), __dmul_rn(c2, avg));
     }
 };
 template <> struct SmaMath<f16_t> {
     using S = uint16_t;
-    __device__ static S blend(S v, S s, float c1, float c2, int np)
+    __device__ static S blend(S v, S s, float c1, float c2, const Div &dv)
     {
-        float avg = __fdiv_rn(f16_to_f32(s), static_cast<float>(np));
+        const float x = f16_to_f32(s);
+        float avg     = dv.pow2 ? __fmul_rn(x, dv.fi) : __fdiv_rn(x, dv.f);
         return f32_to_f16(__fadd_rn(__fmul_rn(c1, f16_to_f32(v)), __fmul_rn(c2, avg)));
     }
 };
 template <> struct SmaMath<bf16_t> {
     using S = uint16_t;
-    __device__ static S blend(S v, S s, float c1, float c2, int np)
+    __device__ static S blend(S v, S s, float c1, float c2, const Div &dv)
     {
-        float avg = __fdiv_rn(bf16_to_f32(s), static_cast<float>(np));
+        const float x = bf16_to_f32(s);
+        float avg     = dv.pow2 ? __fmul_rn(x, dv.fi) : __fdiv_rn(x, dv.f);
         return f32_to_bf16(__fadd_rn(__fmul_rn(c1, bf16_to_f32(v)), __fmul_rn(c2, avg)));
     }
 };
@@ -448,7 +480,7 @@ template <> struct SmaMath<bf16_t> {
 template <typename T, typename C, int BLOCK, int UNROLL>
 __global__ void __launch_bounds__(BLOCK)
     sma_kernel(void *v, const void *s, size_t n, size_t head, size_t nvec,
-               C c1, C c2, int np, int vec_ok)
+               C c1, C c2, Div np, int vec_ok)
 {
     using S         = typename SmaMath<T>::S;
     constexpr int V = Vec<S>::N;
@@ -473,24 +505,31 @@ __global__ void __launch_bounds__(BLOCK)
     const size_t ntiles = (nvec + tile - 1) / tile;
     for (size_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const size_t v0 = t * tile + threadIdx.x;
-        Vec<S> a[UNROLL], b[UNROLL];
+        if (v0 + (UNROLL - 1) * BLOCK < nvec) {
+            // full tile: every load issued before the first use
+            Vec<S> a[UNROLL], b[UNROLL];
 #pragma unroll
-        for (int u = 0; u < UNROLL; ++u) {
-            if (v0 + u * BLOCK < nvec) a[u] = ld_vec<S, 1>(vb, v0 + u * BLOCK);
-        }
+            for (int u = 0; u < UNROLL; ++u) a[u] = ld_vec<S, 1>(vb, v0 + u * BLOCK);
 #pragma unroll
-        for (int u = 0; u < UNROLL; ++u) {
-            if (v0 + u * BLOCK < nvec) b[u] = ld_vec<S, 1>(sb, v0 + u * BLOCK);
-        }
+            for (int u = 0; u < UNROLL; ++u) b[u] = ld_vec<S, 1>(sb, v0 + u * BLOCK);
 #pragma unroll
-        for (int u = 0; u < UNROLL; ++u) {
-            if (v0 + u * BLOCK < nvec) {
+            for (int u = 0; u < UNROLL; ++u) {
                 Vec<S> r;
 #pragma unroll
                 for (int e = 0; e < V; ++e) {
                     r.e[e] = SmaMath<T>::blend(a[u].e[e], b[u].e[e], c1, c2, np);
                 }
                 st_vec<S>(vb, v0 + u * BLOCK, r);
+            }
+        } else {
+            for (int u = 0; u < UNROLL; ++u) {
+                const size_t vi = v0 + u * BLOCK;
+                if (vi >= nvec) break;
+                Vec<S> a = ld_vec<S, 1>(vb, vi), b = ld_vec<S, 1>(sb, vi);
+                Vec<S> r;
+#pragma unroll
+                for (int e = 0; e < V; ++e) r.e[e] = SmaMath<T>::blend(a.e[e], b.e[e], c1, c2, np);
+                st_vec<S>(vb, vi, r);
             }
         }
     }

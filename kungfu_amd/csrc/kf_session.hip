@@ -2,24 +2,36 @@
 // boundary of SURVEY §8b B2: kf_session_all_reduce mirrors
 // GoKungfuAllReduce(sendBuf, recvBuf, count, dtype, op, name, done=nil)
 // (srcs/go/libkungfu-comm/collective.go:34-45) -> Session.AllReduce
-// (srcs/go/kungfu/session/allreduce.go:10-12).
+// (srcs/go/kungfu/session/allreduce.go:10-12) -> runStrategiesWithHash /
+// runGraphs (session.go:231-326), for peers that share one host.
 //
-// Strategy: STAR around rank 0, what KungFu runs when all peers share a host
-// (AUTO -> STAR, strategy.go:196-205; BINARY_TREE_STAR degenerates to the
-// same star, topology.go:76-101). Per bucket (session.go:231-326):
-//   * ceil(bytes / 1 MiB) chunks by EvenPartition, named "part::<name>[b:e]";
-//   * reduce graph: peers sendOnto rank 0 (NoFlag); rank 0 folds each chunk in
-//     ARRIVAL order, RecvBuf = effective o peer (recvOnto, session.go:255-264);
-//   * bcast graph: rank 0 sends each finished chunk with WaitRecvBuf; peers
-//     read it straight into RecvBuf (recvInto, session.go:266-270).
-// Sends run on their own thread (the reference's goroutines), so a peer never
-// blocks the root by not reading. Transport: unix sockets with the rchannel
-// handshake and framing (kf_ingest.hip), one simplex connection per direction.
+// What is restated, with the reduce moved onto the GPU:
+//   * chunking: ceil(bytes / 1 MiB) chunks, EvenPartition by element count,
+//     named "part::<name>[b:e]" (session.go:301-326, workspace.go:18-25);
+//   * per chunk, the strategy sl[hash(i, name) % len(sl)] with nameBasedHash
+//     (sum of squared code points, shard.go:17-23) or simpleHash (= i);
+//   * strategy lists for one host (strategy.go:121-205, topology.go:17-160):
+//     STAR / TREE / BINARY_TREE_STAR / MULTI_STAR / MULTI_BINARY_TREE_STAR /
+//     AUTO -> a star at rank 0; CLIQUE -> k stars, rooted at r; RING -> k
+//     rings, reduce chain r+1 -> ... -> r, bcast chain r -> ... -> r-1;
+//     BINARY_TREE -> i's children 2i+1, 2i+2. Reduce graph = reversed bcast
+//     graph + self loops (GenDefaultReduceGraph) except for RING;
+//   * runGraphs: a node folds every reduce-graph predecessor's chunk IN
+//     ARRIVAL ORDER into RecvBuf (effective o peer: SendBuf before the first
+//     receive, RecvBuf after — recvOnto, session.go:241-264), then sends to
+//     its reduce successors (sendOnto, NoFlag); in the bcast graph it takes
+//     its predecessor's chunk straight into RecvBuf (recvInto, WaitRecvBuf)
+//     or forwards SendBuf if it received nothing (w.Forward), then sends to
+//     its bcast successors (sendInto, WaitRecvBuf).
+// Chunks progress independently (the reference runs a goroutine per chunk):
+// one poll loop handles whatever message arrives next — NoFlag = reduce phase,
+// WaitRecvBuf = bcast phase — and one sender thread drains a FIFO, so no peer
+// ever blocks on a peer that is not reading.
 //
-// Device mode: send/recv are HBM pointers; chunks land in page-locked slots,
-// are copied up and folded by the HIP kernel (kf_ingest_recv_onto). Host mode:
-// send/recv are host pointers; the fold is std_transform_2 (GPU offload) or a
-// C callback (the CPU baseline leg of bench.py passes the oracle's).
+// Device mode: send/recv are HBM pointers; a peer chunk lands in a page-locked
+// slot, is copied to HBM and folded by the HIP kernel (kf_ingest_recv_onto).
+// Host mode: host pointers; the fold is std_transform_2's GPU path
+// (kf_transform2_host) or a C callback (bench.py's CPU-baseline leg).
 #include <hip/hip_runtime.h>
 #include <poll.h>
 #include <sys/socket.h>
@@ -27,8 +39,12 @@
 #include <unistd.h>
 
 #include <cerrno>
+#include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -38,10 +54,10 @@
 
 namespace
 {
-constexpr size_t kChunk     = size_t(1) << 20;  // session.go:301-304
-constexpr int kPortBase     = 10000;            // plan/hostspec.go:121-124
-constexpr uint32_t kIPv4    = 0x7F000001;
-constexpr int kConnRetry    = 500;              // config.go:15-18
+constexpr size_t kChunk      = size_t(1) << 20;  // session.go:301-304
+constexpr int kPortBase      = 10000;            // plan/hostspec.go:121-124
+constexpr uint32_t kIPv4     = 0x7F000001;
+constexpr int kConnRetry     = 500;              // config.go:15-18
 constexpr int kRetryPeriodUs = 200000;
 
 thread_local std::string t_sess_error;
@@ -71,21 +87,183 @@ std::vector<std::pair<size_t, size_t>> even_partition(size_t n, size_t k)
     return parts;
 }
 
+// nameBasedHash (shard.go:17-23): Go ranges over a string by rune, so decode
+// UTF-8 and add each code point squared (uint64 wrap-around).
+uint64_t name_hash(const std::string &s)
+{
+    uint64_t h = 0;
+    for (size_t i = 0; i < s.size();) {
+        const unsigned char c = static_cast<unsigned char>(s[i]);
+        uint32_t cp;
+        int len;
+        if (c < 0x80) {
+            cp = c, len = 1;
+        } else if ((c >> 5) == 0x6 && i + 1 < s.size()) {
+            cp = ((c & 0x1f) << 6) | (s[i + 1] & 0x3f), len = 2;
+        } else if ((c >> 4) == 0xe && i + 2 < s.size()) {
+            cp = ((c & 0x0f) << 12) | ((s[i + 1] & 0x3f) << 6) | (s[i + 2] & 0x3f), len = 3;
+        } else if ((c >> 3) == 0x1e && i + 3 < s.size()) {
+            cp = ((c & 0x07) << 18) | ((s[i + 1] & 0x3f) << 12) | ((s[i + 2] & 0x3f) << 6) |
+                 (s[i + 3] & 0x3f),
+            len = 4;
+        } else {
+            cp = 0xfffd, len = 1;  // invalid byte: Go yields U+FFFD
+        }
+        h += static_cast<uint64_t>(cp) * cp;
+        i += len;
+    }
+    return h;
+}
+
+// One communication graph: prevs / nexts per rank (graph.go:18-108).
+struct Graph {
+    std::vector<std::vector<int>> prev, next;
+    explicit Graph(int n) : prev(n), next(n) {}
+    void edge(int i, int j)
+    {
+        if (i == j) return;  // self loops only mark "reduces"; implicit here
+        next[i].push_back(j);
+        prev[j].push_back(i);
+    }
+    Graph reversed() const
+    {
+        Graph r(static_cast<int>(prev.size()));
+        for (size_t i = 0; i < next.size(); ++i)
+            for (int j : next[i]) r.edge(j, static_cast<int>(i));
+        return r;
+    }
+};
+
+struct Strategy {
+    Graph reduce, bcast;
+};
+
+Strategy simple(const Graph &bg) { return Strategy{bg.reversed(), bg}; }
+
+Graph star(int k, int r)
+{
+    Graph g(k);
+    for (int i = 0; i < k; ++i)
+        if (i != r) g.edge(r, i);
+    return g;
+}
+
+std::vector<Strategy> strategy_list(int strategy, int k)
+{
+    std::vector<Strategy> sl;
+    switch (strategy) {
+    case KungFu_Clique:
+        for (int r = 0; r < k; ++r) sl.push_back(simple(star(k, r)));
+        break;
+    case KungFu_Ring:  // GenCircularGraphPair (topology.go:149-160)
+        for (int r = 0; r < k; ++r) {
+            Graph g(k), b(k);
+            for (int i = 1; i < k; ++i) {
+                g.edge((r + i) % k, (r + i + 1) % k);
+                b.edge((r + i - 1) % k, (r + i) % k);
+            }
+            sl.push_back(Strategy{g, b});
+        }
+        break;
+    case KungFu_BinaryTree: {  // GenBinaryTree (topology.go:42-53)
+        Graph g(k);
+        for (int i = 0; i < k; ++i) {
+            if (2 * i + 1 < k) g.edge(i, 2 * i + 1);
+            if (2 * i + 2 < k) g.edge(i, 2 * i + 2);
+        }
+        sl.push_back(simple(g));
+        break;
+    }
+    default:  // every star-shaped strategy on one host, and AUTO (-> STAR)
+        sl.push_back(simple(star(k, 0)));
+        break;
+    }
+    return sl;
+}
+
+int parse_strategy(const char *s)
+{
+    static const std::pair<const char *, int> names[] = {
+        {"STAR", KungFu_Star},
+        {"MULTI_STAR", KungFu_MultiStar},
+        {"RING", KungFu_Ring},
+        {"CLIQUE", KungFu_Clique},
+        {"TREE", KungFu_Tree},
+        {"BINARY_TREE", KungFu_BinaryTree},
+        {"BINARY_TREE_STAR", KungFu_BinaryTreeStar},
+        {"MULTI_BINARY_TREE_STAR", KungFu_MultiBinaryTreeStar},
+        {"AUTO", KungFu_AUTO},
+    };
+    for (auto &n : names)
+        if (std::strcmp(s, n.first) == 0) return n.second;
+    return -1;
+}
+
+struct Stashed {  // a message that arrived before its all-reduce started
+    std::string name;
+    uint32_t flags;
+    std::vector<char> data;
+};
+
+int read_exact(int fd, void *buf, size_t n)
+{
+    char *p = static_cast<char *>(buf);
+    while (n > 0) {
+        ssize_t r = ::read(fd, p, n);
+        if (r < 0 && errno == EINTR) continue;
+        if (r <= 0) return fail(KF_ERR_IO, "read: unexpected end of stream");
+        p += r;
+        n -= static_cast<size_t>(r);
+    }
+    return KF_OK;
+}
+
+struct SendItem {
+    int fd;
+    std::string name;
+    uint32_t flags;
+    const char *ptr;
+    size_t bytes;
+    void *stream;
+};
+
 }  // namespace
 
 struct kf_session {
     int rank = 0, size = 1;
     std::string dir;
-    uint32_t token = 0;
+    uint32_t token  = 0;
     int device_mode = 1;
-    int listen_fd   = -1;
+    int strategy    = KungFu_BinaryTreeStar;  // kungfu-run default (flags.go:90)
+    int hash_name   = 1;                      // NAME (config.go:45)
+    std::vector<Strategy> sl;
+    int listen_fd = -1;
     std::unordered_map<int, int> out_fd, in_fd;  // peer -> fd
     kf_ingest_t *ingest = nullptr, *egress = nullptr;
     kf_host_reduce_fn host_fn = nullptr;
-    std::vector<char> scratch;  // host-mode landing buffer (pooled, one chunk)
+    std::vector<char> scratch;  // host-mode landing buffer (one chunk)
+    std::deque<Stashed> stash;  // per-name mailbox for early messages
+
+    // sender thread
+    std::thread sender;
+    std::mutex mu;
+    std::condition_variable cv_work, cv_idle;
+    std::deque<SendItem> queue;
+    size_t inflight = 0;
+    bool stopping   = false;
+    int send_rc     = KF_OK;
+    std::string send_err;
 
     ~kf_session()
     {
+        if (sender.joinable()) {
+            {
+                std::lock_guard<std::mutex> l(mu);
+                stopping = true;
+            }
+            cv_work.notify_all();
+            sender.join();
+        }
         for (auto &kv : out_fd) ::close(kv.second);
         for (auto &kv : in_fd) ::close(kv.second);
         if (listen_fd >= 0) {
@@ -96,15 +274,56 @@ struct kf_session {
         if (egress) kf_ingest_destroy(egress);
     }
 
-    std::vector<int> star_peers() const
+    void sender_loop()
     {
-        std::vector<int> v;
-        if (rank == 0) {
-            for (int p = 1; p < size; ++p) v.push_back(p);
-        } else {
-            v.push_back(0);
+        for (;;) {
+            SendItem it;
+            {
+                std::unique_lock<std::mutex> l(mu);
+                cv_work.wait(l, [&] { return stopping || !queue.empty(); });
+                if (queue.empty()) return;
+                it = queue.front();
+                queue.pop_front();
+            }
+            int rc = KF_OK;
+            if (send_rc == KF_OK) {
+                rc = device_mode
+                         ? kf_ingest_send_from_device(egress, it.fd, it.name.c_str(), it.flags,
+                                                      it.ptr, it.bytes, it.stream)
+                         : kf_rch_send(it.fd, it.name.c_str(), it.flags, it.ptr,
+                                       static_cast<uint32_t>(it.bytes));
+            }
+            {
+                std::lock_guard<std::mutex> l(mu);
+                if (rc != KF_OK && send_rc == KF_OK) {
+                    send_rc  = rc;
+                    send_err = kf_ingest_last_error();
+                }
+                if (--inflight == 0) cv_idle.notify_all();
+            }
         }
-        return v;
+    }
+
+    void enqueue(SendItem it)
+    {
+        {
+            std::lock_guard<std::mutex> l(mu);
+            queue.push_back(std::move(it));
+            ++inflight;
+        }
+        cv_work.notify_one();
+    }
+
+    int drain()
+    {
+        std::unique_lock<std::mutex> l(mu);
+        cv_idle.wait(l, [&] { return inflight == 0; });
+        if (send_rc != KF_OK) {
+            const int rc = send_rc;
+            send_rc      = KF_OK;
+            return fail(rc, "send: " + send_err);
+        }
+        return KF_OK;
     }
 
     int connect_all()
@@ -121,11 +340,11 @@ struct kf_session {
             ::listen(listen_fd, size) < 0) {
             return fail(KF_ERR_IO, "bind/listen " + path + ": " + strerror(errno));
         }
-        const std::vector<int> peers = star_peers();
-        int accept_rc                = KF_OK;
+        // full mesh: one simplex connection per ordered pair (client_pool.go)
+        int accept_rc = KF_OK;
         std::string accept_err;
         std::thread acceptor([&] {
-            for (size_t i = 0; i < peers.size(); ++i) {
+            for (int i = 0; i < size - 1; ++i) {
                 int c = ::accept(listen_fd, nullptr, nullptr);
                 if (c < 0) {
                     accept_rc  = KF_ERR_IO;
@@ -145,7 +364,8 @@ struct kf_session {
             }
         });
         int rc = KF_OK;
-        for (int p : peers) {
+        for (int p = 0; p < size && rc == KF_OK; ++p) {
+            if (p == rank) continue;
             int fd = ::socket(AF_UNIX, SOCK_STREAM, 0);
             sockaddr_un b{};
             b.sun_family = AF_UNIX;
@@ -158,14 +378,12 @@ struct kf_session {
                 }
                 ::usleep(kRetryPeriodUs);
             }
-            if (rc != KF_OK) {
-                ::close(fd);
-                break;
+            if (rc == KF_OK) {
+                rc = kf_rch_client_handshake(fd, KF_RCH_CONN_COLLECTIVE,
+                                             static_cast<uint16_t>(kPortBase + rank), kIPv4, token);
+                if (rc != KF_OK) t_sess_error = kf_ingest_last_error();
             }
-            rc = kf_rch_client_handshake(fd, KF_RCH_CONN_COLLECTIVE,
-                                         static_cast<uint16_t>(kPortBase + rank), kIPv4, token);
             if (rc != KF_OK) {
-                t_sess_error = kf_ingest_last_error();
                 ::close(fd);
                 break;
             }
@@ -178,16 +396,6 @@ struct kf_session {
         return KF_OK;
     }
 
-    int send_chunk(int fd, const std::string &name, uint32_t flags, const char *src,
-                   size_t bytes, void *stream)
-    {
-        if (device_mode) {
-            return kf_ingest_send_from_device(egress, fd, name.c_str(), flags, src, bytes,
-                                              stream);
-        }
-        return kf_rch_send(fd, name.c_str(), flags, src, static_cast<uint32_t>(bytes));
-    }
-
     int all_reduce(const char *send, char *recv, size_t count, KungFu_Datatype dt,
                    KungFu_Op op, const std::string &name, void *stream);
 };
@@ -198,8 +406,8 @@ int kf_session::all_reduce(const char *send, char *recv, size_t count, KungFu_Da
     const size_t isz   = kungfu_type_size(dt);
     const bool inplace = send == recv;
     const size_t bytes = count * isz;
-    if (count == 0) return KF_OK;
-    if (size == 1) {  // isolated: w.Forward() (session.go:235-238)
+    if (count == 0) return KF_OK;  // w.IsEmpty()
+    if (size == 1) {               // every graph isolated: w.Forward()
         if (inplace) return KF_OK;
         if (device_mode) {
             hipStream_t s = static_cast<hipStream_t>(stream);
@@ -212,109 +420,184 @@ int kf_session::all_reduce(const char *send, char *recv, size_t count, KungFu_Da
         }
         return KF_OK;
     }
-    const size_t k = (bytes + kChunk - 1) / kChunk;
+    const size_t k   = (bytes + kChunk - 1) / kChunk;
     const auto parts = even_partition(count, k);
-    std::vector<std::string> names;
+    struct Chunk {
+        std::string name;
+        const Strategy *st;
+        size_t pending_reduce;  // reduce-graph predecessors not yet folded
+        int recv_count;
+        bool bcast_done;
+    };
+    std::vector<Chunk> chunks(parts.size());
     std::unordered_map<std::string, size_t> index;
     for (size_t i = 0; i < parts.size(); ++i) {
-        names.push_back("part::" + name + "[" + std::to_string(parts[i].first) + ":" +
-                        std::to_string(parts[i].second) + "]");
-        index[names.back()] = i;
+        auto &c = chunks[i];
+        c.name  = "part::" + name + "[" + std::to_string(parts[i].first) + ":" +
+                 std::to_string(parts[i].second) + "]";
+        const uint64_t h = hash_name ? name_hash(c.name) : static_cast<uint64_t>(i);
+        c.st             = &sl[h % sl.size()];
+        c.pending_reduce = c.st->reduce.prev[rank].size();
+        c.recv_count     = 0;
+        c.bcast_done     = false;
+        index[c.name]    = i;
     }
-    char hname[512];
-    uint32_t flags = 0;
+    auto cptr = [&](const char *base, size_t i) { return base + parts[i].first * isz; };
+    auto clen = [&](size_t i) { return (parts[i].second - parts[i].first) * isz; };
+    auto effective = [&](size_t i) -> const char * {
+        return (chunks[i].recv_count > 0 || inplace) ? cptr(recv, i) : cptr(send, i);
+    };
+    auto finish_bcast = [&](size_t i) {  // after recvInto or at the bcast root
+        auto &c = chunks[i];
+        if (c.st->bcast.prev[rank].empty() && c.recv_count == 0 && !inplace) {
+            // w.Forward(): nothing received in either graph
+            if (device_mode) {  // errors surface at the final stream sync
+                (void)hipMemcpyAsync(const_cast<char *>(cptr(recv, i)), cptr(send, i), clen(i),
+                                     hipMemcpyDeviceToDevice, static_cast<hipStream_t>(stream));
+            } else {
+                std::memcpy(const_cast<char *>(cptr(recv, i)), cptr(send, i), clen(i));
+            }
+        }
+        for (int p : c.st->bcast.next[rank]) {
+            enqueue({out_fd[p], c.name, KF_RCH_WAIT_RECV_BUF, effective(i), clen(i), stream});
+        }
+        c.bcast_done = true;
+    };
+    auto finish_reduce = [&](size_t i) {  // all predecessors folded
+        auto &c = chunks[i];
+        for (int p : c.st->reduce.next[rank]) {
+            enqueue({out_fd[p], c.name, KF_RCH_NO_FLAG, effective(i), clen(i), stream});
+        }
+        if (c.st->bcast.prev[rank].empty()) finish_bcast(i);
+    };
 
-    if (rank != 0) {
-        // sendOnto the root on a thread, recvInto from the root here
-        int send_rc = KF_OK;
-        std::string send_err;
-        std::thread sender([&] {
-            for (size_t i = 0; i < parts.size() && send_rc == KF_OK; ++i) {
-                const auto &pr = parts[i];
-                send_rc = send_chunk(out_fd[0], names[i], KF_RCH_NO_FLAG, send + pr.first * isz,
-                                     (pr.second - pr.first) * isz, stream);
-                if (send_rc != KF_OK) send_err = kf_ingest_last_error();
-            }
-        });
-        int rc  = KF_OK;
-        int src = in_fd[0];
-        for (size_t got = 0; got < parts.size() && rc == KF_OK; ++got) {
-            rc = kf_rch_recv_header(src, hname, sizeof(hname), nullptr, &flags);
-            if (rc != KF_OK) break;
-            auto it = index.find(hname);
-            if (it == index.end()) {
-                rc = fail(KF_ERR_PROTO, std::string("unexpected message ") + hname);
-                break;
-            }
-            const auto &pr = parts[it->second];
-            const uint32_t len = static_cast<uint32_t>((pr.second - pr.first) * isz);
-            rc = device_mode ? kf_ingest_recv_into(ingest, src, len, recv + pr.first * isz, stream)
-                             : kf_rch_recv_body(src, recv + pr.first * isz, len);
+    size_t remaining = chunks.size();
+    for (size_t i = 0; i < chunks.size(); ++i) {
+        if (chunks[i].pending_reduce == 0) {
+            finish_reduce(i);
+            if (chunks[i].bcast_done) --remaining;
         }
-        if (rc != KF_OK) ::shutdown(out_fd[0], SHUT_RDWR);  // unblock the sender
-        sender.join();
-        if (rc != KF_OK) {
-            if (t_sess_error.empty()) t_sess_error = kf_ingest_last_error();
-            return rc;
+    }
+    if (!device_mode && scratch.size() < kChunk + 64) scratch.resize(kChunk + 64);
+    int rc = KF_OK;
+    // one message for chunk i: from the socket fd (mem == nullptr) or from a
+    // stashed copy in host memory
+    auto handle = [&](size_t i, uint32_t flags, int fd, const char *mem) -> int {
+        auto &c            = chunks[i];
+        const size_t n     = parts[i].second - parts[i].first;
+        char *dst          = const_cast<char *>(cptr(recv, i));
+        const uint32_t len = static_cast<uint32_t>(clen(i));
+        int r              = KF_OK;
+        if (flags & KF_RCH_WAIT_RECV_BUF) {  // bcast: recvInto RecvBuf
+            if (device_mode) {
+                r = mem ? kf_ingest_copy_host(ingest, mem, len, dst, stream)
+                        : kf_ingest_recv_into(ingest, fd, len, dst, stream);
+            } else if (mem) {
+                std::memcpy(dst, mem, len);
+            } else {
+                r = kf_rch_recv_body(fd, dst, len);
+            }
+            if (r != KF_OK) return fail(r, kf_ingest_last_error());
+            ++c.recv_count;
+            finish_bcast(i);
+            --remaining;
+            return KF_OK;
         }
-        if (send_rc != KF_OK) return fail(send_rc, send_err);
+        // reduce: recvOnto, RecvBuf = effective o peer
+        const char *own = effective(i);
         if (device_mode) {
-            int s = kf_ingest_sync(ingest);
-            if (s != KF_OK) return fail(s, kf_ingest_last_error());
+            r = mem ? kf_ingest_fold_host(ingest, mem, len, dst, own, n, dt, op, stream)
+                    : kf_ingest_recv_onto(ingest, fd, len, dst, own, n, dt, op, stream);
+            if (r != KF_OK) return fail(r, kf_ingest_last_error());
+        } else {
+            const char *peer = mem;
+            if (!mem) {
+                r = kf_rch_recv_body(fd, scratch.data(), len);
+                if (r != KF_OK) return fail(r, kf_ingest_last_error());
+                peer = scratch.data();
+            }
+            if (host_fn) {
+                if (host_fn(own, peer, dst, static_cast<int64_t>(n), static_cast<int>(dt),
+                            static_cast<int>(op)) != 0) {
+                    return fail(KF_ERR_OP, "host reduce callback failed");
+                }
+            } else {
+                r = kf_transform2_host(own, peer, dst, n, dt, op);
+                if (r != KF_OK) return fail(r, kf_last_error());
+            }
+        }
+        ++c.recv_count;
+        if (--c.pending_reduce == 0) {
+            finish_reduce(i);
+            if (c.bcast_done) --remaining;
         }
         return KF_OK;
+    };
+    // messages of this all-reduce that arrived during the previous one
+    for (auto it = stash.begin(); it != stash.end() && rc == KF_OK;) {
+        auto f = index.find(it->name);
+        if (f == index.end()) {
+            ++it;
+            continue;
+        }
+        rc = handle(f->second, it->flags, -1, it->data.data());
+        it = stash.erase(it);
     }
-
-    // root: fold every peer's chunks in arrival order
-    std::vector<int> folded(parts.size(), 0);
-    const std::vector<int> peers = star_peers();
     std::vector<pollfd> pfds;
-    for (int p : peers) pfds.push_back({in_fd[p], POLLIN, 0});
-    size_t remaining = parts.size() * peers.size();
-    if (!device_mode && scratch.size() < kChunk + 64) scratch.resize(kChunk + 64);
-    while (remaining > 0) {
+    for (auto &kv : in_fd) pfds.push_back({kv.second, POLLIN, 0});
+    char hname[512];
+    uint32_t flags = 0;
+    while (remaining > 0 && rc == KF_OK) {
         if (::poll(pfds.data(), pfds.size(), -1) < 0) {
             if (errno == EINTR) continue;
-            return fail(KF_ERR_IO, std::string("poll: ") + strerror(errno));
+            rc = fail(KF_ERR_IO, std::string("poll: ") + strerror(errno));
+            break;
         }
-        for (auto &pf : pfds) {
-            if (!(pf.revents & (POLLIN | POLLHUP | POLLERR))) continue;
-            int rc = kf_rch_recv_header(pf.fd, hname, sizeof(hname), nullptr, &flags);
-            if (rc != KF_OK) return fail(rc, kf_ingest_last_error());
+        size_t open_fds = 0;
+        for (auto &pf : pfds) open_fds += pf.fd >= 0;
+        if (open_fds == 0) {
+            rc = fail(KF_ERR_IO, "every peer connection closed before the all-reduce finished");
+            break;
+        }
+        for (size_t q = 0; q < pfds.size() && rc == KF_OK && remaining > 0; ++q) {
+            if (pfds[q].fd < 0 || !(pfds[q].revents & (POLLIN | POLLHUP | POLLERR))) continue;
+            const int fd = pfds[q].fd;
+            char probe;
+            if (::recv(fd, &probe, 1, MSG_PEEK | MSG_DONTWAIT) == 0) {
+                // clean EOF at a message boundary: that peer is done with us
+                // (a finished peer closes connections we may not need); stop
+                // polling it
+                pfds[q].fd = -1;
+                continue;
+            }
+            rc = kf_rch_recv_header(fd, hname, sizeof(hname), nullptr, &flags);
+            if (rc != KF_OK) {
+                t_sess_error = kf_ingest_last_error();
+                break;
+            }
             auto it = index.find(hname);
-            if (it == index.end()) return fail(KF_ERR_PROTO, std::string("unexpected message ") + hname);
-            const size_t c   = it->second;
-            const auto &pr   = parts[c];
-            const size_t n   = pr.second - pr.first;
-            char *dst        = recv + pr.first * isz;
-            const char *own  = (folded[c] > 0 || inplace) ? dst : send + pr.first * isz;
-            const uint32_t len = static_cast<uint32_t>(n * isz);
-            if (device_mode) {
-                rc = kf_ingest_recv_onto(ingest, pf.fd, len, dst, own, n, dt, op, stream);
-                if (rc != KF_OK) return fail(rc, kf_ingest_last_error());
-            } else {
-                rc = kf_rch_recv_body(pf.fd, scratch.data(), len);
-                if (rc != KF_OK) return fail(rc, kf_ingest_last_error());
-                if (host_fn) {
-                    rc = host_fn(own, scratch.data(), dst, static_cast<int64_t>(n),
-                                 static_cast<int>(dt), static_cast<int>(op));
-                    if (rc != 0) return fail(KF_ERR_OP, "host reduce callback failed");
-                } else {
-                    rc = kf_transform2_host(own, scratch.data(), dst, n, dt, op);
-                    if (rc != KF_OK) return fail(rc, kf_last_error());
-                }
+            if (it != index.end()) {
+                rc = handle(it->second, flags, fd, nullptr);
+                continue;
             }
-            --remaining;
-            if (++folded[c] == static_cast<int>(peers.size())) {  // chunk done: bcast
-                for (int p : peers) {
-                    rc = send_chunk(out_fd[p], names[c], KF_RCH_WAIT_RECV_BUF, dst, len, stream);
-                    if (rc != KF_OK) return fail(rc, kf_ingest_last_error());
-                }
-            }
+            // not ours (yet): keep it for the all-reduce that owns the name
+            Stashed m{hname, flags, {}};
+            uint32_t len = 0;
+            unsigned char lb[4];
+            rc = read_exact(fd, lb, 4);
+            if (rc != KF_OK) break;
+            len = uint32_t(lb[0]) | (uint32_t(lb[1]) << 8) | (uint32_t(lb[2]) << 16) |
+                  (uint32_t(lb[3]) << 24);
+            m.data.resize(len);
+            rc = read_exact(fd, m.data.data(), len);
+            if (rc == KF_OK) stash.push_back(std::move(m));
         }
     }
+    const int drc = drain();  // our sends must be out before the buffers return
+    if (rc != KF_OK) return rc;
+    if (drc != KF_OK) return drc;
     if (device_mode) {
-        int rc = kf_ingest_sync(ingest);
+        rc = kf_ingest_sync(ingest);
         if (rc != KF_OK) return fail(rc, kf_ingest_last_error());
         if (hipStreamSynchronize(static_cast<hipStream_t>(stream)) != hipSuccess) {
             return fail(KF_ERR_HIP, "stream sync");
@@ -338,6 +621,21 @@ kf_session_t *kf_session_create(int rank, int size, const char *sock_dir, uint32
     s->dir         = sock_dir;
     s->token       = token;
     s->device_mode = device_mode ? 1 : 0;
+    // the reference reads these from the environment kungfu-run sets
+    // (env/envs.go:12, env/config.go:73-76, config/config.go:45,61-62)
+    if (const char *e = std::getenv("KUNGFU_ALLREDUCE_STRATEGY")) {
+        const int st = parse_strategy(e);
+        if (st < 0) {
+            t_sess_error = std::string("unknown KUNGFU_ALLREDUCE_STRATEGY ") + e;
+            delete s;
+            return nullptr;
+        }
+        s->strategy = st;
+    }
+    if (const char *e = std::getenv("KUNGFU_CONFIG_STRATEGY_HASH_METHOD")) {
+        s->hash_name = std::strcmp(e, "NAME") == 0 || std::strcmp(e, "name") == 0;
+    }
+    s->sl = strategy_list(s->strategy, size);
     if (s->device_mode) {
         s->ingest = kf_ingest_create(kChunk + 4096, 8);
         s->egress = kf_ingest_create(kChunk + 4096, 2);
@@ -351,7 +649,17 @@ kf_session_t *kf_session_create(int rank, int size, const char *sock_dir, uint32
         delete s;
         return nullptr;
     }
+    s->sender = std::thread([s] { s->sender_loop(); });
     return s;
+}
+
+int kf_session_set_strategy(kf_session_t *s, int strategy, int hash_by_name)
+{
+    if (!s || strategy < KungFu_Tree || strategy > KungFu_AUTO) return KF_ERR_ARG;
+    s->strategy  = strategy;
+    s->hash_name = hash_by_name ? 1 : 0;
+    s->sl        = strategy_list(strategy, s->size);
+    return KF_OK;
 }
 
 int kf_session_set_host_reduce(kf_session_t *s, kf_host_reduce_fn fn)

@@ -2,12 +2,12 @@
 native engine in kungfu_amd/csrc/kf_session.hip (kf_session_* C ABI).
 
 Mirrors ``Session.AllReduce`` (srcs/go/kungfu/session/allreduce.go:10-12 ->
-session.go:231-326) for the strategy KungFu runs when all peers share a host
-(STAR around rank 0: AUTO selects it, strategy.go:196-205, and
-BINARY_TREE_STAR degenerates to it, topology.go:76-101): 1 MiB chunks by
-EvenPartition named ``part::<name>[b:e]``, peers send to rank 0, rank 0 folds
-in arrival order and sends each finished chunk back with WaitRecvBuf. Peers
-are processes on unix sockets speaking the reference's rchannel framing.
+session.go:231-326) for peers that share a host: 1 MiB chunks by
+EvenPartition named ``part::<name>[b:e]``, each chunk's strategy picked by the
+reference's name hash, reduce-graph folds in arrival order, bcast with
+WaitRecvBuf. Strategies: the star family (the single-host default:
+BINARY_TREE_STAR / AUTO), CLIQUE, RING, BINARY_TREE. Peers are processes on
+unix sockets speaking the reference's rchannel framing.
 
 Modes:
   "device": send/recv are GPU tensors; chunks land in page-locked slots, are
@@ -24,10 +24,17 @@ from .base import OP, OP_NAMES
 CHUNK_SIZE = 1 << 20  # session.go:301-304
 PORT_BASE = 10000
 
+# KungFu_Strategy codes (srcs/cpp/include/kungfu/strategy.h:7-17) by the names
+# kungfu-run accepts (srcs/go/kungfu/base/strategy.go:24-36)
+STRATEGIES = {
+    "TREE": 0, "BINARY_TREE": 1, "RING": 2, "STAR": 3, "MULTI_STAR": 4,
+    "CLIQUE": 5, "BINARY_TREE_STAR": 6, "MULTI_BINARY_TREE_STAR": 7, "AUTO": 8,
+}
+
 
 class Session:
     def __init__(self, rank, size, sock_dir, mode="device", token=0,
-                 host_reduce_fn=None):
+                 host_reduce_fn=None, strategy=None, hash_method="NAME"):
         if mode not in ("device", "host"):
             raise ValueError(mode)
         self.rank, self.size, self.mode = rank, size, mode
@@ -37,6 +44,10 @@ class Session:
         if not self._h:
             raise _lib.KungFuAMDError("kf_session_create: " +
                                       self.lib.kf_session_last_error().decode())
+        if strategy is not None:  # else KUNGFU_ALLREDUCE_STRATEGY / default
+            _lib.check(self.lib.kf_session_set_strategy(
+                self._h, STRATEGIES[strategy], 1 if hash_method == "NAME" else 0),
+                "kf_session_set_strategy")
         if host_reduce_fn is not None:
             if mode != "host":
                 raise ValueError("host_reduce_fn needs mode='host'")

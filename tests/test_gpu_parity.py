@@ -165,7 +165,7 @@ def test_denormals_not_flushed(lib, dev):
     assert np.all(got[:3] != 0)
 
 
-@pytest.mark.parametrize("k", [3, 4, 5, 8, 16])
+@pytest.mark.parametrize("k", [3, 4, 5, 6, 7, 8, 16])
 def test_k_input_ring_order_bit_exact(lib, orc, dev, k):
     # The k-input fused reduce, fed in the reference ring order, reproduces the
     # reference RING all-reduce of that chunk bit for bit (schedule.py).

@@ -32,10 +32,12 @@ def inputs(rank, n, kind):
     return np.random.default_rng(40 + rank).standard_normal(n).astype(np.float32)
 
 
-def _body(rank, size, sock_dir, mode, kind, n, errq):
+def _body(rank, size, sock_dir, mode, kind, n, errq, strategy=None):
     sys.path[:0] = [ROOT, HERE]
     try:
         from kungfu_amd.session import Session
+        if strategy is not None:
+            os.environ["KUNGFU_ALLREDUCE_STRATEGY"] = strategy  # as kungfu-run sets it
         if mode == "device":
             import torch
             dev = torch.device("cuda:0")
@@ -57,8 +59,12 @@ def _body(rank, size, sock_dir, mode, kind, n, errq):
             s.all_reduce(z, z, "inplace")
             got_inplace = z
         s.close()
-        check(rank, size, kind, n, got)
-        check(rank, size, kind, n, got_inplace)
+        if strategy is not None:
+            check_strategy(size, kind, n, strategy, "NegotiatedGrad_0/AllReduce", got)
+            check_strategy(size, kind, n, strategy, "inplace", got_inplace)
+        else:
+            check(rank, size, kind, n, got)
+            check(rank, size, kind, n, got_inplace)
     except Exception:
         errq.put("rank %d: %s" % (rank, traceback.format_exc()))
 
@@ -82,11 +88,35 @@ def check(rank, size, kind, n, got):
         assert any(np.array_equal(got[b:e], o) for o in opts), (rank, b, e)
 
 
-def run(size, mode, kind, n):
+def check_strategy(size, kind, n, strategy, name, got):
+    """Every chunk equals the reference schedule (oracle/schedule.py) for this
+    strategy under SOME arrival order; RING has exactly one order."""
+    from oracle import schedule
+    xs = [inputs(r, n, kind) for r in range(size)]
+    dt = "i32" if kind == "iota" else "f32"
+    multi = [r for r in range(size)]  # nodes whose prevs may arrive in any order
+    outs = []
+    for perms in itertools.product(*[list(itertools.permutations(range(size)))] * 1):
+        order = perms[0]
+
+        def arrival(r, prevs, order=order):
+            return sorted(prevs, key=order.index)
+        outs.append(schedule.all_reduce(xs, dt, "sum", strategy=strategy, name=name,
+                                        arrival=arrival)[0])
+    del multi
+    k = (n * 4 + (1 << 20) - 1) >> 20
+    from kungfu_amd.base import EvenPartition
+    for b, e in EvenPartition(0, n, k):
+        assert any(np.array_equal(got[b:e], o[b:e]) for o in outs), (strategy, b, e)
+    if strategy == "RING":
+        assert all(np.array_equal(outs[0], o) for o in outs)  # order-free
+
+
+def run(size, mode, kind, n, strategy=None):
     ctx = mp.get_context("spawn")
     errq = ctx.SimpleQueue()
     with tempfile.TemporaryDirectory() as d:
-        ps = [ctx.Process(target=_body, args=(r, size, d, mode, kind, n, errq))
+        ps = [ctx.Process(target=_body, args=(r, size, d, mode, kind, n, errq, strategy))
               for r in range(size)]
         for p in ps:
             p.start()
@@ -104,6 +134,19 @@ def run(size, mode, kind, n):
                                          (3, "rand", 600011)])
 def test_session_host_mode(size, kind, n):
     run(size, "host", kind, n)
+
+
+@pytest.mark.parametrize("strategy", ["RING", "CLIQUE", "BINARY_TREE", "STAR",
+                                      "BINARY_TREE_STAR", "AUTO"])
+@pytest.mark.parametrize("size", [2, 3, 4])
+def test_session_strategies_host(strategy, size):
+    # 1 MiB chunks, so each chunk of the 5-chunk bucket picks its own root
+    run(size, "host", "rand", (5 << 20) // 4 + 17, strategy=strategy)
+
+
+def test_session_strategies_iota():
+    for strategy in ("RING", "CLIQUE", "BINARY_TREE"):
+        run(4, "host", "iota", 16, strategy=strategy)
 
 
 def test_session_single_peer_forward():
@@ -125,3 +168,13 @@ def test_session_device_mode(size, kind, n):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     run(size, "device", kind, n)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("strategy,size", [("RING", 3), ("RING", 4), ("CLIQUE", 3),
+                                           ("BINARY_TREE", 4)])
+def test_session_device_strategies(strategy, size):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    run(size, "device", "rand", (5 << 20) // 4 + 17, strategy=strategy)
