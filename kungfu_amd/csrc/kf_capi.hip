@@ -175,28 +175,17 @@ void launch_geom(const InPtrs &ptrs, int k, void *out, size_t n, const Plan &p,
     launch_vec<T, OP, EPI, KC, U, 1>(ptrs, k, out, n, p, np, s);
 }
 
-// SUM folds of the gradient dtypes get a compile-time input count for
-// k = 3..8 (all k loads in flight); everything else runs the runtime-k loop.
+// k = 1 (the shard epilogue) and k = 2 (the hot path) are compile-time; for
+// k > 2 the runtime loop — inputs 0 and 1 up front, then one input at a time —
+// measured faster than loading all k inputs at once (k = 4: 221.8 vs 226.4 us,
+// k = 8: 405.9 vs 419.8 us for 256 MiB fp32, profiles/r01/kernel_rates*.jsonl):
+// fewer concurrent streams keep DRAM rows open longer.
 template <typename T, int OP, int EPI>
 void launch_k(const InPtrs &ptrs, int k, void *out, size_t n, const Plan &p,
               const Div &np, hipStream_t s)
 {
     if (k == 2) return launch_geom<T, OP, EPI, 2>(ptrs, k, out, n, p, np, s);
-    constexpr bool fast = OP == OP_SUM && (std::is_same<T, float>::value ||
-                                           std::is_same<T, f16_t>::value ||
-                                           std::is_same<T, bf16_t>::value);
-    if constexpr (fast) {
-        switch (k) {
-        case 1: return launch_geom<T, OP, EPI, 1>(ptrs, k, out, n, p, np, s);
-        case 3: return launch_geom<T, OP, EPI, 3>(ptrs, k, out, n, p, np, s);
-        case 4: return launch_geom<T, OP, EPI, 4>(ptrs, k, out, n, p, np, s);
-        case 5: return launch_geom<T, OP, EPI, 5>(ptrs, k, out, n, p, np, s);
-        case 6: return launch_geom<T, OP, EPI, 6>(ptrs, k, out, n, p, np, s);
-        case 7: return launch_geom<T, OP, EPI, 7>(ptrs, k, out, n, p, np, s);
-        case 8: return launch_geom<T, OP, EPI, 8>(ptrs, k, out, n, p, np, s);
-        default: break;
-        }
-    }
+    if (k == 1) return launch_geom<T, OP, EPI, 1>(ptrs, k, out, n, p, np, s);
     launch_geom<T, OP, EPI, 0>(ptrs, k, out, n, p, np, s);
 }
 
