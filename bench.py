@@ -365,15 +365,22 @@ def main():
         step_s = t.item() / args.steps
         value = world * s_bytes / step_s / 2**30
         busbw = 2 * (world - 1) / world * s_bytes / step_s / 1e9
+        # the same 64 buckets issued one RS/AG pair each (no fusion), beside
+        per_s = _timed(lambda: ex.all_reduce_(pieces, average=True, coalesce=False),
+                       min(args.steps, 20), 2, dev, world)
         out["collective"] = {
             "busbw_GBps": round(busbw, 2),
             "algbw_GiBps_per_gpu": round(s_bytes / step_s / 2**30, 3),
             "xgmi_bound_GBps": round(153.0 * (world - 1), 1),
             "frac_of_xgmi": round(busbw / (153.0 * (world - 1)), 4),
             "buckets": args.buckets,
+            "fused": "contiguous ready buckets run as one RS -> /np -> AG "
+                     "(the reference's nccl_fusion, sync_sgd.py:87-92)",
+            "per_bucket_ms_per_step": round(per_s * 1e3, 4),
+            "per_bucket_busbw_GBps": round(2 * (world - 1) / world * s_bytes / per_s / 1e9, 2),
         }
-        workload = ("C3: S-SGD all-reduce of %d fp32 buckets (256 MiB) per rank: "
-                    "RCCL reduce-scatter -> HIP /np -> RCCL all-gather" % len(pieces))
+        workload = ("C3: S-SGD all-reduce of %d fp32 buckets (256 MiB) per rank, "
+                    "fused: RCCL reduce-scatter -> HIP /np -> RCCL all-gather" % len(pieces))
         parallelism = "dp%d" % world
         kt = torch.tensor([kernel_s], dtype=torch.float64, device=dev)
         dist.all_reduce(kt, op=dist.ReduceOp.MAX)

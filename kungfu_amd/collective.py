@@ -48,6 +48,36 @@ class HipEpilogue:
         return ops.sma_blend_(v, summed, np_, alpha)
 
 
+def coalesce_runs(buckets):
+    """Maximal runs of buckets that are consecutive in one storage, each as
+    one flat view."""
+    runs, cur = [], []
+
+    def flush():
+        if not cur:
+            return
+        if len(cur) == 1:
+            runs.append(cur[0])
+        else:
+            first = cur[0]
+            n = sum(t.numel() for t in cur)
+            runs.append(torch.empty(0, dtype=first.dtype, device=first.device).set_(
+                first.untyped_storage(), first.storage_offset(), (n,)))
+        cur.clear()
+
+    for b in buckets:
+        if cur:
+            last = cur[-1]
+            adjacent = (b.dtype == last.dtype and b.device == last.device and
+                        b.untyped_storage().data_ptr() == last.untyped_storage().data_ptr() and
+                        b.storage_offset() == last.storage_offset() + last.numel())
+            if not adjacent:
+                flush()
+        cur.append(b)
+    flush()
+    return runs
+
+
 def padded_count(count, world, itemsize):
     """Smallest length >= count that splits into `world` aligned shards."""
     unit = world * max(1, ALIGN_BYTES // itemsize)
@@ -78,9 +108,17 @@ class Exchange:
             raise ValueError("bucket length %d not divisible by world %d; use "
                              "padded_count()" % (buf.numel(), self.world))
 
-    def all_reduce_(self, buckets, op="sum", average=False):
+    def all_reduce_(self, buckets, op="sum", average=False, coalesce=True):
         """In-place all-reduce of flat padded buckets. average=True applies the
-        S-SGD epilogue (sum, then / np) on each shard."""
+        S-SGD epilogue (sum, then / np) on each shard.
+
+        coalesce=True merges buckets that lie back to back in one storage
+        (GradBuckets(n_buckets=k) lays them out that way) into one
+        reduce-scatter -> epilogue -> all-gather run: the same values with
+        one RCCL launch pair instead of one per bucket — the fusion the
+        reference's S-SGD applies to ready gradients (nccl_fusion,
+        sync_sgd.py:87-92). Buckets handed over one call at a time (e.g. as
+        backward produces them) are reduced as they come."""
         red = OP_NAMES[op] if isinstance(op, str) else OP(op)
         if average and red != OP.SUM:
             raise ValueError("average requires op='sum'")
@@ -89,6 +127,11 @@ class Exchange:
         if self.world == 1:
             # a single peer: the reduce is the identity; g / 1 == g exactly
             return buckets
+        if coalesce:
+            runs = coalesce_runs(buckets)
+            if len(runs) < len(buckets):
+                self.all_reduce_(runs, op=op, average=average, coalesce=False)
+                return buckets
         shards = []
         works = []
         for i, b in enumerate(buckets):

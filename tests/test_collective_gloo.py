@@ -249,3 +249,39 @@ def test_all_reduce_with_hip_epilogue():
     run_world("body_all_reduce", 2, use_gpu=True)
     run_world("body_sync_sgd", 3, use_gpu=True)
     run_world("body_sma", 2, use_gpu=True)
+
+
+def test_coalesce_runs():
+    from kungfu_amd.collective import GradBuckets, coalesce_runs
+    gb = GradBuckets([1000, 3000, 5000], torch.float32, torch.device("cpu"), 2, n_buckets=3)
+    runs = coalesce_runs(gb.buckets)
+    assert len(runs) == 1 and runs[0].numel() == sum(b.numel() for b in gb.buckets)
+    assert runs[0].data_ptr() == gb.buckets[0].data_ptr()
+    gb2 = GradBuckets([1000, 3000], torch.float32, torch.device("cpu"), 2, bucket_bytes=4000)
+    assert len(coalesce_runs(gb2.buckets)) == len(gb2.buckets)  # separate storages
+    # order matters: reversed buckets are not one run
+    assert len(coalesce_runs(gb.buckets[::-1])) == 3
+
+
+def body_coalesced_equals_per_bucket(rank, world, use_gpu):
+    from kungfu_amd.collective import Exchange, GradBuckets
+    ex = Exchange(epilogue=_epilogue(use_gpu))
+    sizes = [5000, 123457, 77, 64000]
+    a = GradBuckets(sizes, torch.float32, torch.device("cpu"), world, n_buckets=6)
+    b = GradBuckets(sizes, torch.float32, torch.device("cpu"), world, n_buckets=6)
+    for i, (va, vb) in enumerate(zip(a.views, b.views)):
+        x = torch.from_numpy(_inputs(rank * 10 + i, va.numel()))
+        va.copy_(x)
+        vb.copy_(x)
+    ex.all_reduce_(a.buckets, average=True, coalesce=True)
+    ex.all_reduce_(b.buckets, average=True, coalesce=False)
+    for va, vb in zip(a.views, b.views):
+        if world == 2:
+            assert torch.equal(va, vb)
+        else:
+            assert torch.allclose(va, vb, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_coalesced_equals_per_bucket(world):
+    run_world("body_coalesced_equals_per_bucket", world)
