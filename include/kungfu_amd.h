@@ -35,6 +35,10 @@
 extern "C" {
 #endif
 
+/* The library is built with -fvisibility=hidden: exactly what this header
+ * declares is exported. */
+#pragma GCC visibility push(default)
+
 /* ---- reference-compatible enums ---------------------------------------- */
 
 enum KungFu_Datatype {
@@ -258,6 +262,8 @@ int kf_session_all_reduce(kf_session_t *s, const void *send, void *recv,
                           const char *name, void *stream);
 void kf_session_destroy(kf_session_t *s);
 const char *kf_session_last_error(void);
+
+#pragma GCC visibility pop
 
 #ifdef __cplusplus
 }

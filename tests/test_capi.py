@@ -15,6 +15,7 @@ LIB = os.path.join(ROOT, "kungfu_amd", "libkungfu_amd.so")
 def declared_functions():
     src = open(HEADER).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    src = re.sub(r"^typedef[^;]*;", "", src, flags=re.M | re.S)
     return sorted(set(re.findall(r"^[A-Za-z_][\w \*]*?\b(\w+)\s*\(", src, re.M)))
 
 
@@ -43,6 +44,8 @@ def test_all_declared_symbols_exported(lib):
         assert f in exported, f
         assert f in _lib.EXPORTED, f
         assert getattr(lib, f) is not None
+    # nothing but the declared C ABI leaks out (no C++ internals)
+    assert exported == set(declared_functions()), exported ^ set(declared_functions())
 
 
 def test_enum_values_bit_identical():
