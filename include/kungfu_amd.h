@@ -198,7 +198,9 @@ int kf_rch_recv_header(int fd, char *name, uint32_t cap, uint32_t *name_len,
 int kf_rch_recv_body(int fd, void *dst, uint32_t expect_len);
 
 /* Page-locked landing slots + device slots for peer chunks. */
-typedef struct kf_ingest kf_ingest_t;
+#pragma GCC visibility pop
+typedef struct kf_ingest kf_ingest_t; /* opaque; its C++ body stays hidden */
+#pragma GCC visibility push(default)
 kf_ingest_t *kf_ingest_create(size_t slot_bytes, int nslots);
 void kf_ingest_destroy(kf_ingest_t *g);
 
@@ -237,7 +239,9 @@ const char *kf_ingest_last_error(void);
 typedef int (*kf_host_reduce_fn)(const void *x, const void *y, void *out,
                                  int64_t n, int dt, int op);
 
-typedef struct kf_session kf_session_t;
+#pragma GCC visibility pop
+typedef struct kf_session kf_session_t; /* opaque; its C++ body stays hidden */
+#pragma GCC visibility push(default)
 
 /* Peer `rank` of `size` on this host: listens on
  * <sock_dir>/kungfu-amd-<10000+rank>.sock and connects to every other peer

@@ -113,7 +113,7 @@ inline uint32_t get_u32(const unsigned char *p)
 
 }  // namespace
 
-struct __attribute__((visibility("hidden"))) kf_ingest {
+struct kf_ingest {
     size_t slot_bytes = 0;
     int nslots        = 0;
     int next          = 0;

@@ -229,7 +229,7 @@ struct SendItem {
 
 }  // namespace
 
-struct __attribute__((visibility("hidden"))) kf_session {
+struct kf_session {
     int rank = 0, size = 1;
     std::string dir;
     uint32_t token  = 0;
