@@ -1,0 +1,132 @@
+"""``kungfu.torch.ops`` mirror (srcs/python/kungfu/torch/ops/collective.py:8-52).
+
+The reference moves a CUDA tensor to the host, all-reduces it there through
+Peer::AllReduce and copies it back (srcs/cpp/src/torch/ops/cuda/collective.cpp:
+20-55). Here the tensor stays in HBM: it is staged into an aligned bucket and
+reduced by RCCL reduce-scatter + all-gather over xGMI (op 'sum' / 'min' /
+'max' / 'prod'); the handle API is kept for the async variants.
+"""
+import torch
+import torch.distributed as dist
+
+from ..collective import Exchange, padded_count
+
+_exchange = None
+
+
+def _ex():
+    global _exchange
+    if _exchange is None:
+        _exchange = Exchange()
+    return _exchange
+
+
+def _world():
+    return dist.get_world_size() if dist.is_initialized() else 1
+
+
+class _Handle:
+    def __init__(self, works, finish):
+        self.works, self.finish = works, finish
+
+
+_handles = {}
+_next = [0]
+
+
+def _staged(x):
+    n = x.numel()
+    L = padded_count(max(n, 1), _world(), x.element_size())
+    buf = torch.zeros(L, dtype=x.dtype, device=x.device)
+    buf[:n].copy_(x.reshape(-1))
+    return buf
+
+
+def all_reduce_fn(x, op=None):
+    """Returns the all-reduced copy of x (collective.py:8-13)."""
+    y = x.clone()
+    inplace_all_reduce_op(y, op)
+    return y
+
+
+def inplace_all_reduce_op(x, op=None):
+    """x <- all-reduce(x) in place (collective.py:16-19)."""
+    op = op or "sum"
+    if _world() == 1:
+        return x
+    buf = _staged(x)
+    _ex().all_reduce_([buf], op=op)
+    x.copy_(buf[:x.numel()].view_as(x))
+    return x
+
+
+def inplace_all_reduce_async_op(x, name, op=None):
+    """Starts x <- all-reduce(x); returns a handle for wait_handle
+    (collective.py:22-25). Reduce-scatter and all-gather are queued on the
+    RCCL stream at once; the copy back happens in wait_handle."""
+    op = op or "sum"
+    h = _next[0]
+    _next[0] += 1
+    if _world() == 1:
+        _handles[h] = _Handle([], lambda: None)
+        return h
+    from ..base import OP_NAMES
+    from ..collective import _RED_OPS
+    buf = _staged(x)
+    world = _world()
+    shard = torch.empty(buf.numel() // world, dtype=buf.dtype, device=buf.device)
+    w1 = dist.reduce_scatter_tensor(shard, buf, op=_RED_OPS[OP_NAMES[op]], async_op=True)
+    if dist.get_backend() == "nccl":
+        # RCCL ops of one communicator run in order on its stream: queue the
+        # all-gather right behind the reduce-scatter
+        works = [w1, dist.all_gather_into_tensor(buf, shard, async_op=True)]
+
+        def finish(x=x, buf=buf):
+            x.copy_(buf[:x.numel()].view_as(x))
+    else:
+        # other backends may run async ops concurrently: gather after the wait
+        works = [w1]
+
+        def finish(x=x, buf=buf, shard=shard):
+            dist.all_gather_into_tensor(buf, shard)
+            x.copy_(buf[:x.numel()].view_as(x))
+
+    _handles[h] = _Handle(works, finish)
+    return h
+
+
+def inplace_broadcast_async_op(x, name):
+    """Starts x <- rank 0's x (collective.py:28-29); returns a handle."""
+    h = _next[0]
+    _next[0] += 1
+    works = [dist.broadcast(x, src=0, async_op=True)] if _world() > 1 else []
+    _handles[h] = _Handle(works, lambda: None)
+    return h
+
+
+def wait_handle(handle):
+    hd = _handles.pop(handle)
+    for w in hd.works:
+        w.wait()
+    hd.finish()
+
+
+def wait_all_handles(handles):
+    for h in handles:
+        wait_handle(h)
+
+
+def broadcast_parameters(state_dict):
+    """Every rank takes rank 0's parameters (collective.py:40-45)."""
+    wait_all_handles([inplace_broadcast_async_op(v, k) for k, v in state_dict.items()])
+
+
+def all_gather(x):
+    """[np] + x.shape tensor of every rank's x (collective.py:48-52)."""
+    world = _world()
+    y = x.new_empty(torch.Size([world] + list(x.shape)))
+    if world == 1:
+        y[0].copy_(x)
+        return y
+    dist.all_gather_into_tensor(y.reshape(-1), x.contiguous().reshape(-1))
+    return y

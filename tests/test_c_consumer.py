@@ -1,0 +1,33 @@
+"""A plain C program built against include/kungfu_amd.h and linked with
+-lkungfu_amd (tests/c/test_dropin.c): the drop-in works for C callers, as the
+reference's C++ unit tests use it (tests/cpp/unit/test_kungfu.cpp:3-20)."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+
+
+@pytest.fixture(scope="module")
+def binary(tmp_path_factory):
+    out = str(tmp_path_factory.mktemp("c") / "test_dropin")
+    lib = os.path.join(ROOT, "kungfu_amd")
+    subprocess.run(["gcc", "-Wall", "-Wextra", "-Werror", "-std=c99",
+                    "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "c", "test_dropin.c"),
+                    "-L", lib, "-lkungfu_amd", "-Wl,-rpath," + lib, "-o", out],
+                   check=True)
+    return out
+
+
+def test_c_consumer_builds_and_type_sizes(binary):
+    r = subprocess.run([binary], capture_output=True, text=True, timeout=300)
+    assert r.returncode in (0, 77), r.stderr  # 77: no device, host checks passed
+
+
+@pytest.mark.gpu
+def test_c_consumer_on_gpu(binary):
+    r = subprocess.run([binary], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "ok" in r.stdout

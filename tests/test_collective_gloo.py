@@ -285,3 +285,30 @@ def body_coalesced_equals_per_bucket(rank, world, use_gpu):
 @pytest.mark.parametrize("world", [2, 3])
 def test_coalesced_equals_per_bucket(world):
     run_world("body_coalesced_equals_per_bucket", world)
+
+
+def body_torch_ops(rank, world, use_gpu):
+    # kungfu.torch.ops surface (srcs/python/kungfu/torch/ops/collective.py)
+    from kungfu_amd.torch import ops
+    x = torch.arange(10, dtype=torch.float32).reshape(2, 5) + rank
+    y = ops.all_reduce_fn(x)
+    assert torch.equal(y, torch.arange(10, dtype=torch.float32).reshape(2, 5) * world
+                       + world * (world - 1) / 2)
+    z = torch.full((7,), float(rank + 1))
+    ops.inplace_all_reduce_op(z, "max")
+    assert torch.all(z == world)
+    hs = [ops.inplace_all_reduce_async_op(torch.ones(1000, dtype=torch.int32) * (rank + 1), "a")]
+    t = torch.ones(33) * (rank + 1)
+    hs.append(ops.inplace_all_reduce_async_op(t, "t"))
+    ops.wait_all_handles(hs)
+    assert torch.all(t == world * (world + 1) / 2)
+    sd = {"w": torch.full((4,), float(rank))}
+    ops.broadcast_parameters(sd)
+    assert torch.all(sd["w"] == 0)
+    g = ops.all_gather(torch.tensor([rank, rank * 10]))
+    assert g.shape == (world, 2) and g[world - 1, 1].item() == (world - 1) * 10
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_torch_ops_surface(world):
+    run_world("body_torch_ops", world)
