@@ -267,6 +267,24 @@ int kf_session_all_reduce(kf_session_t *s, const void *send, void *recv,
 void kf_session_destroy(kf_session_t *s);
 const char *kf_session_last_error(void);
 
+/* ---- peer-to-peer over xGMI (kungfu_amd/p2p.py) ------------------------ */
+
+#define KF_IPC_HANDLE_BYTES 64
+#define KF_MAX_SEGMENTS 16
+
+/* Export the allocation holding dev_ptr for another process of this node:
+ * handle[KF_IPC_HANDLE_BYTES] + the byte offset of dev_ptr inside it. */
+int kf_ipc_export(const void *dev_ptr, void *handle, size_t *offset);
+/* Map a peer's exported allocation; *base_out + offset is its dev_ptr. */
+int kf_ipc_import(const void *handle, void **base_out);
+int kf_ipc_close(void *base);
+/* One launch copying nseg byte ranges dst[off_j, off_j + len_j) <-
+ * srcs[j][off_j, off_j + len_j) (e.g. the shards other GPUs reduced, read
+ * over xGMI); every offset, length and pointer 16-byte aligned. */
+int kf_gather_segments(void *dst, const void *const *srcs, const size_t *offsets,
+                       const size_t *lens, int nseg, void *stream);
+const char *kf_p2p_last_error(void);
+
 #pragma GCC visibility pop
 
 #ifdef __cplusplus

@@ -46,6 +46,11 @@ EXPORTED = (
     "kf_session_all_reduce",
     "kf_session_destroy",
     "kf_session_last_error",
+    "kf_ipc_export",
+    "kf_ipc_import",
+    "kf_ipc_close",
+    "kf_gather_segments",
+    "kf_p2p_last_error",
 )
 
 STATUS = {
@@ -164,6 +169,18 @@ def load():
     lib.kf_session_destroy.restype = None
     lib.kf_session_last_error.argtypes = []
     lib.kf_session_last_error.restype = ctypes.c_char_p
+    lib.kf_ipc_export.argtypes = [c_void_p, c_void_p, ctypes.POINTER(c_size_t)]
+    lib.kf_ipc_export.restype = c_int
+    lib.kf_ipc_import.argtypes = [c_void_p, ctypes.POINTER(c_void_p)]
+    lib.kf_ipc_import.restype = c_int
+    lib.kf_ipc_close.argtypes = [c_void_p]
+    lib.kf_ipc_close.restype = c_int
+    lib.kf_gather_segments.argtypes = [c_void_p, ctypes.POINTER(c_void_p),
+                                       ctypes.POINTER(c_size_t), ctypes.POINTER(c_size_t),
+                                       c_int, c_void_p]
+    lib.kf_gather_segments.restype = c_int
+    lib.kf_p2p_last_error.argtypes = []
+    lib.kf_p2p_last_error.restype = ctypes.c_char_p
     _lib = lib
     return lib
 
@@ -172,7 +189,7 @@ def check(rc, what):
     if rc != 0:
         lib = load()
         detail = (lib.kf_session_last_error().decode() or lib.kf_last_error().decode()
-                  or lib.kf_ingest_last_error().decode())
+                  or lib.kf_ingest_last_error().decode() or lib.kf_p2p_last_error().decode())
         raise KungFuAMDError("%s failed: %s (%s)" % (what, STATUS.get(rc, rc), detail))
 
 

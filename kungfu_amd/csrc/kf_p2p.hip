@@ -1,0 +1,132 @@
+// kf_p2p.hip — peer-to-peer pieces for an all-reduce over xGMI without RCCL:
+// HIP IPC export/import of device buffers between the processes of one node,
+// and a gather kernel that pulls several peers' shards in one launch.
+//
+// The exchange built on them (kungfu_amd/p2p.py): every rank folds ITS shard
+// of the bucket straight out of every peer's HBM with the k-input reduce
+// kernel (kf_bucket_reduce_avg, ranks in order — deterministic), then gathers
+// the other shards from their owners with kf_gather_segments. On MI355X every
+// GPU has a direct xGMI link to each of the 7 others, so both phases spread
+// their reads over all links at once.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <string>
+
+#include "kungfu_amd.h"
+
+namespace
+{
+thread_local std::string t_p2p_error;
+
+int hip_fail(hipError_t e, const char *what)
+{
+    t_p2p_error = std::string(what) + ": " + hipGetErrorString(e);
+    return KF_ERR_HIP;
+}
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+struct Segs {
+    const char *src[KF_MAX_SEGMENTS];
+    size_t off[KF_MAX_SEGMENTS];
+    size_t len[KF_MAX_SEGMENTS];  // bytes, multiple of 16
+};
+
+// blockIdx.y = segment; each block copies 4 x 16 B per thread per tile,
+// non-temporal both ways (each byte moves once).
+__global__ void __launch_bounds__(256) gather_kernel(char *dst, Segs segs)
+{
+    const int s       = blockIdx.y;
+    const size_t nvec = segs.len[s] / 16;
+    const u32x4 *src  = reinterpret_cast<const u32x4 *>(segs.src[s] + segs.off[s]);
+    u32x4 *out        = reinterpret_cast<u32x4 *>(dst + segs.off[s]);
+    const size_t tile = 256 * 4;
+    for (size_t t = blockIdx.x; t * tile < nvec; t += gridDim.x) {
+        const size_t v0 = t * tile + threadIdx.x;
+        u32x4 r[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (v0 + u * 256 < nvec) r[u] = __builtin_nontemporal_load(src + v0 + u * 256);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (v0 + u * 256 < nvec) __builtin_nontemporal_store(r[u], out + v0 + u * 256);
+        }
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int kf_ipc_export(const void *dev_ptr, void *handle, size_t *offset)
+{
+    if (!dev_ptr || !handle || !offset) return KF_ERR_ARG;
+    hipDeviceptr_t base = nullptr;
+    size_t size         = 0;
+    hipError_t e = hipMemGetAddressRange(&base, &size, const_cast<void *>(dev_ptr));
+    if (e != hipSuccess) return hip_fail(e, "hipMemGetAddressRange");
+    hipIpcMemHandle_t h;
+    e = hipIpcGetMemHandle(&h, base);
+    if (e != hipSuccess) return hip_fail(e, "hipIpcGetMemHandle");
+    static_assert(sizeof(hipIpcMemHandle_t) <= KF_IPC_HANDLE_BYTES, "handle size");
+    std::memset(handle, 0, KF_IPC_HANDLE_BYTES);
+    std::memcpy(handle, &h, sizeof(h));
+    *offset = static_cast<size_t>(static_cast<const char *>(dev_ptr) -
+                                  static_cast<const char *>(base));
+    return KF_OK;
+}
+
+int kf_ipc_import(const void *handle, void **base_out)
+{
+    if (!handle || !base_out) return KF_ERR_ARG;
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, handle, sizeof(h));
+    hipError_t e = hipIpcOpenMemHandle(base_out, h, hipIpcMemLazyEnablePeerAccess);
+    if (e != hipSuccess) return hip_fail(e, "hipIpcOpenMemHandle");
+    return KF_OK;
+}
+
+int kf_ipc_close(void *base)
+{
+    if (!base) return KF_ERR_ARG;
+    hipError_t e = hipIpcCloseMemHandle(base);
+    if (e != hipSuccess) return hip_fail(e, "hipIpcCloseMemHandle");
+    return KF_OK;
+}
+
+int kf_gather_segments(void *dst, const void *const *srcs, const size_t *offsets,
+                       const size_t *lens, int nseg, void *stream)
+{
+    if (nseg < 0 || nseg > KF_MAX_SEGMENTS) return KF_ERR_ARG;
+    if (nseg == 0) return KF_OK;
+    if (!dst || !srcs || !offsets || !lens) return KF_ERR_ARG;
+    Segs segs;
+    size_t maxlen = 0;
+    for (int i = 0; i < nseg; ++i) {
+        if (!srcs[i] || (lens[i] % 16) || (offsets[i] % 16) ||
+            (reinterpret_cast<uintptr_t>(srcs[i]) % 16) ||
+            (reinterpret_cast<uintptr_t>(dst) % 16)) {
+            t_p2p_error = "kf_gather_segments: segments must be 16-byte aligned";
+            return KF_ERR_ARG;
+        }
+        segs.src[i] = static_cast<const char *>(srcs[i]);
+        segs.off[i] = offsets[i];
+        segs.len[i] = lens[i];
+        if (lens[i] > maxlen) maxlen = lens[i];
+    }
+    const size_t tile   = 256 * 4 * 16;
+    size_t bx           = (maxlen + tile - 1) / tile;
+    if (bx > 65535) bx = 65535;
+    if (bx < 1) bx = 1;
+    dim3 grid(static_cast<unsigned>(bx), static_cast<unsigned>(nseg));
+    gather_kernel<<<grid, 256, 0, static_cast<hipStream_t>(stream)>>>(static_cast<char *>(dst), segs);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "gather_kernel launch");
+    return KF_OK;
+}
+
+const char *kf_p2p_last_error(void) { return t_p2p_error.c_str(); }
+
+}  // extern "C"

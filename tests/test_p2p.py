@@ -1,0 +1,76 @@
+"""xGMI peer-to-peer all-reduce (kungfu_amd/p2p.py) with ranks as processes
+sharing cuda:0 (HIP IPC works between processes on one device), gloo for the
+barriers. The fold order is rank order, so results are bit-exact against the
+oracle for every world size."""
+import os
+import sys
+import traceback
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+pytestmark = pytest.mark.gpu
+
+
+def _body(rank, world, port, errq):
+    sys.path[:0] = [ROOT, HERE]
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from kungfu_amd.collective import GradBuckets
+        from kungfu_amd.p2p import P2PExchange
+        from oracle import oracle
+        dev = torch.device("cuda:0")
+        sizes = [100003, 5000, 777777, 64]
+        gb = GradBuckets(sizes, torch.float32, dev, world, n_buckets=4)
+        xs = [[np.random.default_rng(1000 * r + i).standard_normal(n).astype(np.float32)
+               for i, n in enumerate(sizes)] for r in range(world)]
+        for v, x in zip(gb.views, xs[rank]):
+            v.copy_(torch.from_numpy(x))
+        ex = P2PExchange(gb.buckets)
+        ex.all_reduce_(average=True)
+        for i, v in enumerate(gb.views):
+            want = oracle.reduce_avg([xs[r][i] for r in range(world)], "f32", world)
+            assert np.array_equal(v.cpu().numpy(), want), i
+        # int32 MAX, a second exchange on other buckets, twice (buffer reuse)
+        gi = GradBuckets([4099], torch.int32, dev, world, n_buckets=1)
+        ex2 = P2PExchange(gi.buckets)
+        for step in range(2):
+            gi.views[0].copy_(torch.arange(4099, dtype=torch.int32, device=dev) * (rank + 1 + step))
+            ex2.all_reduce_(op="max")
+            assert torch.equal(gi.views[0].cpu(), torch.arange(4099, dtype=torch.int32) * (world + step))
+        ex.close()
+        ex2.close()
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:
+        errq.put("rank %d: %s" % (rank, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_p2p_all_reduce_bit_exact(world):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    errq = ctx.SimpleQueue()
+    ps = [ctx.Process(target=_body, args=(r, world, port, errq)) for r in range(world)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(timeout=300)
+    errs = []
+    while not errq.empty():
+        errs.append(errq.get())
+    assert not errs, "\n".join(errs)
+    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
