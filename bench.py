@@ -75,6 +75,8 @@ def parse():
     ap.add_argument("--config", default="default", choices=["default", "c1"],
                     help="c1: BASELINE configs[0], np=2 localhost all-reduce of "
                          "one 4 MiB fp32 bucket over the rchannel wire format")
+    ap.add_argument("--c1-np", type=int, default=2,
+                    help="peers for --config c1 (BASELINE configs[0] is np=2)")
     ap.add_argument("--c1-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--c1-rank", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--c1-mode", default="device", help=argparse.SUPPRESS)
@@ -203,13 +205,16 @@ def c1_child(args):
     cpu      — host buffers, the oracle's restatement of the reference reduce
                (this is bench.py's CPU-baseline leg)."""
     from kungfu_amd.session import Session
-    r = args.c1_rank
+    r, npeers = args.c1_rank, args.c1_np
     x = ((r + 1) * (np.arange(C1_ELEMS) % 1024) / 1024).astype(np.float32)
-    want = (3 * (np.arange(C1_ELEMS) % 1024) / 1024).astype(np.float32)
-    if args.c1_mode == "device":
+    # sum_r (r+1) * (i mod 1024) / 1024: every partial sum is exact in fp32
+    want = (npeers * (npeers + 1) // 2 * (np.arange(C1_ELEMS) % 1024) / 1024).astype(np.float32)
+    if args.c1_mode.startswith("device"):
+        if args.c1_mode == "device_chain":  # the reference's 2-input recvOnto chain
+            os.environ["KUNGFU_AMD_BATCH_FOLD"] = "0"
         dev = torch.device("cuda", 0)
         xs, ys = torch.from_numpy(x).to(dev), torch.zeros(C1_ELEMS, device=dev)
-        sess = Session(r, 2, args.c1_dir, mode="device")
+        sess = Session(r, npeers, args.c1_dir, mode="device")
         result = lambda: ys.cpu().numpy()  # noqa: E731
     else:
         xs, ys = x, np.zeros_like(x)
@@ -217,7 +222,7 @@ def c1_child(args):
         if args.c1_mode == "cpu":
             from oracle import oracle
             fn = ctypes.cast(oracle.lib().oracle_transform2, ctypes.c_void_p)
-        sess = Session(r, 2, args.c1_dir, mode="host", host_reduce_fn=fn)
+        sess = Session(r, npeers, args.c1_dir, mode="host", host_reduce_fn=fn)
         result = lambda: ys  # noqa: E731
     name = "NegotiatedGrad_0/AllReduce"
     for _ in range(args.warmup):
@@ -237,22 +242,24 @@ def c1_child(args):
         print(json.dumps({"mode": args.c1_mode, "correct": ok,
                           "latency_ms_median": round(med * 1e3, 4),
                           "latency_ms_min": round(ts[0] * 1e3, 4),
-                          "rate_GiBps": round(4 * (2 - 1) * nbytes / med / 2**30, 3)}),
+                          "rate_GiBps": round(4 * (npeers - 1) * nbytes / med / 2**30, 3)}),
               flush=True)
 
 
 def c1_parent(args):
-    """Launch the two peers per mode (subprocesses, one unix socket each)."""
+    """Launch the np peers per mode (subprocesses, one unix socket each)."""
     import subprocess
     import tempfile
     res = {}
-    for mode in ("device", "dropin", "cpu"):
+    modes = ("device", "device_chain", "dropin", "cpu") if args.c1_np > 2 else \
+        ("device", "dropin", "cpu")
+    for mode in modes:
         with tempfile.TemporaryDirectory() as d:
             cmd = [sys.executable, os.path.abspath(__file__), "--c1-child",
                    "--c1-mode", mode, "--c1-dir", d, "--steps", str(args.steps),
-                   "--warmup", str(args.warmup)]
+                   "--warmup", str(args.warmup), "--c1-np", str(args.c1_np)]
             procs = [subprocess.Popen(cmd + ["--c1-rank", str(r)], stdout=subprocess.PIPE,
-                                      text=True, cwd=ROOT) for r in range(2)]
+                                      text=True, cwd=ROOT) for r in range(args.c1_np)]
             outs = [p.communicate(timeout=600)[0] for p in procs]
             if any(p.returncode for p in procs):
                 res[mode] = {"error": "peer exit codes %s" % [p.returncode for p in procs]}
@@ -261,9 +268,10 @@ def c1_parent(args):
     line = {
         "metric": "C1 all-reduce rate 4(np-1)*bytes/t (kungfu-bench-allreduce.go:73-80)",
         "unit": "GiB/s",
-        "config": {"workload": "C1: np=2 localhost, one 4 MiB fp32 bucket, 4 x 1 MiB "
+        "config": {"workload": "C1: np=%d localhost, one 4 MiB fp32 bucket, 4 x 1 MiB "
                                "chunks, STAR at rank 0, rchannel framing over unix "
-                               "sockets", "elements": C1_ELEMS},
+                               "sockets" % args.c1_np, "elements": C1_ELEMS,
+                   "np": args.c1_np},
         "steps": args.steps, "warmup": args.warmup,
         "modes": res,
     }

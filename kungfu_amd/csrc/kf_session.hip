@@ -30,6 +30,12 @@
 //
 // Device mode: send/recv are HBM pointers; a peer chunk lands in a page-locked
 // slot, is copied to HBM and folded by the HIP kernel (kf_ingest_recv_onto).
+// A node with several reduce predecessors (the star root: np-1 of them) stages
+// each arrival in HBM and folds them all in ONE k-input launch when the last
+// one is in: own o p_a1 o p_a2 o ... in arrival order, the same left fold as
+// the reference's chain of recvOnto calls, so the result is bit-identical
+// (reads (k+1)*S and writes S once, instead of 3*S per predecessor). bf16 keeps
+// the per-hop chain: its k-input kernel rounds once, not per hop.
 // Host mode: host pointers; the fold is std_transform_2's GPU path
 // (kf_transform2_host) or a C callback (bench.py's CPU-baseline leg).
 #include <hip/hip_runtime.h>
@@ -242,6 +248,9 @@ struct kf_session {
     kf_ingest_t *ingest = nullptr, *egress = nullptr;
     kf_host_reduce_fn host_fn = nullptr;
     std::vector<char> scratch;  // host-mode landing buffer (one chunk)
+    int batch_fold = 1;         // device mode: k-input fold at multi-predecessor nodes
+    char *stage       = nullptr;  // HBM staging: [predecessor arrival][bucket bytes]
+    size_t stage_bytes = 0;
     std::deque<Stashed> stash;  // per-name mailbox for early messages
 
     // sender thread
@@ -272,6 +281,7 @@ struct kf_session {
         }
         if (ingest) kf_ingest_destroy(ingest);
         if (egress) kf_ingest_destroy(egress);
+        if (stage) (void)hipFree(stage);
     }
 
     void sender_loop()
@@ -428,9 +438,11 @@ int kf_session::all_reduce(const char *send, char *recv, size_t count, KungFu_Da
         size_t pending_reduce;  // reduce-graph predecessors not yet folded
         int recv_count;
         bool bcast_done;
+        bool batched;  // stage the reduce arrivals, fold them in one launch
     };
     std::vector<Chunk> chunks(parts.size());
     std::unordered_map<std::string, size_t> index;
+    size_t need_stage = 0;
     for (size_t i = 0; i < parts.size(); ++i) {
         auto &c = chunks[i];
         c.name  = "part::" + name + "[" + std::to_string(parts[i].first) + ":" +
@@ -440,7 +452,20 @@ int kf_session::all_reduce(const char *send, char *recv, size_t count, KungFu_Da
         c.pending_reduce = c.st->reduce.prev[rank].size();
         c.recv_count     = 0;
         c.bcast_done     = false;
+        c.batched        = device_mode && batch_fold && dt != KungFu_BFLOAT16 &&
+                    c.pending_reduce >= 2 && c.pending_reduce + 1 <= KF_MAX_INPUTS;
+        if (c.batched && c.pending_reduce * bytes > need_stage) need_stage = c.pending_reduce * bytes;
         index[c.name]    = i;
+    }
+    if (need_stage > stage_bytes) {  // the previous all-reduce ended synchronized
+        if (stage) (void)hipFree(stage);
+        stage       = nullptr;
+        stage_bytes = 0;
+        if (hipMalloc(&stage, need_stage) != hipSuccess) {
+            stage = nullptr;
+            return fail(KF_ERR_HIP, "hipMalloc staging for the k-input fold");
+        }
+        stage_bytes = need_stage;
     }
     auto cptr = [&](const char *base, size_t i) { return base + parts[i].first * isz; };
     auto clen = [&](size_t i) { return (parts[i].second - parts[i].first) * isz; };
@@ -501,6 +526,24 @@ int kf_session::all_reduce(const char *send, char *recv, size_t count, KungFu_Da
             ++c.recv_count;
             finish_bcast(i);
             --remaining;
+            return KF_OK;
+        }
+        if (c.batched) {  // stage arrival #recv_count; fold once all are in
+            char *slot = stage + static_cast<size_t>(c.recv_count) * bytes + parts[i].first * isz;
+            r = mem ? kf_ingest_copy_host(ingest, mem, len, slot, stream)
+                    : kf_ingest_recv_into(ingest, fd, len, slot, stream);
+            if (r != KF_OK) return fail(r, kf_ingest_last_error());
+            ++c.recv_count;
+            if (--c.pending_reduce > 0) return KF_OK;
+            const void *ins[KF_MAX_INPUTS];
+            ins[0] = inplace ? dst : cptr(send, i);  // effective before the first receive
+            for (int a = 0; a < c.recv_count; ++a) {
+                ins[a + 1] = stage + static_cast<size_t>(a) * bytes + parts[i].first * isz;
+            }
+            r = kf_bucket_reduce(ins, c.recv_count + 1, dst, n, dt, op, stream);
+            if (r != KF_OK) return fail(r, kf_last_error());
+            finish_reduce(i);
+            if (c.bcast_done) --remaining;
             return KF_OK;
         }
         // reduce: recvOnto, RecvBuf = effective o peer
@@ -632,6 +675,7 @@ kf_session_t *kf_session_create(int rank, int size, const char *sock_dir, uint32
         }
         s->strategy = st;
     }
+    if (const char *e = std::getenv("KUNGFU_AMD_BATCH_FOLD")) s->batch_fold = std::atoi(e) != 0;
     if (const char *e = std::getenv("KUNGFU_CONFIG_STRATEGY_HASH_METHOD")) {
         s->hash_name = std::strcmp(e, "NAME") == 0 || std::strcmp(e, "name") == 0;
     }

@@ -32,8 +32,9 @@ def inputs(rank, n, kind):
     return np.random.default_rng(40 + rank).standard_normal(n).astype(np.float32)
 
 
-def _body(rank, size, sock_dir, mode, kind, n, errq, strategy=None):
+def _body(rank, size, sock_dir, mode, kind, n, errq, strategy=None, env=None):
     sys.path[:0] = [ROOT, HERE]
+    os.environ.update(env or {})
     try:
         from kungfu_amd.session import Session
         if strategy is not None:
@@ -112,11 +113,11 @@ def check_strategy(size, kind, n, strategy, name, got):
         assert all(np.array_equal(outs[0], o) for o in outs)  # order-free
 
 
-def run(size, mode, kind, n, strategy=None):
+def run(size, mode, kind, n, strategy=None, env=None):
     ctx = mp.get_context("spawn")
     errq = ctx.SimpleQueue()
     with tempfile.TemporaryDirectory() as d:
-        ps = [ctx.Process(target=_body, args=(r, size, d, mode, kind, n, errq, strategy))
+        ps = [ctx.Process(target=_body, args=(r, size, d, mode, kind, n, errq, strategy, env))
               for r in range(size)]
         for p in ps:
             p.start()
@@ -172,9 +173,24 @@ def test_session_device_mode(size, kind, n):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("strategy,size", [("RING", 3), ("RING", 4), ("CLIQUE", 3),
-                                           ("BINARY_TREE", 4)])
-def test_session_device_strategies(strategy, size):
+                                           ("BINARY_TREE", 4), ("STAR", 4), ("CLIQUE", 4)])
+@pytest.mark.parametrize("batch_fold", ["1", "0"])
+def test_session_device_strategies(strategy, size, batch_fold):
+    # batch_fold=1: nodes with >= 2 reduce predecessors (star/clique roots,
+    # binary-tree inner nodes) stage the arrivals in HBM and fold them in one
+    # k-input launch; 0: the reference's chain of 2-input recvOnto folds.
+    # Either way each chunk must equal the schedule for some arrival order.
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    run(size, "device", "rand", (5 << 20) // 4 + 17, strategy=strategy)
+    run(size, "device", "rand", (5 << 20) // 4 + 17, strategy=strategy,
+        env={"KUNGFU_AMD_BATCH_FOLD": batch_fold})
+
+
+@pytest.mark.gpu
+def test_session_device_batched_iota():
+    # fake_agent.cpp:15-44 KAT (iota * np) through the k-input fold at np=4
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    run(4, "device", "iota", (3 << 20) // 4 + 5)
