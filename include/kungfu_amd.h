@@ -233,7 +233,7 @@ int kf_ingest_copy_host(kf_ingest_t *g, const void *host, uint32_t len,
 int kf_ingest_sync(kf_ingest_t *g);
 const char *kf_ingest_last_error(void);
 
-/* ---- single-host session engine (collective boundary) ---- */
+/* ---- session engine (collective boundary) ---------------- */
 
 /* Host-mode fold callback: out = x op y over n elements; 0 = ok. */
 typedef int (*kf_host_reduce_fn)(const void *x, const void *y, void *out,
@@ -244,7 +244,7 @@ typedef struct kf_session kf_session_t; /* opaque; its C++ body stays hidden */
 #pragma GCC visibility push(default)
 
 /* Peer `rank` of `size` on this host: listens on
- * <sock_dir>/kungfu-amd-<10000+rank>.sock and connects to every other peer
+ * <sock_dir>/kungfu-amd-127.0.0.1-<10000+rank>.sock and connects to every other peer
  * (rchannel handshake with `token`). The strategy and chunk hash come from
  * KUNGFU_ALLREDUCE_STRATEGY / KUNGFU_CONFIG_STRATEGY_HASH_METHOD as in the
  * reference (default BINARY_TREE_STAR, NAME). device_mode = 1: buffers passed
@@ -252,6 +252,17 @@ typedef struct kf_session kf_session_t; /* opaque; its C++ body stays hidden */
  * failure (kf_session_last_error). */
 kf_session_t *kf_session_create(int rank, int size, const char *sock_dir,
                                 uint32_t token, int device_mode);
+/* Peer `self_spec` of the cluster `peer_list`, in the formats kungfu-run
+ * exports as KUNGFU_SELF_SPEC / KUNGFU_INIT_PEERS ("ipv4:port" and a
+ * comma-separated list of them, plan/id.go:34-50, plan/peerlist.go:180-192);
+ * the rank is self's index in the list. Peers with the same IPv4 connect over
+ * <sock_dir>/kungfu-amd-<ipv4>-<port>.sock, the others over TCP to ipv4:port
+ * (rchannel/connection/connection.go:58-64); every peer listens on its own
+ * address. Multi-host strategies (TREE, BINARY_TREE_STAR, MULTI_*, AUTO ->
+ * BINARY_TREE_STAR) follow the hosts (plan/topology.go:5-136). */
+kf_session_t *kf_session_create_peers(const char *peer_list, const char *self_spec,
+                                      const char *sock_dir, uint32_t token,
+                                      int device_mode);
 /* Override the strategy (KungFu_Strategy) and chunk hash (1 = NAME,
  * 0 = SIMPLE); every peer must use the same. */
 int kf_session_set_strategy(kf_session_t *s, int strategy, int hash_by_name);

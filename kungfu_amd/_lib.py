@@ -41,6 +41,7 @@ EXPORTED = (
     "kf_ingest_sync",
     "kf_ingest_last_error",
     "kf_session_create",
+    "kf_session_create_peers",
     "kf_session_set_strategy",
     "kf_session_set_host_reduce",
     "kf_session_all_reduce",
@@ -153,6 +154,9 @@ def load():
     lib.kf_ingest_last_error.restype = ctypes.c_char_p
     lib.kf_session_create.argtypes = [c_int, c_int, ctypes.c_char_p, u32, c_int]
     lib.kf_session_create.restype = c_void_p
+    lib.kf_session_create_peers.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
+                                            u32, c_int]
+    lib.kf_session_create_peers.restype = c_void_p
     lib.kf_session_set_strategy.argtypes = [c_void_p, c_int, c_int]
     lib.kf_session_set_strategy.restype = c_int
     lib.kf_ingest_fold_host.argtypes = [c_void_p, c_void_p, u32, c_void_p, c_void_p,

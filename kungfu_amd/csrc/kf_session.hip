@@ -39,11 +39,15 @@
 // Host mode: host pointers; the fold is std_transform_2's GPU path
 // (kf_transform2_host) or a C callback (bench.py's CPU-baseline leg).
 #include <hip/hip_runtime.h>
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
 #include <poll.h>
 #include <sys/socket.h>
 #include <sys/un.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cerrno>
 #include <condition_variable>
 #include <cstdio>
@@ -74,9 +78,57 @@ int fail(int rc, const std::string &what)
     return rc;
 }
 
-std::string sock_path(const std::string &dir, int rank)
+// A peer's address (plan/addr.go NetAddr): IPv4 + port. Peers with the same
+// IPv4 are colocated and talk over a unix socket named by the port (SockFile,
+// addr.go:24-26, under the session's directory); others over TCP
+// (connection.go:58-64).
+struct PeerAddr {
+    uint32_t ip;
+    uint16_t port;
+    bool operator==(const PeerAddr &o) const { return ip == o.ip && port == o.port; }
+};
+
+// the address is in the name too, so emulated hosts (127.0.0.x) sharing a
+// directory and port numbers do not collide
+std::string sock_path(const std::string &dir, const PeerAddr &p)
 {
-    return dir + "/kungfu-amd-" + std::to_string(kPortBase + rank) + ".sock";
+    char ip[INET_ADDRSTRLEN];
+    in_addr a{};
+    a.s_addr = htonl(p.ip);
+    ::inet_ntop(AF_INET, &a, ip, sizeof(ip));
+    return dir + "/kungfu-amd-" + ip + "-" + std::to_string(p.port) + ".sock";
+}
+
+// "a.b.c.d:port" (ParsePeerID, plan/id.go:34-50)
+bool parse_peer(const std::string &s, PeerAddr *p)
+{
+    const size_t c = s.rfind(':');
+    if (c == std::string::npos) return false;
+    in_addr a{};
+    if (::inet_pton(AF_INET, s.substr(0, c).c_str(), &a) != 1) return false;
+    char *end       = nullptr;
+    const long port = std::strtol(s.c_str() + c + 1, &end, 10);
+    if (*end != 0 || port <= 0 || port > 65535) return false;
+    p->ip   = ntohl(a.s_addr);
+    p->port = static_cast<uint16_t>(port);
+    return true;
+}
+
+// comma-separated (ParsePeerList, plan/peerlist.go:180-192)
+bool parse_peer_list(const std::string &s, std::vector<PeerAddr> *out)
+{
+    out->clear();
+    size_t b = 0;
+    for (;;) {
+        const size_t e = s.find(',', b);
+        PeerAddr p;
+        if (!parse_peer(s.substr(b, e == std::string::npos ? std::string::npos : e - b), &p)) {
+            return false;
+        }
+        out->push_back(p);
+        if (e == std::string::npos) return true;
+        b = e + 1;
+    }
 }
 
 std::vector<std::pair<size_t, size_t>> even_partition(size_t n, size_t k)
@@ -154,10 +206,78 @@ Graph star(int k, int r)
     return g;
 }
 
-std::vector<Strategy> strategy_list(int strategy, int k)
+// getLocalMasters (topology.go:5-15): the first rank seen on each host
+std::vector<int> local_masters(const std::vector<uint32_t> &hosts, std::vector<int> *master_of)
 {
+    std::vector<int> masters;
+    master_of->assign(hosts.size(), -1);
+    for (size_t r = 0; r < hosts.size(); ++r) {
+        int m = -1;
+        for (int q : masters)
+            if (hosts[q] == hosts[r]) m = q;
+        if (m < 0) {
+            masters.push_back(static_cast<int>(r));
+            m = static_cast<int>(r);
+        }
+        (*master_of)[r] = m;
+    }
+    return masters;
+}
+
+// every non-master hangs off its host's master (the star inside each host)
+Graph host_stars(const std::vector<uint32_t> &hosts, std::vector<int> *masters)
+{
+    std::vector<int> master_of;
+    *masters = local_masters(hosts, &master_of);
+    Graph g(static_cast<int>(hosts.size()));
+    for (size_t r = 0; r < hosts.size(); ++r)
+        if (master_of[r] != static_cast<int>(r)) g.edge(master_of[r], static_cast<int>(r));
+    return g;
+}
+
+Graph multi_star(const std::vector<uint32_t> &hosts, int root)  // topology.go:55-74
+{
+    std::vector<int> m;
+    Graph g = host_stars(hosts, &m);
+    const int k = static_cast<int>(m.size());
+    if (k > 1)
+        for (int i = 0; i < k; ++i)
+            if (i != root) g.edge(m[root], m[i]);
+    return g;
+}
+
+Graph binary_tree_star(const std::vector<uint32_t> &hosts, int offset)  // topology.go:76-101
+{
+    std::vector<int> m;
+    Graph g     = host_stars(hosts, &m);
+    const int k = static_cast<int>(m.size());
+    if (k > 1) {
+        auto idx = [&](int i) { return (i + offset) % k; };
+        for (int i = 0; i < k; ++i) {
+            if (2 * i + 1 < k) g.edge(m[idx(i)], m[idx(2 * i + 1)]);
+            if (2 * i + 2 < k) g.edge(m[idx(i)], m[idx(2 * i + 2)]);
+        }
+    }
+    return g;
+}
+
+// strategy.go:121-205; hosts[r] = IPv4 of rank r
+std::vector<Strategy> strategy_list(int strategy, const std::vector<uint32_t> &hosts)
+{
+    const int k = static_cast<int>(hosts.size());
+    std::vector<int> masters, master_of;
+    masters = local_masters(hosts, &master_of);
+    if (strategy == KungFu_AUTO)  // autoSelect (strategy.go:165-174)
+        strategy = masters.size() == 1 ? KungFu_Star : KungFu_BinaryTreeStar;
     std::vector<Strategy> sl;
     switch (strategy) {
+    case KungFu_Star:
+        sl.push_back(simple(star(k, 0)));
+        break;
+    case KungFu_MultiStar:
+        for (size_t i = 0; i < masters.size(); ++i)
+            sl.push_back(simple(multi_star(hosts, static_cast<int>(i))));
+        break;
     case KungFu_Clique:
         for (int r = 0; r < k; ++r) sl.push_back(simple(star(k, r)));
         break;
@@ -171,6 +291,12 @@ std::vector<Strategy> strategy_list(int strategy, int k)
             sl.push_back(Strategy{g, b});
         }
         break;
+    case KungFu_Tree: {  // GenTree (topology.go:17-31)
+        Graph g = host_stars(hosts, &masters);
+        for (size_t i = 1; i < masters.size(); ++i) g.edge(masters[0], masters[i]);
+        sl.push_back(simple(g));
+        break;
+    }
     case KungFu_BinaryTree: {  // GenBinaryTree (topology.go:42-53)
         Graph g(k);
         for (int i = 0; i < k; ++i) {
@@ -180,8 +306,12 @@ std::vector<Strategy> strategy_list(int strategy, int k)
         sl.push_back(simple(g));
         break;
     }
-    default:  // every star-shaped strategy on one host, and AUTO (-> STAR)
-        sl.push_back(simple(star(k, 0)));
+    case KungFu_MultiBinaryTreeStar:
+        for (size_t i = 0; i < masters.size(); ++i)
+            sl.push_back(simple(binary_tree_star(hosts, static_cast<int>(i))));
+        break;
+    default:  // KungFu_BinaryTreeStar
+        sl.push_back(simple(binary_tree_star(hosts, 0)));
         break;
     }
     return sl;
@@ -206,6 +336,7 @@ int parse_strategy(const char *s)
 }
 
 struct Stashed {  // a message that arrived before its all-reduce started
+    int peer;
     std::string name;
     uint32_t flags;
     std::vector<char> data;
@@ -243,7 +374,8 @@ struct kf_session {
     int strategy    = KungFu_BinaryTreeStar;  // kungfu-run default (flags.go:90)
     int hash_name   = 1;                      // NAME (config.go:45)
     std::vector<Strategy> sl;
-    int listen_fd = -1;
+    std::vector<PeerAddr> peers;           // rank -> address (KUNGFU_INIT_PEERS)
+    int listen_unix = -1, listen_tcp = -1;
     std::unordered_map<int, int> out_fd, in_fd;  // peer -> fd
     kf_ingest_t *ingest = nullptr, *egress = nullptr;
     kf_host_reduce_fn host_fn = nullptr;
@@ -275,10 +407,11 @@ struct kf_session {
         }
         for (auto &kv : out_fd) ::close(kv.second);
         for (auto &kv : in_fd) ::close(kv.second);
-        if (listen_fd >= 0) {
-            ::close(listen_fd);
-            ::unlink(sock_path(dir, rank).c_str());
+        if (listen_unix >= 0) {
+            ::close(listen_unix);
+            ::unlink(sock_path(dir, peers[rank]).c_str());
         }
+        if (listen_tcp >= 0) ::close(listen_tcp);
         if (ingest) kf_ingest_destroy(ingest);
         if (egress) kf_ingest_destroy(egress);
         if (stage) (void)hipFree(stage);
@@ -336,70 +469,165 @@ struct kf_session {
         return KF_OK;
     }
 
+    bool colocated(int p) const { return peers[p].ip == peers[rank].ip; }
+
+    std::vector<uint32_t> hosts() const
+    {
+        std::vector<uint32_t> h;
+        for (auto &p : peers) h.push_back(p.ip);
+        return h;
+    }
+
+    int rank_of(uint32_t ip, uint16_t port) const
+    {
+        for (size_t r = 0; r < peers.size(); ++r)
+            if (peers[r] == PeerAddr{ip, port}) return static_cast<int>(r);
+        return -1;
+    }
+
+    // a connected, handshaken simplex connection to peer p (client_pool.go),
+    // unix socket if colocated else TCP, retried like ConnRetryCount/Period
+    int dial(int p, int *out)
+    {
+        const PeerAddr &to = peers[p];
+        for (int attempt = 0;; ++attempt) {
+            int fd = -1, ok = 0;
+            if (colocated(p)) {
+                fd = ::socket(AF_UNIX, SOCK_STREAM, 0);
+                sockaddr_un b{};
+                b.sun_family = AF_UNIX;
+                std::strcpy(b.sun_path, sock_path(dir, to).c_str());
+                ok = fd >= 0 && ::connect(fd, reinterpret_cast<sockaddr *>(&b), sizeof(b)) == 0;
+            } else {
+                fd = ::socket(AF_INET, SOCK_STREAM, 0);
+                sockaddr_in b{};
+                b.sin_family      = AF_INET;
+                b.sin_port        = htons(to.port);
+                b.sin_addr.s_addr = htonl(to.ip);
+                ok = fd >= 0 && ::connect(fd, reinterpret_cast<sockaddr *>(&b), sizeof(b)) == 0;
+                if (ok) {
+                    int one = 1;
+                    (void)::setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+                }
+            }
+            if (ok) {
+                const int rc = kf_rch_client_handshake(fd, KF_RCH_CONN_COLLECTIVE, peers[rank].port,
+                                                       peers[rank].ip, token);
+                if (rc != KF_OK) {
+                    t_sess_error = kf_ingest_last_error();
+                    ::close(fd);
+                    return rc;
+                }
+                *out = fd;
+                return KF_OK;
+            }
+            const int err = errno;
+            if (fd >= 0) ::close(fd);
+            if (attempt + 1 >= kConnRetry) {
+                return fail(KF_ERR_IO, "connect to peer " + std::to_string(p) + ": " + strerror(err));
+            }
+            ::usleep(kRetryPeriodUs);
+        }
+    }
+
+    int listen_on()
+    {
+        bool any_local = false, any_remote = false;
+        for (int p = 0; p < size; ++p) {
+            if (p == rank) continue;
+            (colocated(p) ? any_local : any_remote) = true;
+        }
+        if (any_local) {  // unix server (server.go:48-70)
+            const std::string path = sock_path(dir, peers[rank]);
+            ::unlink(path.c_str());
+            listen_unix = ::socket(AF_UNIX, SOCK_STREAM, 0);
+            sockaddr_un a{};
+            a.sun_family = AF_UNIX;
+            if (path.size() >= sizeof(a.sun_path)) return fail(KF_ERR_ARG, "socket path too long");
+            std::strcpy(a.sun_path, path.c_str());
+            if (listen_unix < 0 ||
+                ::bind(listen_unix, reinterpret_cast<sockaddr *>(&a), sizeof(a)) < 0 ||
+                ::listen(listen_unix, size) < 0) {
+                return fail(KF_ERR_IO, "bind/listen " + path + ": " + strerror(errno));
+            }
+        }
+        if (any_remote) {  // tcp server (server.go:24-46), on this peer's own address
+            listen_tcp = ::socket(AF_INET, SOCK_STREAM, 0);
+            int one    = 1;
+            if (listen_tcp >= 0)
+                (void)::setsockopt(listen_tcp, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+            sockaddr_in a{};
+            a.sin_family      = AF_INET;
+            a.sin_port        = htons(peers[rank].port);
+            a.sin_addr.s_addr = htonl(peers[rank].ip);
+            if (listen_tcp < 0 ||
+                ::bind(listen_tcp, reinterpret_cast<sockaddr *>(&a), sizeof(a)) < 0 ||
+                ::listen(listen_tcp, size) < 0) {
+                return fail(KF_ERR_IO, "bind/listen tcp port " + std::to_string(peers[rank].port) +
+                                           ": " + strerror(errno));
+            }
+        }
+        return KF_OK;
+    }
+
     int connect_all()
     {
-        const std::string path = sock_path(dir, rank);
-        ::unlink(path.c_str());
-        listen_fd = ::socket(AF_UNIX, SOCK_STREAM, 0);
-        if (listen_fd < 0) return fail(KF_ERR_IO, "socket: " + std::string(strerror(errno)));
-        sockaddr_un a{};
-        a.sun_family = AF_UNIX;
-        if (path.size() >= sizeof(a.sun_path)) return fail(KF_ERR_ARG, "socket path too long");
-        std::strcpy(a.sun_path, path.c_str());
-        if (::bind(listen_fd, reinterpret_cast<sockaddr *>(&a), sizeof(a)) < 0 ||
-            ::listen(listen_fd, size) < 0) {
-            return fail(KF_ERR_IO, "bind/listen " + path + ": " + strerror(errno));
-        }
-        // full mesh: one simplex connection per ordered pair (client_pool.go)
+        int rc = listen_on();
+        if (rc != KF_OK) return rc;
+        // full mesh: one simplex connection per ordered pair (client_pool.go);
+        // the acceptor learns who dialled from the connection header
         int accept_rc = KF_OK;
         std::string accept_err;
         std::thread acceptor([&] {
-            for (int i = 0; i < size - 1; ++i) {
-                int c = ::accept(listen_fd, nullptr, nullptr);
-                if (c < 0) {
+            std::vector<pollfd> ls;
+            if (listen_unix >= 0) ls.push_back({listen_unix, POLLIN, 0});
+            if (listen_tcp >= 0) ls.push_back({listen_tcp, POLLIN, 0});
+            int got = 0;
+            while (got < size - 1) {
+                if (::poll(ls.data(), ls.size(), -1) < 0) {
+                    if (errno == EINTR) continue;
                     accept_rc  = KF_ERR_IO;
-                    accept_err = std::string("accept: ") + strerror(errno);
+                    accept_err = std::string("poll: ") + strerror(errno);
                     return;
                 }
-                uint16_t type = 0, port = 0;
-                uint32_t ip   = 0;
-                int rc        = kf_rch_server_handshake(c, token, &type, &port, &ip);
-                if (rc != KF_OK) {
-                    accept_rc  = rc;
-                    accept_err = kf_ingest_last_error();
-                    ::close(c);
-                    return;
+                for (auto &l : ls) {
+                    if (!(l.revents & (POLLIN | POLLHUP | POLLERR))) continue;
+                    int c = ::accept(l.fd, nullptr, nullptr);
+                    if (c < 0) {
+                        accept_rc  = KF_ERR_IO;
+                        accept_err = std::string("accept: ") + strerror(errno);
+                        return;
+                    }
+                    if (l.fd == listen_tcp) {
+                        int one = 1;
+                        (void)::setsockopt(c, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+                    }
+                    uint16_t type = 0, port = 0;
+                    uint32_t ip = 0;
+                    int hrc     = kf_rch_server_handshake(c, token, &type, &port, &ip);
+                    const int p = hrc == KF_OK ? rank_of(ip, port) : -1;
+                    if (p < 0 || p == rank || in_fd.count(p)) {
+                        accept_rc  = hrc != KF_OK ? hrc : KF_ERR_PROTO;
+                        accept_err = hrc != KF_OK ? std::string(kf_ingest_last_error())
+                                                  : "connection from a peer not in the list";
+                        ::close(c);
+                        return;
+                    }
+                    in_fd[p] = c;
+                    ++got;
                 }
-                in_fd[port - kPortBase] = c;
             }
         });
-        int rc = KF_OK;
         for (int p = 0; p < size && rc == KF_OK; ++p) {
             if (p == rank) continue;
-            int fd = ::socket(AF_UNIX, SOCK_STREAM, 0);
-            sockaddr_un b{};
-            b.sun_family = AF_UNIX;
-            std::strcpy(b.sun_path, sock_path(dir, p).c_str());
-            int attempt = 0;
-            while (::connect(fd, reinterpret_cast<sockaddr *>(&b), sizeof(b)) < 0) {
-                if (++attempt >= kConnRetry) {
-                    rc = fail(KF_ERR_IO, "connect " + sock_path(dir, p) + ": " + strerror(errno));
-                    break;
-                }
-                ::usleep(kRetryPeriodUs);
-            }
-            if (rc == KF_OK) {
-                rc = kf_rch_client_handshake(fd, KF_RCH_CONN_COLLECTIVE,
-                                             static_cast<uint16_t>(kPortBase + rank), kIPv4, token);
-                if (rc != KF_OK) t_sess_error = kf_ingest_last_error();
-            }
-            if (rc != KF_OK) {
-                ::close(fd);
-                break;
-            }
-            out_fd[p] = fd;
+            int fd = -1;
+            rc     = dial(p, &fd);
+            if (rc == KF_OK) out_fd[p] = fd;
         }
-        if (rc != KF_OK) ::shutdown(listen_fd, SHUT_RDWR);  // unblock the acceptor
+        if (rc != KF_OK) {  // unblock the acceptor
+            if (listen_unix >= 0) ::shutdown(listen_unix, SHUT_RDWR);
+            if (listen_tcp >= 0) ::shutdown(listen_tcp, SHUT_RDWR);
+        }
         acceptor.join();
         if (rc != KF_OK) return rc;
         if (accept_rc != KF_OK) return fail(accept_rc, accept_err);
@@ -439,6 +667,7 @@ int kf_session::all_reduce(const char *send, char *recv, size_t count, KungFu_Da
         int recv_count;
         bool bcast_done;
         bool batched;  // stage the reduce arrivals, fold them in one launch
+        std::vector<int> waiting;  // reduce predecessors not yet heard from
     };
     std::vector<Chunk> chunks(parts.size());
     std::unordered_map<std::string, size_t> index;
@@ -450,6 +679,7 @@ int kf_session::all_reduce(const char *send, char *recv, size_t count, KungFu_Da
         const uint64_t h = hash_name ? name_hash(c.name) : static_cast<uint64_t>(i);
         c.st             = &sl[h % sl.size()];
         c.pending_reduce = c.st->reduce.prev[rank].size();
+        c.waiting        = c.st->reduce.prev[rank];
         c.recv_count     = 0;
         c.bcast_done     = false;
         c.batched        = device_mode && batch_fold && dt != KungFu_BFLOAT16 &&
@@ -505,10 +735,25 @@ int kf_session::all_reduce(const char *send, char *recv, size_t count, KungFu_Da
     }
     if (!device_mode && scratch.size() < kChunk + 64) scratch.resize(kChunk + 64);
     int rc = KF_OK;
+    // Is this message (from `peer`) one chunk i still waits for in THIS call?
+    // The same names recur every step, and a peer that has finished this step
+    // may already send the next one's; such a message waits in the stash, as
+    // in the reference's per-name mailbox (handler/collective.go:27-61).
+    auto expects = [&](size_t i, uint32_t flags, int peer) -> bool {
+        const auto &c = chunks[i];
+        if (flags & KF_RCH_WAIT_RECV_BUF) {
+            const auto &bp = c.st->bcast.prev[rank];
+            return !c.bcast_done && std::find(bp.begin(), bp.end(), peer) != bp.end();
+        }
+        return std::find(c.waiting.begin(), c.waiting.end(), peer) != c.waiting.end();
+    };
     // one message for chunk i: from the socket fd (mem == nullptr) or from a
     // stashed copy in host memory
-    auto handle = [&](size_t i, uint32_t flags, int fd, const char *mem) -> int {
+    auto handle = [&](size_t i, uint32_t flags, int peer, int fd, const char *mem) -> int {
         auto &c            = chunks[i];
+        if (!(flags & KF_RCH_WAIT_RECV_BUF)) {
+            c.waiting.erase(std::find(c.waiting.begin(), c.waiting.end(), peer));
+        }
         const size_t n     = parts[i].second - parts[i].first;
         char *dst          = const_cast<char *>(cptr(recv, i));
         const uint32_t len = static_cast<uint32_t>(clen(i));
@@ -579,15 +824,19 @@ int kf_session::all_reduce(const char *send, char *recv, size_t count, KungFu_Da
     // messages of this all-reduce that arrived during the previous one
     for (auto it = stash.begin(); it != stash.end() && rc == KF_OK;) {
         auto f = index.find(it->name);
-        if (f == index.end()) {
+        if (f == index.end() || !expects(f->second, it->flags, it->peer)) {
             ++it;
             continue;
         }
-        rc = handle(f->second, it->flags, -1, it->data.data());
+        rc = handle(f->second, it->flags, it->peer, -1, it->data.data());
         it = stash.erase(it);
     }
     std::vector<pollfd> pfds;
-    for (auto &kv : in_fd) pfds.push_back({kv.second, POLLIN, 0});
+    std::vector<int> pfd_peer;
+    for (auto &kv : in_fd) {
+        pfds.push_back({kv.second, POLLIN, 0});
+        pfd_peer.push_back(kv.first);
+    }
     char hname[512];
     uint32_t flags = 0;
     while (remaining > 0 && rc == KF_OK) {
@@ -618,13 +867,14 @@ int kf_session::all_reduce(const char *send, char *recv, size_t count, KungFu_Da
                 t_sess_error = kf_ingest_last_error();
                 break;
             }
-            auto it = index.find(hname);
-            if (it != index.end()) {
-                rc = handle(it->second, flags, fd, nullptr);
+            const int peer = pfd_peer[q];
+            auto it        = index.find(hname);
+            if (it != index.end() && expects(it->second, flags, peer)) {
+                rc = handle(it->second, flags, peer, fd, nullptr);
                 continue;
             }
-            // not ours (yet): keep it for the all-reduce that owns the name
-            Stashed m{hname, flags, {}};
+            // not ours (yet): keep it for the all-reduce call it belongs to
+            Stashed m{peer, hname, flags, {}};
             uint32_t len = 0;
             unsigned char lb[4];
             rc = read_exact(fd, lb, 4);
@@ -651,16 +901,17 @@ int kf_session::all_reduce(const char *send, char *recv, size_t count, KungFu_Da
 
 extern "C" {
 
-kf_session_t *kf_session_create(int rank, int size, const char *sock_dir, uint32_t token,
-                                int device_mode)
+}  // extern "C"
+
+namespace
 {
-    if (size < 1 || rank < 0 || rank >= size || !sock_dir) {
-        t_sess_error = "bad rank/size/dir";
-        return nullptr;
-    }
+kf_session_t *create_session(int rank, std::vector<PeerAddr> peers, const char *sock_dir,
+                             uint32_t token, int device_mode)
+{
     auto *s        = new kf_session;
     s->rank        = rank;
-    s->size        = size;
+    s->size        = static_cast<int>(peers.size());
+    s->peers       = std::move(peers);
     s->dir         = sock_dir;
     s->token       = token;
     s->device_mode = device_mode ? 1 : 0;
@@ -679,7 +930,7 @@ kf_session_t *kf_session_create(int rank, int size, const char *sock_dir, uint32
     if (const char *e = std::getenv("KUNGFU_CONFIG_STRATEGY_HASH_METHOD")) {
         s->hash_name = std::strcmp(e, "NAME") == 0 || std::strcmp(e, "name") == 0;
     }
-    s->sl = strategy_list(s->strategy, size);
+    s->sl = strategy_list(s->strategy, s->hosts());
     if (s->device_mode) {
         s->ingest = kf_ingest_create(kChunk + 4096, 8);
         s->egress = kf_ingest_create(kChunk + 4096, 2);
@@ -689,12 +940,55 @@ kf_session_t *kf_session_create(int rank, int size, const char *sock_dir, uint32
             return nullptr;
         }
     }
-    if (size > 1 && s->connect_all() != KF_OK) {
+    if (s->size > 1 && s->connect_all() != KF_OK) {
         delete s;
         return nullptr;
     }
     s->sender = std::thread([s] { s->sender_loop(); });
     return s;
+}
+}  // namespace
+
+extern "C" {
+
+kf_session_t *kf_session_create(int rank, int size, const char *sock_dir, uint32_t token,
+                                int device_mode)
+{
+    if (size < 1 || rank < 0 || rank >= size || !sock_dir) {
+        t_sess_error = "bad rank/size/dir";
+        return nullptr;
+    }
+    // one host: 127.0.0.1, ports 10000 + rank (hostspec.go:121-124)
+    std::vector<PeerAddr> peers;
+    for (int r = 0; r < size; ++r) peers.push_back({kIPv4, static_cast<uint16_t>(kPortBase + r)});
+    return create_session(rank, std::move(peers), sock_dir, token, device_mode);
+}
+
+kf_session_t *kf_session_create_peers(const char *peer_list, const char *self_spec,
+                                      const char *sock_dir, uint32_t token, int device_mode)
+{
+    std::vector<PeerAddr> peers;
+    PeerAddr self;
+    if (!peer_list || !self_spec || !sock_dir || !parse_peer_list(peer_list, &peers) ||
+        !parse_peer(self_spec, &self)) {
+        t_sess_error = "bad peer list / self spec (want ipv4:port[,ipv4:port...])";
+        return nullptr;
+    }
+    int rank = -1;
+    for (size_t r = 0; r < peers.size(); ++r) {
+        for (size_t q = 0; q < r; ++q) {
+            if (peers[q] == peers[r]) {
+                t_sess_error = "duplicate peer in the list";
+                return nullptr;
+            }
+        }
+        if (peers[r] == self) rank = static_cast<int>(r);
+    }
+    if (rank < 0) {  // peer.go: self must be in the initial cluster
+        t_sess_error = std::string("self ") + self_spec + " not in the peer list";
+        return nullptr;
+    }
+    return create_session(rank, std::move(peers), sock_dir, token, device_mode);
 }
 
 int kf_session_set_strategy(kf_session_t *s, int strategy, int hash_by_name)
@@ -702,7 +996,7 @@ int kf_session_set_strategy(kf_session_t *s, int strategy, int hash_by_name)
     if (!s || strategy < KungFu_Tree || strategy > KungFu_AUTO) return KF_ERR_ARG;
     s->strategy  = strategy;
     s->hash_name = hash_by_name ? 1 : 0;
-    s->sl        = strategy_list(strategy, s->size);
+    s->sl        = strategy_list(strategy, s->hosts());
     return KF_OK;
 }
 

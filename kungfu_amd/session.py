@@ -33,14 +33,30 @@ STRATEGIES = {
 
 
 class Session:
-    def __init__(self, rank, size, sock_dir, mode="device", token=0,
-                 host_reduce_fn=None, strategy=None, hash_method="NAME"):
+    """Peer `rank` of `size` on this host, or — with ``peers`` (the
+    KUNGFU_INIT_PEERS list, "ip:port,...") and ``self_spec`` (KUNGFU_SELF_SPEC)
+    — a peer of a multi-host cluster: colocated peers use unix sockets under
+    ``sock_dir``, the others TCP; multi-host strategies follow the hosts."""
+
+    def __init__(self, rank=None, size=None, sock_dir="/tmp", mode="device", token=0,
+                 host_reduce_fn=None, strategy=None, hash_method="NAME",
+                 peers=None, self_spec=None):
         if mode not in ("device", "host"):
             raise ValueError(mode)
-        self.rank, self.size, self.mode = rank, size, mode
+        self.mode = mode
         self.lib = _lib.load()
-        self._h = self.lib.kf_session_create(rank, size, sock_dir.encode(), token,
-                                             1 if mode == "device" else 0)
+        dm = 1 if mode == "device" else 0
+        if peers is not None:
+            plist = peers.split(",") if isinstance(peers, str) else list(peers)
+            if self_spec not in plist:
+                raise ValueError("self %r not in peer list" % (self_spec,))
+            self.rank, self.size = plist.index(self_spec), len(plist)
+            self._h = self.lib.kf_session_create_peers(",".join(plist).encode(),
+                                                       self_spec.encode(), sock_dir.encode(),
+                                                       token, dm)
+        else:
+            self.rank, self.size = rank, size
+            self._h = self.lib.kf_session_create(rank, size, sock_dir.encode(), token, dm)
         if not self._h:
             raise _lib.KungFuAMDError("kf_session_create: " +
                                       self.lib.kf_session_last_error().decode())
@@ -53,6 +69,14 @@ class Session:
                 raise ValueError("host_reduce_fn needs mode='host'")
             _lib.check(self.lib.kf_session_set_host_reduce(self._h, host_reduce_fn),
                        "kf_session_set_host_reduce")
+
+    @classmethod
+    def from_env(cls, sock_dir="/tmp", **kw):
+        """As a peer started by kungfu-run: KUNGFU_INIT_PEERS / KUNGFU_SELF_SPEC
+        (srcs/go/kungfu/env/envs.go:9-11)."""
+        import os
+        return cls(peers=os.environ["KUNGFU_INIT_PEERS"],
+                   self_spec=os.environ["KUNGFU_SELF_SPEC"], sock_dir=sock_dir, **kw)
 
     def close(self):
         if self._h:

@@ -194,3 +194,148 @@ def test_session_device_batched_iota():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     run(4, "device", "iota", (3 << 20) // 4 + 5)
+
+
+def _repeat_body(rank, size, sock_dir, strategy, steps, errq):
+    sys.path[:0] = [ROOT, HERE]
+    try:
+        os.environ["KUNGFU_ALLREDUCE_STRATEGY"] = strategy
+        from kungfu_amd.session import Session
+        s = Session(rank, size, sock_dir, mode="host", host_reduce_fn=oracle_reduce_fn())
+        n = (3 << 20) // 4 + 5
+        for t in range(steps):
+            # the same name every step, as an optimizer's gradient all-reduce
+            x = (np.arange(n) * (rank + 1) + t).astype(np.int32)
+            y = np.zeros_like(x)
+            s.all_reduce(x, y, "grad")
+            want = (np.arange(n) * (size * (size + 1) // 2) + size * t).astype(np.int32)
+            assert np.array_equal(y, want), (rank, t)
+        s.close()
+    except Exception:
+        errq.put("rank %d: %s" % (rank, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("strategy,size", [("RING", 4), ("BINARY_TREE", 5), ("CLIQUE", 3),
+                                           ("STAR", 4)])
+def test_session_same_name_back_to_back(strategy, size):
+    # a peer that finished step t may send step t+1's message for a chunk
+    # while this peer still polls for step t: it must wait for step t+1
+    # (the reference's per-name mailbox, handler/collective.go:27-61)
+    ctx = mp.get_context("spawn")
+    errq = ctx.SimpleQueue()
+    with tempfile.TemporaryDirectory() as d:
+        ps = [ctx.Process(target=_repeat_body, args=(r, size, d, strategy, 40, errq))
+              for r in range(size)]
+        for p in ps:
+            p.start()
+        for p in ps:
+            p.join(timeout=300)
+    errs = []
+    while not errq.empty():
+        errs.append(errq.get())
+    assert not errs, "\n".join(errs)
+    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+
+
+def _fake_peer(sock_dir, token, msgs, n_bcast, out, err):
+    """Rank 1 of 2 speaking the rchannel protocol by hand: sends `msgs`
+    (name, flags, payload) in the given order, then reads n_bcast messages."""
+    import socket
+    import struct
+    import threading
+    import time
+    try:
+        me = os.path.join(sock_dir, "kungfu-amd-127.0.0.1-10001.sock")
+        root = os.path.join(sock_dir, "kungfu-amd-127.0.0.1-10000.sock")
+        srv = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+        srv.bind(me)
+        srv.listen(1)
+        c = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+        for _ in range(500):
+            try:
+                c.connect(root)
+                break
+            except OSError:
+                time.sleep(0.05)
+        # connection header {u16 type=Collective, u16 port, u32 ipv4}, then ack
+        c.sendall(struct.pack("<HHI", 2, 10001, 0x7F000001))
+        assert struct.unpack("<I", c.recv(4))[0] == token
+        a, _ = srv.accept()
+        hdr = b""
+        while len(hdr) < 8:
+            hdr += a.recv(8 - len(hdr))
+        a.sendall(struct.pack("<I", token))
+
+        def exact(k):
+            b = b""
+            while len(b) < k:
+                chunk = a.recv(k - len(b))
+                assert chunk, "root closed early"
+                b += chunk
+            return b
+
+        def reader():  # a real peer reads while it writes
+            try:
+                for _ in range(n_bcast):
+                    nl = struct.unpack("<I", exact(4))[0]
+                    name = exact(nl).decode()
+                    flags, ln = struct.unpack("<II", exact(8))
+                    out.append((name, flags, exact(ln)))
+            except Exception:
+                err.append(traceback.format_exc())
+        rd = threading.Thread(target=reader)
+        rd.start()
+        for name, flags, payload in msgs:
+            nb = name.encode()
+            c.sendall(struct.pack("<I", len(nb)) + nb + struct.pack("<II", flags, len(payload))
+                      + payload)
+        rd.join(timeout=60)
+        c.close()
+        a.close()
+        srv.close()
+    except Exception:
+        err.append(traceback.format_exc())
+
+
+@pytest.mark.timeout(120)
+def test_session_next_step_message_waits_for_its_call():
+    # the fake peer interleaves step t+1's chunk-0 message between step t's
+    # chunk-0 and chunk-1 messages, as messages from several peers can
+    # interleave; the root must keep it for step t+1 (per-name mailbox,
+    # handler/collective.go:27-61) instead of folding it twice into step t
+    import threading
+    from kungfu_amd.base import EvenPartition
+    from kungfu_amd.session import Session
+    n = (1 << 18) + 3  # 2 chunks of int32
+    parts = list(EvenPartition(0, n, 2))
+    names = ["part::grad[%d:%d]" % (b, e) for b, e in parts]
+    x1 = [np.arange(n, dtype=np.int32) * 3, np.arange(n, dtype=np.int32) * 5 + 1]
+    msgs = [(names[0], 0, x1[0][parts[0][0]:parts[0][1]].tobytes()),
+            (names[0], 0, x1[1][parts[0][0]:parts[0][1]].tobytes()),  # step 1, early
+            (names[1], 0, x1[0][parts[1][0]:parts[1][1]].tobytes()),
+            (names[1], 0, x1[1][parts[1][0]:parts[1][1]].tobytes())]
+    out, err = [], []
+    with tempfile.TemporaryDirectory() as d:
+        t = threading.Thread(target=_fake_peer, args=(d, 7, msgs, 4, out, err))
+        t.start()
+        os.environ.pop("KUNGFU_ALLREDUCE_STRATEGY", None)
+        s = Session(0, 2, d, mode="host", token=7, host_reduce_fn=oracle_reduce_fn())
+        x0 = [np.arange(n, dtype=np.int32) + 7, np.arange(n, dtype=np.int32) * 2]
+        ys = []
+        for step in range(2):
+            y = np.zeros(n, np.int32)
+            s.all_reduce(x0[step], y, "grad")
+            ys.append(y)
+        t.join(timeout=60)
+        s.close()
+    assert not err, err[0]
+    for step in range(2):
+        assert np.array_equal(ys[step], x0[step] + x1[step]), step
+    # the bcast the peer received: step 0 then step 1, both chunks, WaitRecvBuf
+    got = {}
+    for name, flags, data in out:
+        assert flags == 1
+        got.setdefault(name, []).append(np.frombuffer(data, np.int32))
+    for c, (b, e) in enumerate(parts):
+        for step in range(2):
+            assert np.array_equal(got[names[c]][step], (x0[step] + x1[step])[b:e])
