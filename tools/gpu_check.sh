@@ -21,7 +21,7 @@ step() {  # step <name> <timeout> <cmd...>
     return $rc
 }
 
-step pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider
+step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread
 rc=$?
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "pytest crashed ($rc): stop"; exit $rc; fi
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
