@@ -154,10 +154,19 @@ def cpu_baseline(x, y, seconds):
                     break
     except OSError:
         pass
+    # the reference's goroutine-per-chunk fan-out (session.go:317-323) over
+    # the box's CPU share: 1 MiB chunks from a work queue on T threads
+    nt = min(16, os.cpu_count() or 1)
+    tm1 = oracle.bench_transform2(xh, yh, zh, "f32", "sum", 2, threads=nt) / 2
+    mreps = max(1, min(1000, int(seconds / 2 / max(tm1, 1e-6))))
+    tm = oracle.bench_transform2(xh, yh, zh, "f32", "sum", mreps, threads=nt)
     return {
         "value": round(reps * s_bytes / t / 2**30, 3),
         "unit": "GiB/s",
         "cores": 1,
+        "multi_thread": {"value": round(mreps * s_bytes / tm / 2**30, 3), "unit": "GiB/s",
+                         "cores": nt, "sample": "%d x 256 MiB in 1 MiB chunks, %.1f s"
+                                                % (mreps, tm)},
         "kind": "port",
         "sample": "%d x std_transform_2(f32, SUM) over the same 256 MiB bucket, "
                   "1 thread, oracle restatement built -O2 -mavx -mf16c, %.1f s, %s"
@@ -166,9 +175,12 @@ def cpu_baseline(x, y, seconds):
 
 
 def host_staged(lib, x, y):
-    """Copy-inclusive rate of the drop-in: host x,y -> HBM -> kernel -> host z
-    (std_transform_2's path), from pageable buffers and from pinned buffers
-    (16 MiB chunks over two streams). Never `value`."""
+    """Copy-inclusive rate of the drop-in (std_transform_2's path): pageable
+    host buffers (copied to HBM and back through the runtime's staging) and
+    page-locked ones (zero copy: the kernel reads x, y and writes z in host
+    memory over PCIe); plus the latency of one 1 MiB chunk, the reference's
+    unit of work (session.go:301-304), next to the CPU restatement's.
+    Never `value` (DESIGN.md)."""
     res = {}
     for kind in ("pageable", "pinned"):
         xh, yh = x.cpu(), y.cpu()
@@ -189,8 +201,34 @@ def host_staged(lib, x, y):
         ok = bool(torch.equal(zh, xh + yh))
         res[kind] = {"value": round(xh.numel() * 4 / t / 2**30, 3), "unit": "GiB/s",
                      "ms_per_call": round(t * 1e3, 3), "correct": ok}
-    res["path"] = "host x,y -> HBM -> HIP kernel -> host z (PCIe incl.), 256 MiB fp32"
+    res["path"] = ("host x,y -> HIP kernel -> host z (PCIe incl.), 256 MiB fp32; "
+                   "pageable: staged through HBM; pinned: zero copy")
+    res["chunk_1MiB"] = chunk_latency(lib, x)
     return res
+
+
+def chunk_latency(lib, x, reps=2000):
+    """One 1 MiB fp32 chunk through std_transform_2 with page-locked buffers,
+    and through the oracle's restatement of the reference reduce (1 thread)."""
+    from oracle import oracle
+    n = (1 << 20) // 4
+    xh = x[:n].cpu().pin_memory()
+    yh = x[n:2 * n].cpu().pin_memory()
+    zh = torch.empty_like(xh).pin_memory()
+    args = (xh.data_ptr(), yh.data_ptr(), zh.data_ptr(), n, KF_FLOAT, KF_SUM)
+    for _ in range(20):
+        lib.std_transform_2(*args)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        lib.std_transform_2(*args)
+    gpu_s = (time.perf_counter() - t0) / reps
+    ok = bool(torch.equal(zh, xh + yh))
+    xa, ya = xh.numpy().copy(), yh.numpy().copy()
+    za = np.empty_like(xa)
+    oracle.bench_transform2(xa, ya, za, "f32", "sum", 20, threads=1)
+    cpu_s = oracle.bench_transform2(xa, ya, za, "f32", "sum", reps, threads=1) / reps
+    return {"gpu_pinned_us": round(gpu_s * 1e6, 2), "cpu_port_us": round(cpu_s * 1e6, 2),
+            "correct": ok, "reps": reps}
 
 
 # ---- C1: np = 2 plumbing over the rchannel wire format ----------------------

@@ -162,12 +162,12 @@ int kf_host_unregister(void *p);
 int kf_set_geometry(int unroll, int grid_cap, int loadnt, int stplain);
 
 /* Host-pointer reduce with a status code instead of exit(): the path
- * std_transform_2 takes. Synchronous, per-thread streams and device scratch.
- * If x, y and out are all page-locked (hipHostMalloc or kf_host_register)
- * the bucket moves in 16 MiB chunks alternating over two streams (H2D of
- * chunk i+1 overlaps kernel + D2H of chunk i); otherwise pageable copies
- * through the runtime's staging. Used by the copy-inclusive measurement
- * (bench.py host_staged). */
+ * std_transform_2 takes. Synchronous, per-thread stream and device scratch.
+ * If x, y and out are all device-accessible (page-locked by hipHostMalloc or
+ * kf_host_register, or HBM of the current device) the kernel reads and writes
+ * them in place (zero copy, over PCIe for host memory); otherwise pageable
+ * copies through the runtime's staging to HBM scratch and back. Used by the
+ * copy-inclusive measurement (bench.py host_staged). */
 int kf_transform2_host(const void *x, const void *y, void *out, size_t n,
                        KungFu_Datatype dt, KungFu_Op op);
 

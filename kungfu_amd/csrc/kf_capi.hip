@@ -98,7 +98,8 @@ Div make_div(int np)
 // ---------------------------------------------------------------------------
 struct Plan {
     size_t head = 0, nvec = 0;
-    bool vec_ok = false;
+    bool vec_ok  = false;
+    int grid_cap = 0;  // 0: geometry().grid_cap (HBM); >0: host-link launch
 };
 
 // Vector body needs every pointer at the same 16-B residue; the head peels
@@ -119,14 +120,13 @@ Plan make_plan(const void *const *in, int k, const void *out, size_t n, int sz)
     return p;
 }
 
-unsigned grid_for(size_t nvec, size_t nedge, int unroll)
+unsigned grid_for(size_t nvec, size_t nedge, int unroll, int cap = 0)
 {
     const size_t tile   = static_cast<size_t>(kBlock) * unroll;
     size_t blocks       = (nvec + tile - 1) / tile;
     const size_t eblk   = (nedge + kBlock - 1) / kBlock;
-    if (blocks > static_cast<size_t>(geometry().grid_cap)) {
-        blocks = geometry().grid_cap;
-    }
+    if (cap <= 0) cap = geometry().grid_cap;
+    if (blocks > static_cast<size_t>(cap)) blocks = cap;
     if (blocks < eblk) blocks = eblk;
     if (blocks < 1) blocks = 1;
     return static_cast<unsigned>(blocks);
@@ -138,7 +138,7 @@ void launch_vec(const InPtrs &ptrs, int k, void *out, size_t n, const Plan &p,
 {
     constexpr int V  = Vec<typename Elt<T>::S>::N;
     const size_t ned = p.head + (n - p.head - p.nvec * V);
-    const unsigned g = grid_for(p.nvec, ned, UNROLL);
+    const unsigned g = grid_for(p.nvec, ned, UNROLL, p.grid_cap);
     reduce_kernel<T, OP, EPI, KC, kBlock, UNROLL, LOADNT, STPLAIN>
         <<<g, kBlock, 0, s>>>(ptrs, k, out, n, p.head, p.nvec, np);
 }
@@ -191,16 +191,18 @@ void launch_k(const InPtrs &ptrs, int k, void *out, size_t n, const Plan &p,
 
 template <typename T, int OP, int EPI>
 int launch_typed(const void *const *in, int k, void *out, size_t n, int npi,
-                 hipStream_t s)
+                 hipStream_t s, int grid_cap)
 {
     const Div np = make_div(npi);
     using S = typename Elt<T>::S;
     InPtrs ptrs;
     for (int j = 0; j < kMaxInputs; ++j) ptrs.p[j] = j < k ? in[j] : nullptr;
-    const Plan p = make_plan(in, k, out, n, sizeof(S));
+    Plan p     = make_plan(in, k, out, n, sizeof(S));
+    p.grid_cap = grid_cap;
     if (!p.vec_ok) {
         size_t blocks = (n + kBlock - 1) / kBlock;
-        if (blocks > 8192) blocks = 8192;
+        const size_t cap = grid_cap > 0 ? static_cast<size_t>(grid_cap) : 8192;
+        if (blocks > cap) blocks = cap;
         reduce_kernel_unaligned<T, OP, EPI, kBlock>
             <<<static_cast<unsigned>(blocks), kBlock, 0, s>>>(ptrs, k, out, n, np);
     } else {
@@ -213,21 +215,21 @@ int launch_typed(const void *const *in, int k, void *out, size_t n, int npi,
 
 template <typename T, int EPI>
 int dispatch_op(const void *const *in, int k, void *out, size_t n, KungFu_Op op,
-                int np, hipStream_t s)
+                int np, hipStream_t s, int gc)
 {
     if constexpr (std::is_same<T, f16_t>::value) {
         if (op != KungFu_SUM) return KF_ERR_OP;  // op.cpp:45-54
-        return launch_typed<T, OP_SUM, EPI>(in, k, out, n, np, s);
+        return launch_typed<T, OP_SUM, EPI>(in, k, out, n, np, s, gc);
     } else {
         if constexpr (EPI == EPI_DIV) {
             if (op != KungFu_SUM) return KF_ERR_OP;
-            return launch_typed<T, OP_SUM, EPI>(in, k, out, n, np, s);
+            return launch_typed<T, OP_SUM, EPI>(in, k, out, n, np, s, gc);
         } else {
             switch (op) {
-            case KungFu_SUM: return launch_typed<T, OP_SUM, EPI>(in, k, out, n, np, s);
-            case KungFu_MIN: return launch_typed<T, OP_MIN, EPI>(in, k, out, n, np, s);
-            case KungFu_MAX: return launch_typed<T, OP_MAX, EPI>(in, k, out, n, np, s);
-            case KungFu_PROD: return launch_typed<T, OP_PROD, EPI>(in, k, out, n, np, s);
+            case KungFu_SUM: return launch_typed<T, OP_SUM, EPI>(in, k, out, n, np, s, gc);
+            case KungFu_MIN: return launch_typed<T, OP_MIN, EPI>(in, k, out, n, np, s, gc);
+            case KungFu_MAX: return launch_typed<T, OP_MAX, EPI>(in, k, out, n, np, s, gc);
+            case KungFu_PROD: return launch_typed<T, OP_PROD, EPI>(in, k, out, n, np, s, gc);
             default: return KF_ERR_OP;
             }
         }
@@ -235,21 +237,21 @@ int dispatch_op(const void *const *in, int k, void *out, size_t n, KungFu_Op op,
 }
 
 int dispatch_none(const void *const *in, int k, void *out, size_t n,
-                  KungFu_Datatype dt, KungFu_Op op, hipStream_t s)
+                  KungFu_Datatype dt, KungFu_Op op, hipStream_t s, int gc = 0)
 {
     switch (dt) {
-    case KungFu_UINT8: return dispatch_op<uint8_t, EPI_NONE>(in, k, out, n, op, 1, s);
-    case KungFu_UINT16: return dispatch_op<uint16_t, EPI_NONE>(in, k, out, n, op, 1, s);
-    case KungFu_UINT32: return dispatch_op<uint32_t, EPI_NONE>(in, k, out, n, op, 1, s);
-    case KungFu_UINT64: return dispatch_op<uint64_t, EPI_NONE>(in, k, out, n, op, 1, s);
-    case KungFu_INT8: return dispatch_op<int8_t, EPI_NONE>(in, k, out, n, op, 1, s);
-    case KungFu_INT16: return dispatch_op<int16_t, EPI_NONE>(in, k, out, n, op, 1, s);
-    case KungFu_INT32: return dispatch_op<int32_t, EPI_NONE>(in, k, out, n, op, 1, s);
-    case KungFu_INT64: return dispatch_op<int64_t, EPI_NONE>(in, k, out, n, op, 1, s);
-    case KungFu_FLOAT16: return dispatch_op<f16_t, EPI_NONE>(in, k, out, n, op, 1, s);
-    case KungFu_FLOAT: return dispatch_op<float, EPI_NONE>(in, k, out, n, op, 1, s);
-    case KungFu_DOUBLE: return dispatch_op<double, EPI_NONE>(in, k, out, n, op, 1, s);
-    case KungFu_BFLOAT16: return dispatch_op<bf16_t, EPI_NONE>(in, k, out, n, op, 1, s);
+    case KungFu_UINT8: return dispatch_op<uint8_t, EPI_NONE>(in, k, out, n, op, 1, s, gc);
+    case KungFu_UINT16: return dispatch_op<uint16_t, EPI_NONE>(in, k, out, n, op, 1, s, gc);
+    case KungFu_UINT32: return dispatch_op<uint32_t, EPI_NONE>(in, k, out, n, op, 1, s, gc);
+    case KungFu_UINT64: return dispatch_op<uint64_t, EPI_NONE>(in, k, out, n, op, 1, s, gc);
+    case KungFu_INT8: return dispatch_op<int8_t, EPI_NONE>(in, k, out, n, op, 1, s, gc);
+    case KungFu_INT16: return dispatch_op<int16_t, EPI_NONE>(in, k, out, n, op, 1, s, gc);
+    case KungFu_INT32: return dispatch_op<int32_t, EPI_NONE>(in, k, out, n, op, 1, s, gc);
+    case KungFu_INT64: return dispatch_op<int64_t, EPI_NONE>(in, k, out, n, op, 1, s, gc);
+    case KungFu_FLOAT16: return dispatch_op<f16_t, EPI_NONE>(in, k, out, n, op, 1, s, gc);
+    case KungFu_FLOAT: return dispatch_op<float, EPI_NONE>(in, k, out, n, op, 1, s, gc);
+    case KungFu_DOUBLE: return dispatch_op<double, EPI_NONE>(in, k, out, n, op, 1, s, gc);
+    case KungFu_BFLOAT16: return dispatch_op<bf16_t, EPI_NONE>(in, k, out, n, op, 1, s, gc);
     default: return KF_ERR_DTYPE;  // BOOL and unknown: op.cpp:88-89
     }
 }
@@ -258,10 +260,10 @@ int dispatch_div(const void *const *in, int k, void *out, size_t n,
                  KungFu_Datatype dt, int np, hipStream_t s)
 {
     switch (dt) {
-    case KungFu_FLOAT16: return dispatch_op<f16_t, EPI_DIV>(in, k, out, n, KungFu_SUM, np, s);
-    case KungFu_FLOAT: return dispatch_op<float, EPI_DIV>(in, k, out, n, KungFu_SUM, np, s);
-    case KungFu_DOUBLE: return dispatch_op<double, EPI_DIV>(in, k, out, n, KungFu_SUM, np, s);
-    case KungFu_BFLOAT16: return dispatch_op<bf16_t, EPI_DIV>(in, k, out, n, KungFu_SUM, np, s);
+    case KungFu_FLOAT16: return dispatch_op<f16_t, EPI_DIV>(in, k, out, n, KungFu_SUM, np, s, 0);
+    case KungFu_FLOAT: return dispatch_op<float, EPI_DIV>(in, k, out, n, KungFu_SUM, np, s, 0);
+    case KungFu_DOUBLE: return dispatch_op<double, EPI_DIV>(in, k, out, n, KungFu_SUM, np, s, 0);
+    case KungFu_BFLOAT16: return dispatch_op<bf16_t, EPI_DIV>(in, k, out, n, KungFu_SUM, np, s, 0);
     default: return KF_ERR_DTYPE;
     }
 }
@@ -301,52 +303,59 @@ int launch_sma(void *v, const void *sum, size_t n, int np, C c1, C c2,
 }
 
 // ---------------------------------------------------------------------------
-// B1 support: per-thread staging context
+// B1 support: host pointers
 // ---------------------------------------------------------------------------
-constexpr int kSlots = 3;                        // pipeline depth
-constexpr size_t kChunkBytes = size_t(16) << 20;  // per input per slot
+// Page-locked host memory is mapped into the GPU's address space, so when x, y
+// and out are all device-accessible (page-locked host or HBM) the reduce
+// kernel reads and writes them in place over PCIe: one launch, no copies.
+// Measured on MI355X (tools/explore/zc_explore.hip, profiles/r01/zc.jsonl):
+// 256 MiB fp32 9.39 ms (the H2D bound for 512 MiB at 57.6 GB/s is 9.3 ms)
+// against 10.49 ms for 16 MiB chunks staged through HBM on two streams, and
+// 59 us against 104 us for a 1 MiB chunk (the reference's chunk size). The
+// link is the bound, so a small grid is enough and leaves the rest of the
+// chip free: `kHostGrid` blocks (32 or 64 measured best of 32..4096:
+// 9.47-9.49 ms per 256 MiB, 61 us per 1 MiB at 32; profiles/r01/zc_grid.txt).
+constexpr int kHostGrid = 32;
 
-// Two streams with one DMA direction each: the measured link is full duplex
-// (tools/explore/pcie_explore.hip: 57.6 GB/s H2D and 56.9 GB/s D2H, both at
-// once in 9.4 ms vs 14.0 ms serial), but the copies of ONE stream run in order
-// through one engine, so H2D and D2H must sit on different streams.
+int host_grid()
+{
+    static const int g = [] {
+        const char *e = std::getenv("KUNGFU_AMD_HOST_GRID");  // tuning only
+        const int v   = e ? std::atoi(e) : 0;
+        return v > 0 ? v : kHostGrid;
+    }();
+    return g;
+}
+
+// Per-thread stream + HBM scratch for pageable buffers.
 struct Staging {
-    hipStream_t in  = nullptr;  // H2D + kernel
-    hipStream_t out = nullptr;  // D2H
-    hipEvent_t k_done[kSlots]   = {};
-    hipEvent_t out_done[kSlots] = {};
-    void *dev                   = nullptr;  // 3 regions: x | y | z
-    size_t cap                  = 0;        // bytes per region
-    int device                  = -1;
+    hipStream_t s = nullptr;
+    void *dev     = nullptr;  // 3 regions: x | y | z
+    size_t cap    = 0;        // bytes per region
 
     ~Staging()
     {
         // Process teardown may have unloaded the runtime already; best effort.
         if (dev) (void)hipFree(dev);
-        for (int i = 0; i < kSlots; ++i) {
-            if (k_done[i]) (void)hipEventDestroy(k_done[i]);
-            if (out_done[i]) (void)hipEventDestroy(out_done[i]);
+        if (s) (void)hipStreamDestroy(s);
+    }
+
+    int ensure_stream()
+    {
+        if (s) return KF_OK;
+        int cnt = 0;
+        if (hipGetDeviceCount(&cnt) != hipSuccess || cnt == 0) {
+            t_last_error = "no HIP device";
+            return KF_ERR_NO_DEVICE;
         }
-        if (in) (void)hipStreamDestroy(in);
-        if (out) (void)hipStreamDestroy(out);
+        KF_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        return KF_OK;
     }
 
     int ensure(size_t bytes)
     {
-        if (!in) {
-            int cnt = 0;
-            if (hipGetDeviceCount(&cnt) != hipSuccess || cnt == 0) {
-                t_last_error = "no HIP device";
-                return KF_ERR_NO_DEVICE;
-            }
-            KF_HIP(hipGetDevice(&device));
-            KF_HIP(hipStreamCreateWithFlags(&in, hipStreamNonBlocking));
-            KF_HIP(hipStreamCreateWithFlags(&out, hipStreamNonBlocking));
-            for (int i = 0; i < kSlots; ++i) {
-                KF_HIP(hipEventCreateWithFlags(&k_done[i], hipEventDisableTiming));
-                KF_HIP(hipEventCreateWithFlags(&out_done[i], hipEventDisableTiming));
-            }
-        }
+        int rc = ensure_stream();
+        if (rc != KF_OK) return rc;
         if (bytes > cap) {
             if (dev) KF_HIP(hipFree(dev));
             dev            = nullptr;
@@ -360,31 +369,38 @@ struct Staging {
 
 thread_local Staging t_staging;
 
-// True when the whole range is page-locked host memory the GPU can DMA
-// (hipHostMalloc'ed, or registered with kf_host_register).
-bool is_pinned(const void *p, size_t bytes)
+// Where a host-API pointer lives: 0 pageable (or unknown to HIP), 1 page-locked
+// host memory (hipHostMalloc / kf_host_register), 2 device memory. `dev` is the
+// address a kernel uses for it. The whole range must be one kind.
+int classify(const void *p, size_t bytes, const void **dev)
 {
-    if (!p) return false;
     hipPointerAttribute_t a;
     if (hipPointerGetAttributes(&a, p) != hipSuccess) {
         (void)hipGetLastError();
-        return false;
+        return 0;
     }
-    if (a.type != hipMemoryTypeHost) return false;
+    int kind = a.type == hipMemoryTypeHost ? 1 : a.type == hipMemoryTypeDevice ? 2 : 0;
+    if (kind == 0 || !a.devicePointer) return 0;
     const void *last = static_cast<const char *>(p) + bytes - 1;
     hipPointerAttribute_t b;
     if (hipPointerGetAttributes(&b, last) != hipSuccess) {
         (void)hipGetLastError();
-        return false;
+        return 0;
     }
-    return b.type == hipMemoryTypeHost;
+    if (b.type != a.type) return 0;
+    if (kind == 2) {  // HBM of another GPU: leave it to the runtime's copies
+        int cur = -1;
+        if (hipGetDevice(&cur) != hipSuccess || cur != a.device) return 0;
+    }
+    *dev = a.devicePointer;
+    return kind;
 }
 
-// Host pointers -> HBM -> kernel -> host. Synchronous.
-//  * pinned x, y, out: 16 MiB chunks through kSlots device slots; per chunk
-//    `in` copies x, y up and runs the kernel, `out` copies z down, so chunk
-//    i's D2H overlaps chunk i+1's H2D (events order slot reuse);
-//  * pageable: whole-buffer copies through the runtime's staging.
+// Host pointers -> reduce -> host. Synchronous.
+//  * all three device-accessible: the kernel works on them in place (zero
+//    copy; over PCIe for page-locked host memory, at the link's rate);
+//  * otherwise: whole-buffer copies through the runtime's staging to HBM
+//    scratch, the kernel, and a copy back.
 int transform2_host(const void *x, const void *y, void *out, size_t n,
                     KungFu_Datatype dt, KungFu_Op op)
 {
@@ -392,53 +408,34 @@ int transform2_host(const void *x, const void *y, void *out, size_t n,
     if (sz == 0 || dt == KungFu_BOOL) return KF_ERR_DTYPE;
     if (n == 0) return KF_OK;
     const size_t bytes = n * static_cast<size_t>(sz);
-    const bool pinned  = bytes > kChunkBytes && is_pinned(x, bytes) &&
-                        is_pinned(y, bytes) && is_pinned(out, bytes);
-    Staging &st = t_staging;
-    int rc      = st.ensure(pinned ? kSlots * kChunkBytes : bytes);
+    Staging &st        = t_staging;
+    const void *gx = nullptr, *gy = nullptr, *gz = nullptr;
+    const int kx = classify(x, bytes, &gx);
+    const int ky = kx ? classify(y, bytes, &gy) : 0;
+    const int kz = ky ? classify(out, bytes, &gz) : 0;
+    if (kx && ky && kz) {
+        int rc = st.ensure_stream();
+        if (rc != KF_OK) return rc;
+        const bool host_link = kx == 1 || ky == 1 || kz == 1;
+        const void *ins[2]   = {gx, gy};
+        rc = dispatch_none(ins, 2, const_cast<void *>(gz), n, dt, op, st.s,
+                           host_link ? host_grid() : 0);
+        if (rc != KF_OK) return rc;
+        KF_HIP(hipStreamSynchronize(st.s));
+        return KF_OK;
+    }
+    int rc = st.ensure(bytes);
     if (rc != KF_OK) return rc;
     char *dx = static_cast<char *>(st.dev);
     char *dy = dx + st.cap;
     char *dz = dy + st.cap;
-    if (!pinned) {
-        hipStream_t s = st.in;
-        KF_HIP(hipMemcpyAsync(dx, x, bytes, hipMemcpyHostToDevice, s));
-        KF_HIP(hipMemcpyAsync(dy, y, bytes, hipMemcpyHostToDevice, s));
-        const void *ins[2] = {dx, dy};
-        rc                 = dispatch_none(ins, 2, dz, n, dt, op, s);
-        if (rc != KF_OK) return rc;
-        KF_HIP(hipMemcpyAsync(out, dz, bytes, hipMemcpyDeviceToHost, s));
-        KF_HIP(hipStreamSynchronize(s));
-        return KF_OK;
-    }
-    const size_t chunk_elems = kChunkBytes / sz;
-    const char *hx = static_cast<const char *>(x);
-    const char *hy = static_cast<const char *>(y);
-    char *hz       = static_cast<char *>(out);
-    size_t i       = 0;
-    for (size_t b = 0; b < n; b += chunk_elems, ++i) {
-        const size_t m   = n - b < chunk_elems ? n - b : chunk_elems;
-        const size_t off = b * sz, len = m * sz;
-        const int slot   = static_cast<int>(i % kSlots);
-        char *sx = dx + slot * kChunkBytes, *sy = dy + slot * kChunkBytes,
-             *szz = dz + slot * kChunkBytes;
-        // x/y slots: their last reader was the kernel kSlots chunks ago, on
-        // `in` itself; the z slot: its last reader was that chunk's D2H
-        KF_HIP(hipMemcpyAsync(sx, hx + off, len, hipMemcpyHostToDevice, st.in));
-        KF_HIP(hipMemcpyAsync(sy, hy + off, len, hipMemcpyHostToDevice, st.in));
-        if (i >= static_cast<size_t>(kSlots)) {
-            KF_HIP(hipStreamWaitEvent(st.in, st.out_done[slot], 0));
-        }
-        const void *ins[2] = {sx, sy};
-        rc                 = dispatch_none(ins, 2, szz, m, dt, op, st.in);
-        if (rc != KF_OK) return rc;
-        KF_HIP(hipEventRecord(st.k_done[slot], st.in));
-        KF_HIP(hipStreamWaitEvent(st.out, st.k_done[slot], 0));
-        KF_HIP(hipMemcpyAsync(hz + off, szz, len, hipMemcpyDeviceToHost, st.out));
-        KF_HIP(hipEventRecord(st.out_done[slot], st.out));
-    }
-    KF_HIP(hipStreamSynchronize(st.in));
-    KF_HIP(hipStreamSynchronize(st.out));
+    KF_HIP(hipMemcpyAsync(dx, x, bytes, hipMemcpyHostToDevice, st.s));
+    KF_HIP(hipMemcpyAsync(dy, y, bytes, hipMemcpyHostToDevice, st.s));
+    const void *ins[2] = {dx, dy};
+    rc                 = dispatch_none(ins, 2, dz, n, dt, op, st.s);
+    if (rc != KF_OK) return rc;
+    KF_HIP(hipMemcpyAsync(out, dz, bytes, hipMemcpyDeviceToHost, st.s));
+    KF_HIP(hipStreamSynchronize(st.s));
     return KF_OK;
 }
 

@@ -11,12 +11,15 @@
 //   RecvBuf, handler/collective.go:43-61)
 //
 // Ingest: a peer chunk is read from the socket straight into a page-locked
-// slot, copied to HBM by the SDMA engine and folded onto the device-resident
-// accumulator by the same HIP kernel as kf_bucket_reduce — replacing
-// "Recv into a pooled Go []byte, then std_transform_2 on the host"
-// (session.go:255-264). Slots are reused round-robin; a slot is refilled only
-// after its previous H2D completed (per-slot event), so the socket read of
-// chunk i+1 overlaps the copy + fold of chunk i.
+// slot and folded onto the device-resident accumulator by the same HIP kernel
+// as kf_bucket_reduce, which reads the slot in place over PCIe (zero copy: the
+// slot is mapped into the GPU's address space) — replacing "Recv into a pooled
+// Go []byte, then std_transform_2 on the host" (session.go:255-264). For the
+// session's 1 MiB chunks that is 33 us against 39 us for an H2D copy + fold
+// (tools/explore/zc_explore.hip). recvInto (bcast) still copies the slot to
+// HBM with the SDMA engine. Slots are reused round-robin; a slot is refilled
+// only after the copy or fold that read it completed (per-slot event), so the
+// socket read of chunk i+1 overlaps the fold of chunk i.
 #include <errno.h>
 #include <hip/hip_runtime.h>
 #include <sys/socket.h>
@@ -118,7 +121,7 @@ struct kf_ingest {
     int nslots        = 0;
     int next          = 0;
     std::vector<void *> host;   // page-locked slots
-    std::vector<void *> dev;    // device slots
+    std::vector<void *> hmap;   // the same slots as the GPU addresses them
     std::vector<hipEvent_t> done;
     std::vector<bool> armed;
     std::mutex mu;  // slot bookkeeping; callers may share one ingest object
@@ -127,8 +130,6 @@ struct kf_ingest {
     {
         for (auto e : done)
             if (e) (void)hipEventDestroy(e);
-        for (auto p : dev)
-            if (p) (void)hipFree(p);
         for (auto p : host)
             if (p) (void)hipHostFree(p);
     }
@@ -242,12 +243,12 @@ kf_ingest_t *kf_ingest_create(size_t slot_bytes, int nslots)
     g->slot_bytes = slot_bytes;
     g->nslots     = nslots;
     g->host.assign(nslots, nullptr);
-    g->dev.assign(nslots, nullptr);
+    g->hmap.assign(nslots, nullptr);
     g->done.assign(nslots, nullptr);
     g->armed.assign(nslots, false);
     for (int i = 0; i < nslots; ++i) {
         if (hipHostMalloc(&g->host[i], slot_bytes, hipHostMallocDefault) != hipSuccess ||
-            hipMalloc(&g->dev[i], slot_bytes) != hipSuccess ||
+            hipHostGetDevicePointer(&g->hmap[i], g->host[i], 0) != hipSuccess ||
             hipEventCreateWithFlags(&g->done[i], hipEventDisableTiming) != hipSuccess) {
             t_ingest_error = "kf_ingest_create: HIP allocation failed";
             delete g;
@@ -273,13 +274,12 @@ int kf_ingest_recv_onto(kf_ingest_t *g, int fd, uint32_t len, void *dev_acc,
     rc = kf_rch_recv_body(fd, g->host[slot], len);
     if (rc != KF_OK) return rc;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    ING_HIP(hipMemcpyAsync(g->dev[slot], g->host[slot], len, hipMemcpyHostToDevice, s));
     // Transform2(RecvBuf, effective, peer): own is SendBuf before the first
-    // receive, RecvBuf afterwards (session.go:241-264)
-    const void *ins[2] = {dev_own ? dev_own : dev_acc, g->dev[slot]};
+    // receive, RecvBuf afterwards (session.go:241-264); peer read in place
+    const void *ins[2] = {dev_own ? dev_own : dev_acc, g->hmap[slot]};
     rc                 = kf_bucket_reduce(ins, 2, dev_acc, count, dt, op, stream);
     if (rc != KF_OK) return rc;
-    // the slot is free again once both the copy and the fold have run
+    // the slot is free again once the fold has run
     ING_HIP(hipEventRecord(g->done[slot], s));
     {
         std::lock_guard<std::mutex> lock(g->mu);
@@ -334,8 +334,7 @@ int kf_ingest_fold_host(kf_ingest_t *g, const void *host, uint32_t len, void *de
     if (rc != KF_OK) return rc;
     std::memcpy(g->host[slot], host, len);
     hipStream_t s = static_cast<hipStream_t>(stream);
-    ING_HIP(hipMemcpyAsync(g->dev[slot], g->host[slot], len, hipMemcpyHostToDevice, s));
-    const void *ins[2] = {dev_own ? dev_own : dev_acc, g->dev[slot]};
+    const void *ins[2] = {dev_own ? dev_own : dev_acc, g->hmap[slot]};
     rc                 = kf_bucket_reduce(ins, 2, dev_acc, count, dt, op, stream);
     if (rc != KF_OK) return rc;
     ING_HIP(hipEventRecord(g->done[slot], s));

@@ -355,8 +355,8 @@ int read_exact(int fd, void *buf, size_t n)
     return KF_OK;
 }
 
-struct SendItem {
-    int fd;
+struct SendItem {  // one chunk to every fd in `fds` (the node's successors)
+    std::vector<int> fds;
     std::string name;
     uint32_t flags;
     const char *ptr;
@@ -377,7 +377,8 @@ struct kf_session {
     std::vector<PeerAddr> peers;           // rank -> address (KUNGFU_INIT_PEERS)
     int listen_unix = -1, listen_tcp = -1;
     std::unordered_map<int, int> out_fd, in_fd;  // peer -> fd
-    kf_ingest_t *ingest = nullptr, *egress = nullptr;
+    kf_ingest_t *ingest = nullptr;
+    void *tx            = nullptr;  // device mode: page-locked outgoing chunk (sender thread)
     kf_host_reduce_fn host_fn = nullptr;
     std::vector<char> scratch;  // host-mode landing buffer (one chunk)
     int batch_fold = 1;         // device mode: k-input fold at multi-predecessor nodes
@@ -413,7 +414,7 @@ struct kf_session {
         }
         if (listen_tcp >= 0) ::close(listen_tcp);
         if (ingest) kf_ingest_destroy(ingest);
-        if (egress) kf_ingest_destroy(egress);
+        if (tx) (void)hipHostFree(tx);
         if (stage) (void)hipFree(stage);
     }
 
@@ -429,22 +430,47 @@ struct kf_session {
                 queue.pop_front();
             }
             int rc = KF_OK;
-            if (send_rc == KF_OK) {
-                rc = device_mode
-                         ? kf_ingest_send_from_device(egress, it.fd, it.name.c_str(), it.flags,
-                                                      it.ptr, it.bytes, it.stream)
-                         : kf_rch_send(it.fd, it.name.c_str(), it.flags, it.ptr,
-                                       static_cast<uint32_t>(it.bytes));
-            }
+            std::string err;
+            if (send_rc == KF_OK) rc = send_item(it, &err);
             {
                 std::lock_guard<std::mutex> l(mu);
                 if (rc != KF_OK && send_rc == KF_OK) {
                     send_rc  = rc;
-                    send_err = kf_ingest_last_error();
+                    send_err = err;
                 }
                 if (--inflight == 0) cv_idle.notify_all();
             }
         }
+    }
+
+    // Device mode: ONE copy of the chunk to page-locked memory, then the same
+    // bytes to every successor (a star root sends its reduced chunk to np-1
+    // peers). The stream sync also orders the copy after the chunk's fold.
+    int send_item(const SendItem &it, std::string *err)
+    {
+        const char *src = it.ptr;
+        if (device_mode) {
+            hipStream_t st = static_cast<hipStream_t>(it.stream);
+            if (it.bytes > kChunk + 4096) {
+                *err = "chunk larger than the tx buffer";
+                return KF_ERR_ARG;
+            }
+            if (hipMemcpyAsync(tx, it.ptr, it.bytes, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipStreamSynchronize(st) != hipSuccess) {
+                *err = "D2H of an outgoing chunk failed";
+                return KF_ERR_HIP;
+            }
+            src = static_cast<const char *>(tx);
+        }
+        for (int fd : it.fds) {
+            const int rc = kf_rch_send(fd, it.name.c_str(), it.flags, src,
+                                       static_cast<uint32_t>(it.bytes));
+            if (rc != KF_OK) {
+                *err = kf_ingest_last_error();
+                return rc;
+            }
+        }
+        return KF_OK;
     }
 
     void enqueue(SendItem it)
@@ -713,15 +739,19 @@ int kf_session::all_reduce(const char *send, char *recv, size_t count, KungFu_Da
                 std::memcpy(const_cast<char *>(cptr(recv, i)), cptr(send, i), clen(i));
             }
         }
-        for (int p : c.st->bcast.next[rank]) {
-            enqueue({out_fd[p], c.name, KF_RCH_WAIT_RECV_BUF, effective(i), clen(i), stream});
+        std::vector<int> fds;
+        for (int p : c.st->bcast.next[rank]) fds.push_back(out_fd[p]);
+        if (!fds.empty()) {
+            enqueue({fds, c.name, KF_RCH_WAIT_RECV_BUF, effective(i), clen(i), stream});
         }
         c.bcast_done = true;
     };
     auto finish_reduce = [&](size_t i) {  // all predecessors folded
         auto &c = chunks[i];
-        for (int p : c.st->reduce.next[rank]) {
-            enqueue({out_fd[p], c.name, KF_RCH_NO_FLAG, effective(i), clen(i), stream});
+        std::vector<int> fds;
+        for (int p : c.st->reduce.next[rank]) fds.push_back(out_fd[p]);
+        if (!fds.empty()) {
+            enqueue({fds, c.name, KF_RCH_NO_FLAG, effective(i), clen(i), stream});
         }
         if (c.st->bcast.prev[rank].empty()) finish_bcast(i);
     };
@@ -933,8 +963,8 @@ kf_session_t *create_session(int rank, std::vector<PeerAddr> peers, const char *
     s->sl = strategy_list(s->strategy, s->hosts());
     if (s->device_mode) {
         s->ingest = kf_ingest_create(kChunk + 4096, 8);
-        s->egress = kf_ingest_create(kChunk + 4096, 2);
-        if (!s->ingest || !s->egress) {
+        if (hipHostMalloc(&s->tx, kChunk + 4096, hipHostMallocDefault) != hipSuccess) s->tx = nullptr;
+        if (!s->ingest || !s->tx) {
             t_sess_error = "kf_ingest_create failed";
             delete s;
             return nullptr;

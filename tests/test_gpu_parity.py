@@ -343,8 +343,8 @@ def test_optimizers_world1_on_gpu(orc, dev):
 
 
 def test_host_paths_pageable_and_pinned(lib, orc):
-    # kf_transform2_host: pageable (runtime staging) and pinned (16 MiB
-    # chunks over two streams, ragged last chunk) give the oracle's bits
+    # kf_transform2_host: pageable (runtime staging) and page-locked (zero
+    # copy: the kernel reads/writes host memory in place) give the oracle's bits
     rng = np.random.default_rng(21)
     n = (40 << 20) // 4 + 12345  # 40 MiB + ragged
     x = rng.standard_normal(n).astype(np.float32)
@@ -370,3 +370,62 @@ def test_host_paths_pageable_and_pinned(lib, orc):
     finally:
         for a in (x, y, z2):
             lib.kf_host_unregister(a.ctypes.data)
+
+
+@pytest.mark.parametrize("dt", ["f32", "f16", "i32", "f64", "u8", "bf16"])
+def test_host_zero_copy_shapes(lib, orc, dt):
+    # zero-copy path (all three page-locked): every dtype, the reference's
+    # 1 MiB chunk, tiny and ragged n, co-misaligned pointers (scalar head),
+    # pointers with different 16-B residues (element kernel), out aliasing x,
+    # and a mixed page-locked/pageable call (falls back to staging)
+    from oracle.oracle import DT, NP
+    code, npdt = DT[dt], NP[dt]
+    rng = np.random.default_rng(zlib.crc32(dt.encode()))
+    isz = np.dtype(npdt).itemsize
+    for n in (1, 7, (1 << 20) // isz, (1 << 20) // isz + 3, 3 << 16):
+        pool = [torch.empty(n * isz + 64, dtype=torch.uint8).pin_memory() for _ in range(3)]
+        for offs in ((0, 0, 0), (isz, isz, isz), (0, isz, 2 * isz)):
+            xs, ys, zs = (_host_view(b, o, n, npdt) for b, o in zip(pool, offs))
+            xs[:] = _rand(orc, rng, dt, n)
+            ys[:] = _rand(orc, rng, dt, n)
+            want = orc.transform2(xs.copy(), ys.copy(), dt, "sum")
+            assert lib.kf_transform2_host(xs.ctypes.data, ys.ctypes.data, zs.ctypes.data, n,
+                                          code, 0) == 0, lib.kf_last_error()
+            assert golden_io.same_bits_or_nan(zs, want), (dt, n, offs)
+        xs, ys, zs = (_host_view(b, 0, n, npdt) for b in pool)
+        x0 = xs.copy()
+        want = orc.transform2(x0, ys.copy(), dt, "sum")
+        lib.std_transform_2(xs.ctypes.data, ys.ctypes.data, xs.ctypes.data, n, code, 0)
+        assert golden_io.same_bits_or_nan(xs, want), (dt, n, "out is x")
+        xs[:] = x0
+        yp = ys.copy()  # pageable
+        lib.std_transform_2(xs.ctypes.data, yp.ctypes.data, zs.ctypes.data, n, code, 0)
+        assert golden_io.same_bits_or_nan(zs, want), (dt, n, "mixed")
+
+
+def test_host_api_on_device_pointers(lib, orc):
+    # std_transform_2 handed HBM pointers runs the kernel on them directly
+    rng = np.random.default_rng(9)
+    n = 100003
+    x = rng.standard_normal(n).astype(np.float32)
+    y = rng.standard_normal(n).astype(np.float32)
+    dx, dy = torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()
+    dz = torch.empty_like(dx)
+    lib.std_transform_2(dx.data_ptr(), dy.data_ptr(), dz.data_ptr(), n, 0x20408, 0)
+    torch.cuda.synchronize()
+    assert np.array_equal(dz.cpu().numpy(), orc.transform2(x, y, "f32", "sum"))
+
+
+def _host_view(buf, off, n, npdt):
+    isz = np.dtype(npdt).itemsize
+    return buf.numpy()[off:off + n * isz].view(npdt)
+
+
+def _rand(orc, rng, dt, n):
+    from oracle.oracle import NP
+    if dt == "bf16":
+        return orc.f32_to_bf16_bits(rng.standard_normal(n).astype(np.float32))
+    if np.issubdtype(NP[dt], np.integer):
+        info = np.iinfo(NP[dt])
+        return rng.integers(info.min, info.max, size=n, dtype=NP[dt], endpoint=True)
+    return (rng.standard_normal(n) * 10).astype(NP[dt])
