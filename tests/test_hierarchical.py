@@ -1,0 +1,159 @@
+"""Hierarchical all-reduce (kungfu_amd/hierarchical.py; the reference's
+ScheduledHierarchicalNcclAllReduce, tensorflow/ops/gpu/collective.cpp:108-162)
+with hosts emulated by loopback addresses: gloo stands in for RCCL inside a
+host, the native session (host mode, the oracle's restatement of the reference
+reduce as the fold) runs across hosts, the oracle does the /np epilogue.
+Expected values: integer sums exactly (the reference's known answers sum to
+np·x / iota·np, fake_agent.cpp:15-44); float averages within the order bound
+(np-1)·2^-24·Σ|x| + one rounding for the division."""
+import ctypes
+import os
+import random
+import socket
+import sys
+import tempfile
+import traceback
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _peers(hosts_sizes, base):
+    out = []
+    for h, n in enumerate(hosts_sizes):
+        out += ["127.0.0.%d:%d" % (h + 1, base + len(out) + i) for i in range(n)]
+    return out
+
+
+def _x(rank, n):
+    return np.random.default_rng(300 + rank).standard_normal(n).astype(np.float32)
+
+
+def _body(rank, peers, port, sock_dir, errq, use_gpu):
+    import faulthandler
+    faulthandler.dump_traceback_later(100, exit=True)  # a hung rank dies loudly
+    sys.path[:0] = [ROOT, HERE]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=len(peers))
+        from cpu_epilogue import CpuEpilogue
+        from kungfu_amd.hierarchical import HierarchicalExchange
+        from oracle import oracle
+        world = len(peers)
+        if use_gpu:
+            dev = torch.device("cuda:0")
+            ex = HierarchicalExchange(peers, rank, sock_dir=sock_dir, mode="device")
+        else:
+            dev = torch.device("cpu")
+            fn = ctypes.cast(oracle.lib().oracle_transform2, ctypes.c_void_p)
+            ex = HierarchicalExchange(peers, rank, sock_dir=sock_dir, mode="host",
+                                      epilogue=CpuEpilogue(), host_reduce_fn=fn)
+        # fp32 S-SGD average over a 3-chunk bucket and a small one
+        for step, n in enumerate(((3 << 20) // 4 + 11, 1000)):
+            m = ex.padded_count(n, 4)
+            b = torch.zeros(m, dtype=torch.float32, device=dev)
+            b[:n] = torch.from_numpy(_x(rank + 10 * step, n)).to(dev)
+            ex.all_reduce_([b], average=True, name="grad%d" % step)
+            xs = [_x(r + 10 * step, n) for r in range(world)]
+            exact = np.sum([x.astype(np.float64) for x in xs], axis=0) / world
+            absum = np.sum([np.abs(x).astype(np.float64) for x in xs], axis=0)
+            got = b[:n].cpu().numpy().astype(np.float64)
+            bound = (world - 1) * 2.0 ** -24 * absum / world + 2.0 ** -24 * np.abs(exact) + 1e-37
+            assert np.all(np.abs(got - exact) <= bound * 1.0001), step
+            assert np.all(b[n:].cpu().numpy() == 0)
+        # int32 SUM and MAX: exact
+        n = 4099
+        m = ex.padded_count(n, 4)
+        bi = torch.zeros(m, dtype=torch.int32, device=dev)
+        bi[:n] = torch.arange(n, dtype=torch.int32, device=dev) + rank
+        ex.all_reduce_([bi], op="sum", name="iota")
+        want = (np.arange(n) * world + world * (world - 1) // 2).astype(np.int32)
+        assert np.array_equal(bi[:n].cpu().numpy(), want)
+        bi[:n] = torch.full((n,), rank * 7, dtype=torch.int32, device=dev)
+        ex.all_reduce_([bi], op="max", name="max")
+        assert torch.all(bi[:n].cpu() == (world - 1) * 7)
+        # the optimizer surface on top: S-SGD averages, SMA blends
+        from kungfu_amd.optimizers import (SynchronousAveragingOptimizer,
+                                           SynchronousSGDOptimizer)
+        w = torch.nn.Parameter(torch.zeros(3000, device=dev))
+        opt = SynchronousSGDOptimizer(torch.optim.SGD([w], lr=1.0), exchange=ex)
+        w.grad = torch.full((3000,), float(rank + 1), device=dev)
+        opt.step()  # w = 0 - mean(rank + 1)
+        assert torch.all(w.detach().cpu() == -(world + 1) / 2)
+        v = torch.nn.Parameter(torch.full((777,), float(2 * rank), device=dev))
+        sma = SynchronousAveragingOptimizer(torch.optim.SGD([v], lr=0.0), alpha=0.5, exchange=ex)
+        v.grad = torch.zeros(777, device=dev)
+        sma.step()  # 0.5 * 2r + 0.5 * mean(2r) = r + (world - 1) / 2
+        assert torch.allclose(v.detach().cpu(), torch.full((777,), rank + (world - 1) / 2))
+        ex.close()
+        dist.barrier()
+    except Exception:
+        errq.put("rank %d: %s" % (rank, traceback.format_exc()))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def _run(hosts_sizes, use_gpu=False):
+    peers = _peers(hosts_sizes, random.Random().randrange(20000, 60000, 16))
+    ctx = mp.get_context("spawn")
+    errq = ctx.SimpleQueue()
+    port = _free_port()
+    with tempfile.TemporaryDirectory() as d:
+        ps = [ctx.Process(target=_body, args=(r, peers, port, d, errq, use_gpu))
+              for r in range(len(peers))]
+        for p in ps:
+            p.start()
+        for p in ps:
+            p.join(timeout=300)
+    errs = []
+    while not errq.empty():
+        errs.append(errq.get())
+    assert not errs, "\n".join(errs)
+    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+
+
+def test_host_layout_matches_partition_by_host():
+    from kungfu_amd.hierarchical import host_layout
+    peers = ["10.0.0.1:1", "10.0.0.2:1", "10.0.0.1:2", "10.0.0.3:1", "10.0.0.2:2"]
+    # PartitionByHost: masters are the first rank seen on each host
+    assert host_layout(peers) == [[0, 2], [1, 4], [3]]
+
+
+def test_two_equal_hosts_2d():
+    # 2 hosts x 2 ranks: local reduce-scatter, per-local-rank cross sessions
+    _run([2, 2])
+
+
+def test_uneven_hosts_via_master():
+    # hosts of 2 and 1 ranks: the reference's reduce -> masters -> broadcast
+    _run([2, 1])
+
+
+def test_one_rank_per_host():
+    # every host one rank: the whole exchange is the cross-host session
+    _run([1, 1, 1])
+
+
+@pytest.mark.gpu
+def test_cross_host_device_sessions():
+    # device-mode cross sessions (HIP folds in HBM) + HIP /np epilogue; one rank
+    # per emulated host so no intra-host collective is needed on a shared GPU
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _run([1, 1], use_gpu=True)
+    _run([1, 1, 1], use_gpu=True)
