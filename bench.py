@@ -24,9 +24,13 @@ the launch stream), peak = 8.0 TB/s HBM3E (MI355X_MICROARCH.md). `traffic` is
 the PMC-measured HBM bytes per launch from profiles/ (rocprofv3 FETCH_SIZE x2
 + WRITE_SIZE, gfx950 correction), null if not recorded.
 
-cpu_baseline: the oracle's restatement of KungFu's std_transform_2 (compiled
-with the reference's -O2 -mavx -mf16c), 1 thread, on the same 256 MiB sum
-repeated for about --cpu-seconds; rank 0 at N = 1 only.
+cpu_baseline: KungFu's own std_transform_2 compiled from the reference's
+sources by `make -C oracle ref` (kind "reference"; built by __graft_entry__
+.build() where /root/reference exists, shipped as oracle/_ref/*.so), or the
+oracle's bit-exact restatement with the same -O2 -mavx -mf16c flags (kind
+"port") when that build is absent; 1 thread on the same 256 MiB sum repeated
+for about --cpu-seconds, plus 1 MiB chunks on up to 16 threads; rank 0 at
+N = 1 only.
 """
 import argparse
 import ctypes
@@ -135,15 +139,32 @@ def time_local_reduce(lib, sets, steps, warmup, world):
 
 
 def cpu_baseline(x, y, seconds):
+    """KungFu's own CPU reduce timed on this host: the reference's
+    std_transform_2 compiled from its sources (oracle/_ref, kind "reference")
+    when that build is present, else the oracle's bit-exact restatement built
+    with the same flags (kind "port"). 1 thread over the whole bucket, plus the
+    reference's goroutine-per-1 MiB-chunk fan-out (session.go:317-323) over
+    the box's CPU share."""
     from oracle import oracle
     oracle.build()
     xh = x.cpu().numpy()
     yh = y.cpu().numpy()
     zh = np.empty_like(xh)
-    oracle.bench_transform2(xh, yh, zh, "f32", "sum", 1, threads=1)  # page in
-    t1 = oracle.bench_transform2(xh, yh, zh, "f32", "sum", 2, threads=1) / 2
+    ref = oracle.ref_transform2_addr()
+    if ref is not None:
+        kind, what = "reference", ("KungFu's std_transform_2 built from its sources "
+                                   "(op.cpp/f16.c/dtype.c, -O2 -mavx -mf16c)")
+        run = lambda reps, threads: oracle.bench_ref(ref, xh, yh, zh, "f32", "sum",  # noqa: E731
+                                                     reps, threads=threads)
+    else:
+        kind, what = "port", "oracle restatement built -O2 -mavx -mf16c"
+        run = lambda reps, threads: oracle.bench_transform2(xh, yh, zh, "f32", "sum",  # noqa: E731
+                                                            reps, threads=threads)
+    run(1, 1)  # page in
+    ok = bool(np.array_equal(zh, xh + yh))
+    t1 = run(2, 1) / 2
     reps = max(1, min(1000, int(seconds / max(t1, 1e-6))))
-    t = oracle.bench_transform2(xh, yh, zh, "f32", "sum", reps, threads=1)
+    t = run(reps, 1)
     s_bytes = xh.nbytes
     cpu_model = "unknown"
     try:
@@ -154,23 +175,21 @@ def cpu_baseline(x, y, seconds):
                     break
     except OSError:
         pass
-    # the reference's goroutine-per-chunk fan-out (session.go:317-323) over
-    # the box's CPU share: 1 MiB chunks from a work queue on T threads
     nt = min(16, os.cpu_count() or 1)
-    tm1 = oracle.bench_transform2(xh, yh, zh, "f32", "sum", 2, threads=nt) / 2
+    tm1 = run(2, nt) / 2
     mreps = max(1, min(1000, int(seconds / 2 / max(tm1, 1e-6))))
-    tm = oracle.bench_transform2(xh, yh, zh, "f32", "sum", mreps, threads=nt)
+    tm = run(mreps, nt)
     return {
         "value": round(reps * s_bytes / t / 2**30, 3),
         "unit": "GiB/s",
         "cores": 1,
+        "kind": kind,
+        "correct": ok,
         "multi_thread": {"value": round(mreps * s_bytes / tm / 2**30, 3), "unit": "GiB/s",
-                         "cores": nt, "sample": "%d x 256 MiB in 1 MiB chunks, %.1f s"
-                                                % (mreps, tm)},
-        "kind": "port",
-        "sample": "%d x std_transform_2(f32, SUM) over the same 256 MiB bucket, "
-                  "1 thread, oracle restatement built -O2 -mavx -mf16c, %.1f s, %s"
-                  % (reps, t, cpu_model),
+                         "cores": nt, "sample": "%d x 256 MiB in 1 MiB chunks on %d threads, "
+                                                "%.1f s" % (mreps, nt, tm)},
+        "sample": "%d x std_transform_2(f32, SUM) over the same 256 MiB bucket, 1 thread, "
+                  "%s, %.1f s, %s" % (reps, what, t, cpu_model),
     }
 
 
@@ -225,9 +244,15 @@ def chunk_latency(lib, x, reps=2000):
     ok = bool(torch.equal(zh, xh + yh))
     xa, ya = xh.numpy().copy(), yh.numpy().copy()
     za = np.empty_like(xa)
-    oracle.bench_transform2(xa, ya, za, "f32", "sum", 20, threads=1)
-    cpu_s = oracle.bench_transform2(xa, ya, za, "f32", "sum", reps, threads=1) / reps
-    return {"gpu_pinned_us": round(gpu_s * 1e6, 2), "cpu_port_us": round(cpu_s * 1e6, 2),
+    ref = oracle.ref_transform2_addr()
+    if ref is not None:
+        run = lambda r: oracle.bench_ref(ref, xa, ya, za, "f32", "sum", r)  # noqa: E731
+    else:
+        run = lambda r: oracle.bench_transform2(xa, ya, za, "f32", "sum", r)  # noqa: E731
+    run(20)
+    cpu_s = run(reps) / reps
+    return {"gpu_pinned_us": round(gpu_s * 1e6, 2), "cpu_us": round(cpu_s * 1e6, 2),
+            "cpu_kind": "reference" if ref is not None else "port",
             "correct": ok, "reps": reps}
 
 

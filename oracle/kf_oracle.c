@@ -327,6 +327,10 @@ int oracle_sma_blend(void *v, const void *sum, int64_t n, int dt, int np,
 
 /* ---- CPU baseline harness (bench.py cpu_baseline leg) -------------------- */
 
+/* std_transform_2's signature (srcs/cpp/include/kungfu/op.h:17-19): lets the
+ * harness time the reference's own compiled function (oracle/_ref) too */
+typedef void (*transform2_fn)(const void *, const void *, void *, int, int, int);
+
 struct chunk_job {
     const char *x, *y;
     char *z;
@@ -335,7 +339,17 @@ struct chunk_job {
     int64_t chunk_elems;
     int64_t next; /* shared counter, guarded by mu */
     pthread_mutex_t mu;
+    transform2_fn fn; /* 0: the restatement */
 };
+
+static void run_span(const struct chunk_job *j, int64_t b, int64_t e, uint32_t sz)
+{
+    if (j->fn) {
+        j->fn(j->x + b * sz, j->y + b * sz, j->z + b * sz, (int)(e - b), j->dt, j->op);
+    } else {
+        oracle_transform2(j->x + b * sz, j->y + b * sz, j->z + b * sz, e - b, j->dt, j->op);
+    }
+}
 
 static void *chunk_worker(void *arg)
 {
@@ -348,8 +362,7 @@ static void *chunk_worker(void *arg)
         pthread_mutex_unlock(&j->mu);
         if (b >= j->n) break;
         int64_t e = b + j->chunk_elems < j->n ? b + j->chunk_elems : j->n;
-        oracle_transform2(j->x + b * sz, j->y + b * sz, j->z + b * sz, e - b,
-                          j->dt, j->op);
+        run_span(j, b, e, sz);
     }
     return 0;
 }
@@ -361,24 +374,21 @@ static double now_s(void)
     return ts.tv_sec + ts.tv_nsec * 1e-9;
 }
 
-/* Time `reps` reductions of n elements, split into chunk_bytes chunks handed
- * to `threads` workers (the goroutine-per-1MiB-chunk model of
- * session.go:313-326). Returns total seconds. */
-double oracle_bench_transform2(const void *x, const void *y, void *z,
-                               int64_t n, int dt, int op, int reps,
-                               int threads, int64_t chunk_bytes)
+static double bench(transform2_fn fn, const void *x, const void *y, void *z, int64_t n,
+                    int dt, int op, int reps, int threads, int64_t chunk_bytes)
 {
     uint32_t sz = oracle_type_size(dt);
     if (sz == 0 || threads < 1) return -1.0;
+    if (fn && n > 2147483647) return -1.0; /* the reference's n is an int */
     double t0 = now_s();
     for (int r = 0; r < reps; ++r) {
-        if (threads == 1) {
-            oracle_transform2(x, y, z, n, dt, op);
-            continue;
-        }
         struct chunk_job j;
         j.x = (const char *)x; j.y = (const char *)y; j.z = (char *)z;
-        j.n = n; j.dt = dt; j.op = op;
+        j.n = n; j.dt = dt; j.op = op; j.fn = fn;
+        if (threads == 1) {
+            run_span(&j, 0, n, sz);
+            continue;
+        }
         j.chunk_elems = chunk_bytes / sz > 0 ? chunk_bytes / sz : 1;
         j.next = 0;
         pthread_mutex_init(&j.mu, 0);
@@ -389,4 +399,23 @@ double oracle_bench_transform2(const void *x, const void *y, void *z,
         pthread_mutex_destroy(&j.mu);
     }
     return now_s() - t0;
+}
+
+/* Time `reps` reductions of n elements, split into chunk_bytes chunks handed
+ * to `threads` workers (the goroutine-per-1MiB-chunk model of
+ * session.go:313-326). Returns total seconds. */
+double oracle_bench_transform2(const void *x, const void *y, void *z,
+                               int64_t n, int dt, int op, int reps,
+                               int threads, int64_t chunk_bytes)
+{
+    return bench(0, x, y, z, n, dt, op, reps, threads, chunk_bytes);
+}
+
+/* The same harness around a std_transform_2-compatible function pointer
+ * (bench.py: the reference's own build, oracle/_ref/libkfbase_ref.so). */
+double oracle_bench_fn(void *fn, const void *x, const void *y, void *z, int64_t n,
+                       int dt, int op, int reps, int threads, int64_t chunk_bytes)
+{
+    if (!fn) return -1.0;
+    return bench((transform2_fn)fn, x, y, z, n, dt, op, reps, threads, chunk_bytes);
 }

@@ -59,6 +59,8 @@ def lib():
         l.oracle_sma_blend.restype = i
         l.oracle_bench_transform2.argtypes = [vp, vp, vp, i64, i, i, i, i, i64]
         l.oracle_bench_transform2.restype = ctypes.c_double
+        l.oracle_bench_fn.argtypes = [vp, vp, vp, vp, i64, i, i, i, i, i64]
+        l.oracle_bench_fn.restype = ctypes.c_double
         _lib = l
     return _lib
 
@@ -117,6 +119,25 @@ def sma_blend(v, summed, dt, np_, alpha):
     if rc != 0:
         raise ValueError("unsupported dtype %s" % dt)
     return out
+
+
+REF_LIB = os.path.join(HERE, "_ref", "libkfbase_ref.so")
+
+
+def ref_transform2_addr():
+    """Address of std_transform_2 in the reference's own build
+    (oracle/_ref, compiled from /root/reference by `make ref`), or None."""
+    if not os.path.exists(REF_LIB):
+        return None
+    ref = ctypes.CDLL(REF_LIB)
+    return ctypes.cast(ref.std_transform_2, ctypes.c_void_p).value
+
+
+def bench_ref(fn_addr, x, y, z, dt, op, reps, threads=1, chunk_bytes=1 << 20):
+    """bench_transform2 around the reference's compiled std_transform_2."""
+    return float(lib().oracle_bench_fn(
+        fn_addr, x.ctypes.data, y.ctypes.data, z.ctypes.data, x.size, _code(dt),
+        OPS.get(op, op), int(reps), int(threads), int(chunk_bytes)))
 
 
 def bench_transform2(x, y, z, dt, op, reps, threads=1, chunk_bytes=1 << 20):
