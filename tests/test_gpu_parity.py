@@ -2,6 +2,7 @@
 reference's golden vectors. Integers bit-exact; floats bit-exact where the
 reference is deterministic (any 2-operand op, ring order, fixed fold order),
 NaN-ness equal where payloads may differ (golden_io.same_bits_or_nan)."""
+import os
 import zlib
 
 import numpy as np
@@ -429,3 +430,43 @@ def _rand(orc, rng, dt, n):
         info = np.iinfo(NP[dt])
         return rng.integers(info.min, info.max, size=n, dtype=NP[dt], endpoint=True)
     return (rng.standard_normal(n) * 10).astype(NP[dt])
+
+
+# ---- straight against the reference's own compiled reduce ----------------
+
+@pytest.mark.parametrize("dt", INT_DTS + ["f16", "f32", "f64"])
+def test_dropin_vs_reference_build(lib, dt):
+    # oracle/_ref/libkfbase_ref.so is KungFu's op.cpp/f16.c/dtype.c compiled
+    # from /root/reference (make -C oracle ref; shipped with the tree). Same
+    # random inputs (with specials mixed in for floats) through both
+    # std_transform_2s, every op the reference accepts for the dtype.
+    import ctypes
+    from oracle import oracle
+    from oracle.oracle import DT, NP
+    if not os.path.exists(oracle.REF_LIB):
+        pytest.skip("reference build absent (make -C oracle ref)")
+    ref = ctypes.CDLL(oracle.REF_LIB)
+    ref.std_transform_2.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int] * 3
+    rng = np.random.default_rng(zlib.crc32(("ref" + dt).encode()))
+    n = (1 << 20) + 5
+    npdt = NP[dt]
+    if dt in INT_DTS:
+        info = np.iinfo(npdt)
+        x = rng.integers(info.min, info.max, size=n, dtype=npdt, endpoint=True)
+        y = rng.integers(info.min, info.max, size=n, dtype=npdt, endpoint=True)
+    else:
+        x = (rng.standard_normal(n) * 1e3).astype(npdt)
+        y = (rng.standard_normal(n) * 1e3).astype(npdt)
+        sp = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, np.finfo(npdt).max,
+                       np.finfo(npdt).tiny / 2, 1.0], dtype=npdt)
+        idx = rng.integers(0, n, size=4096)
+        x[idx] = sp[rng.integers(0, sp.size, size=idx.size)]
+        y[idx[::-1]] = sp[rng.integers(0, sp.size, size=idx.size)]
+    ops = ["sum"] if dt == "f16" else ["sum", "min", "max", "prod"]
+    for op in ops:
+        code = {"sum": 0, "min": 1, "max": 2, "prod": 3}[op]
+        want = np.empty_like(x)
+        got = np.empty_like(x)
+        ref.std_transform_2(x.ctypes.data, y.ctypes.data, want.ctypes.data, n, DT[dt], code)
+        lib.std_transform_2(x.ctypes.data, y.ctypes.data, got.ctypes.data, n, DT[dt], code)
+        assert golden_io.same_bits_or_nan(got, want), (dt, op)

@@ -134,3 +134,38 @@ def test_bf16_build_semantics(oracle_mod):
     nanbits = np.array([0x7F81, 0xFFC1], np.uint16)
     f = oracle_mod.bf16_bits_to_f32(nanbits)
     assert np.all(np.isnan(oracle_mod.bf16_bits_to_f32(oracle_mod.f32_to_bf16_bits(f))))
+
+
+@pytest.mark.parametrize("dt", ["u8", "u16", "u32", "u64", "i8", "i16", "i32", "i64",
+                                "f16", "f32", "f64"])
+def test_oracle_vs_reference_build_random(oracle_mod, dt):
+    # beyond the stored vectors: fresh random inputs (specials mixed in)
+    # through the oracle and the reference's own compiled std_transform_2
+    import ctypes
+    import os
+    import zlib
+    if not os.path.exists(oracle_mod.REF_LIB):
+        pytest.skip("reference build absent (make -C oracle ref)")
+    ref = ctypes.CDLL(oracle_mod.REF_LIB)
+    ref.std_transform_2.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int] * 3
+    rng = np.random.default_rng(zlib.crc32(dt.encode()))
+    npdt = oracle_mod.NP[dt]
+    n = 100003
+    if np.issubdtype(npdt, np.integer):
+        info = np.iinfo(npdt)
+        x = rng.integers(info.min, info.max, size=n, dtype=npdt, endpoint=True)
+        y = rng.integers(info.min, info.max, size=n, dtype=npdt, endpoint=True)
+    else:
+        x = (rng.standard_normal(n) * 1e3).astype(npdt)
+        y = (rng.standard_normal(n) * 1e3).astype(npdt)
+        sp = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, np.finfo(npdt).max,
+                       np.finfo(npdt).tiny / 2], dtype=npdt)
+        idx = rng.integers(0, n, size=2000)
+        x[idx] = sp[rng.integers(0, sp.size, size=idx.size)]
+        y[idx[::-1]] = sp[rng.integers(0, sp.size, size=idx.size)]
+    for op in (["sum"] if dt == "f16" else ["sum", "min", "max", "prod"]):
+        want = np.empty_like(x)
+        ref.std_transform_2(x.ctypes.data, y.ctypes.data, want.ctypes.data, n,
+                            oracle_mod.DT[dt], oracle_mod.OPS[op])
+        got = oracle_mod.transform2(x, y, dt, op)
+        assert golden_io.same_bits_or_nan(got, want), (dt, op)
