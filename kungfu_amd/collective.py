@@ -119,6 +119,16 @@ class Exchange:
         reference's S-SGD applies to ready gradients (nccl_fusion,
         sync_sgd.py:87-92). Buckets handed over one call at a time (e.g. as
         backward produces them) are reduced as they come."""
+        self.start_(buckets, op=op, average=average, coalesce=coalesce).wait()
+        return buckets
+
+    def start_(self, buckets, op="sum", average=False, coalesce=True, key="ar"):
+        """Queue the all-reduce of `buckets` and return a handle whose wait()
+        completes it. With RCCL nothing here blocks the host: each shard
+        epilogue is ordered behind its reduce-scatter on the device, and each
+        all-gather behind its epilogue, so this can be called from a backward
+        hook while later gradients are still being computed. Concurrent calls
+        must use different `key`s (their shard workspaces)."""
         red = OP_NAMES[op] if isinstance(op, str) else OP(op)
         if average and red != OP.SUM:
             raise ValueError("average requires op='sum'")
@@ -126,16 +136,15 @@ class Exchange:
             self._check(b)
         if self.world == 1:
             # a single peer: the reduce is the identity; g / 1 == g exactly
-            return buckets
+            return _Handle([])
         if coalesce:
             runs = coalesce_runs(buckets)
             if len(runs) < len(buckets):
-                self.all_reduce_(runs, op=op, average=average, coalesce=False)
-                return buckets
+                return self.start_(runs, op=op, average=average, coalesce=False, key=key)
         shards = []
         works = []
         for i, b in enumerate(buckets):
-            shard = self._workspace(("rs", i), b.numel() // self.world, b)
+            shard = self._workspace((key, "rs", i), b.numel() // self.world, b)
             works.append(dist.reduce_scatter_tensor(shard, b, op=_RED_OPS[red],
                                                     group=self.group, async_op=True))
             shards.append(shard)
@@ -146,9 +155,7 @@ class Exchange:
                 self.epilogue.div_(shard, self.world)
             gathers.append(dist.all_gather_into_tensor(b, shard, group=self.group,
                                                        async_op=True))
-        for g in gathers:
-            g.wait()
-        return buckets
+        return _Handle(gathers)
 
     def sma_(self, buckets, alpha):
         """SMA over flat variable buckets (sma_sgd.py:60-65): each rank's v
@@ -183,6 +190,18 @@ class Exchange:
             w.wait()
             self.epilogue.sma_blend_(b, s, self.world, alpha)
         return buckets
+
+
+class _Handle:
+    """Pending collectives of one start_() call."""
+
+    def __init__(self, works):
+        self.works = works
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+        self.works = []
 
 
 class GradBuckets:

@@ -57,7 +57,74 @@ class _Bucketed:
 
 
 class _SyncSGD(_Bucketed):
+    def _kf_setup_overlap(self):
+        """Buckets in backward order (parameters reversed) with one
+        post-accumulate-grad hook per parameter: when the last gradient of a
+        bucket is in, that bucket's RS -> /np -> AG is queued at once, while
+        backward goes on computing earlier layers. Buckets are launched strictly
+        in index order (a ready bucket waits for the ones before it), so every
+        rank issues the same collectives in the same order."""
+        groups = {}
+        for p in reversed(self._kf_params):
+            groups.setdefault((p.dtype, p.device), []).append(p)
+        self._kf_slots = []  # (bucket, [(param, view)]) in launch order
+        self._kf_slot_of = {}
+        for (dtype, device), ps in groups.items():
+            gb = GradBuckets([p.numel() for p in ps], dtype, device,
+                             self._kf_ex.world, bucket_bytes=self._kf_bucket_bytes)
+            members = [[] for _ in gb.buckets]
+            for p, v in zip(ps, gb.views):
+                j = next(j for j, b in enumerate(gb.buckets)
+                         if b.data_ptr() <= v.data_ptr() < b.data_ptr() + b.numel() * b.element_size())
+                members[j].append((p, v.view_as(p)))
+            for b, m in zip(gb.buckets, members):
+                for p, v in m:
+                    self._kf_slot_of[p] = (len(self._kf_slots), v)
+                self._kf_slots.append((b, m))
+        self._kf_reset_overlap()
+        for p in self._kf_params:
+            p.register_post_accumulate_grad_hook(self._kf_grad_ready)
+
+    def _kf_reset_overlap(self):
+        self._kf_missing = [len(m) for _, m in self._kf_slots]
+        self._kf_next = 0
+        self._kf_handles = []
+
+    def _kf_grad_ready(self, p):
+        i, v = self._kf_slot_of[p]
+        if p.grad.data_ptr() != v.data_ptr():
+            v.copy_(p.grad)
+        self._kf_missing[i] -= 1
+        self._kf_launch_ready()
+
+    def _kf_launch_ready(self):
+        while self._kf_next < len(self._kf_slots) and self._kf_missing[self._kf_next] <= 0:
+            b, _ = self._kf_slots[self._kf_next]
+            self._kf_handles.append(self._kf_ex.start_(
+                [b], op=self._kf_op, average=self._kf_average, coalesce=False,
+                key="ovl%d" % self._kf_next))
+            self._kf_next += 1
+
+    def _kf_finish_overlap(self):
+        # parameters that got no gradient this step contribute zeros
+        # (sync_gradients' rule); then every remaining bucket goes, in order
+        for i, (b, m) in enumerate(self._kf_slots):
+            if i >= self._kf_next and self._kf_missing[i] > 0:
+                for p, v in m:
+                    if p.grad is None:
+                        v.zero_()
+                self._kf_missing[i] = 0
+        self._kf_launch_ready()
+        for h in self._kf_handles:
+            h.wait()
+        for b, m in self._kf_slots:
+            for p, v in m:
+                p.grad = v
+        self._kf_reset_overlap()
+
     def sync_gradients(self):
+        if self._kf_overlap:
+            return self._kf_finish_overlap()
         if self._kf_groups is None:
             self._kf_build(None)
         for ps, gb in self._kf_groups:
@@ -79,15 +146,27 @@ class _SyncSGD(_Bucketed):
 
 
 def SynchronousSGDOptimizer(optimizer, named_parameters=None, op=None,
-                            average=True, exchange=None, bucket_bytes=32 << 20):
+                            average=True, exchange=None, bucket_bytes=32 << 20,
+                            overlap=False):
     """S-SGD: all-reduce gradients (sum, then / np when average) before each
-    step. Returns the wrapped optimizer (reference: sync_sgd.py:81-84)."""
+    step. Returns the wrapped optimizer (reference: sync_sgd.py:81-84).
+
+    overlap=True starts each bucket's exchange from a backward hook as soon as
+    its gradients are complete (one backward per step), so the RCCL traffic
+    of late layers hides behind the backward of early ones; step() waits for
+    the rest. Same values as overlap=False up to the bucket grouping."""
     opt = _wrap(optimizer, _SyncSGD)
     opt._kf_setup(named_parameters, exchange, bucket_bytes)
     opt._kf_op = op if op is not None else "sum"
     opt._kf_average = bool(average)
     if opt._kf_average and opt._kf_op != "sum":
         raise ValueError("average=True needs op='sum'")
+    opt._kf_overlap = bool(overlap)
+    if opt._kf_overlap:
+        if not hasattr(opt._kf_ex, "start_"):
+            raise ValueError("overlap=True needs an exchange with start_() "
+                             "(collective.Exchange)")
+        opt._kf_setup_overlap()
     return opt
 
 

@@ -249,6 +249,7 @@ def test_all_reduce_with_hip_epilogue():
     run_world("body_all_reduce", 2, use_gpu=True)
     run_world("body_sync_sgd", 3, use_gpu=True)
     run_world("body_sma", 2, use_gpu=True)
+    run_world("body_sync_sgd_overlap", 2, use_gpu=True)
 
 
 def test_coalesce_runs():
@@ -312,3 +313,51 @@ def body_torch_ops(rank, world, use_gpu):
 @pytest.mark.parametrize("world", [2, 3])
 def test_torch_ops_surface(world):
     run_world("body_torch_ops", world)
+
+
+def body_sync_sgd_overlap(rank, world, use_gpu):
+    # buckets exchanged from backward hooks (overlap=True) give the same
+    # parameters as the exchange in step(); small buckets so a step has many,
+    # a layer that gets no gradient (zeros contributed), three steps with
+    # zero_grad(set_to_none) in between
+    from kungfu_amd.collective import Exchange
+    from kungfu_amd.optimizers import SynchronousSGDOptimizer
+
+    def model():
+        torch.manual_seed(3)
+        m = torch.nn.Sequential(torch.nn.Linear(17, 40), torch.nn.Tanh(),
+                                torch.nn.Linear(40, 30), torch.nn.Tanh(),
+                                torch.nn.Linear(30, 3))
+        m.register_parameter("unused", torch.nn.Parameter(torch.ones(25)))
+        return m
+
+    a, b = model(), model()
+    oa = SynchronousSGDOptimizer(torch.optim.SGD(a.parameters(), lr=0.1, momentum=0.9),
+                                 exchange=Exchange(epilogue=_epilogue(use_gpu)),
+                                 bucket_bytes=2048, overlap=True)
+    ob = SynchronousSGDOptimizer(torch.optim.SGD(b.parameters(), lr=0.1, momentum=0.9),
+                                 exchange=Exchange(epilogue=_epilogue(use_gpu)),
+                                 bucket_bytes=2048)
+    assert len(oa._kf_slots) > 3
+    for step in range(3):
+        for m, o in ((a, oa), (b, ob)):
+            o.zero_grad()
+            _loss(m, rank + 7 * step).backward()
+            if o is oa:  # every bucket with gradients went out during backward
+                assert oa._kf_next == len(oa._kf_slots) - 1  # all but `unused`'s
+            o.step()
+    for p, q in zip(a.parameters(), b.parameters()):
+        if world == 2:
+            assert torch.equal(p, q)
+        else:
+            assert torch.allclose(p, q, rtol=0, atol=1e-6)
+    flat = torch.cat([p.detach().reshape(-1) for p in a.parameters()])
+    allf = [torch.empty_like(flat) for _ in range(world)]
+    dist.all_gather(allf, flat)
+    for f in allf:
+        assert torch.equal(f, flat)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sync_sgd_overlap(world):
+    run_world("body_sync_sgd_overlap", world)
