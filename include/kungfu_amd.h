@@ -150,6 +150,15 @@ const char *kf_version(void);
 /* Last HIP error string recorded by the library on this thread. */
 const char *kf_last_error(void);
 
+/* kf_bucket_reduce / kf_bucket_reduce_avg for inputs that sit behind
+ * different links (kungfu_amd/p2p.py: shard `rank` of every peer's bucket,
+ * mapped over xGMI): every thread has the loads of up to 8 inputs in flight
+ * before the first add, so all links carry traffic at once; the fold order is
+ * still inputs[0], inputs[1], ... (bit-identical result). np > 0: SUM then
+ * / np (float dtypes); np == 0: the plain op. Same contract as B2. */
+int kf_bucket_reduce_peers(const void *const *inputs, int k, void *out, size_t n,
+                           KungFu_Datatype dt, KungFu_Op op, int np, void *stream);
+
 /* Page-lock / release a host range so std_transform_2 and
  * kf_transform2_host can DMA it directly (e.g. a receive-buffer pool the
  * transport reuses, srcs/go/rchannel/connection/byte_slice_pool.go:28-60). */

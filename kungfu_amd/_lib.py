@@ -17,6 +17,7 @@ EXPORTED = (
     "float16_sum",
     "kf_bucket_reduce",
     "kf_bucket_reduce_avg",
+    "kf_bucket_reduce_peers",
     "kf_bucket_div",
     "kf_sma_blend",
     "kf_device_count",
@@ -103,6 +104,9 @@ def load():
     lib.kf_bucket_reduce_avg.argtypes = [ctypes.POINTER(c_void_p), c_int, c_void_p,
                                          c_size_t, c_int, c_int, c_void_p]
     lib.kf_bucket_reduce_avg.restype = c_int
+    lib.kf_bucket_reduce_peers.argtypes = [ctypes.POINTER(c_void_p), c_int, c_void_p,
+                                           c_size_t, c_int, c_int, c_int, c_void_p]
+    lib.kf_bucket_reduce_peers.restype = c_int
     lib.kf_bucket_div.argtypes = [c_void_p, c_size_t, c_int, c_int, c_void_p]
     lib.kf_bucket_div.restype = c_int
     lib.kf_sma_blend.argtypes = [c_void_p, c_void_p, c_size_t, c_int, c_int,

@@ -102,6 +102,9 @@ struct Plan {
     int grid_cap = 0;  // 0: geometry().grid_cap (HBM); >0: host-link launch
 };
 
+// launch-mode bits passed down the dispatch chain
+enum { LM_NONE = 0, LM_SPREAD = 1 };  // LM_SPREAD: inputs behind different links
+
 // Vector body needs every pointer at the same 16-B residue; the head peels
 // elements until they are aligned.
 Plan make_plan(const void *const *in, int k, const void *out, size_t n, int sz)
@@ -191,7 +194,7 @@ void launch_k(const InPtrs &ptrs, int k, void *out, size_t n, const Plan &p,
 
 template <typename T, int OP, int EPI>
 int launch_typed(const void *const *in, int k, void *out, size_t n, int npi,
-                 hipStream_t s, int grid_cap)
+                 hipStream_t s, int grid_cap, int mode = LM_NONE)
 {
     const Div np = make_div(npi);
     using S = typename Elt<T>::S;
@@ -199,7 +202,13 @@ int launch_typed(const void *const *in, int k, void *out, size_t n, int npi,
     for (int j = 0; j < kMaxInputs; ++j) ptrs.p[j] = j < k ? in[j] : nullptr;
     Plan p     = make_plan(in, k, out, n, sizeof(S));
     p.grid_cap = grid_cap;
-    if (!p.vec_ok) {
+    if (p.vec_ok && (mode & LM_SPREAD) && k > 1) {
+        constexpr int V  = Vec<S>::N;
+        const size_t ned = p.head + (n - p.head - p.nvec * V);
+        const unsigned g = grid_for(p.nvec, ned, 1);
+        reduce_spread_kernel<T, OP, EPI, kBlock><<<g, kBlock, 0, s>>>(ptrs, k, out, n, p.head,
+                                                                      p.nvec, np);
+    } else if (!p.vec_ok) {
         size_t blocks = (n + kBlock - 1) / kBlock;
         const size_t cap = grid_cap > 0 ? static_cast<size_t>(grid_cap) : 8192;
         if (blocks > cap) blocks = cap;
@@ -215,21 +224,21 @@ int launch_typed(const void *const *in, int k, void *out, size_t n, int npi,
 
 template <typename T, int EPI>
 int dispatch_op(const void *const *in, int k, void *out, size_t n, KungFu_Op op,
-                int np, hipStream_t s, int gc)
+                int np, hipStream_t s, int gc, int mode)
 {
     if constexpr (std::is_same<T, f16_t>::value) {
         if (op != KungFu_SUM) return KF_ERR_OP;  // op.cpp:45-54
-        return launch_typed<T, OP_SUM, EPI>(in, k, out, n, np, s, gc);
+        return launch_typed<T, OP_SUM, EPI>(in, k, out, n, np, s, gc, mode);
     } else {
         if constexpr (EPI == EPI_DIV) {
             if (op != KungFu_SUM) return KF_ERR_OP;
-            return launch_typed<T, OP_SUM, EPI>(in, k, out, n, np, s, gc);
+            return launch_typed<T, OP_SUM, EPI>(in, k, out, n, np, s, gc, mode);
         } else {
             switch (op) {
-            case KungFu_SUM: return launch_typed<T, OP_SUM, EPI>(in, k, out, n, np, s, gc);
-            case KungFu_MIN: return launch_typed<T, OP_MIN, EPI>(in, k, out, n, np, s, gc);
-            case KungFu_MAX: return launch_typed<T, OP_MAX, EPI>(in, k, out, n, np, s, gc);
-            case KungFu_PROD: return launch_typed<T, OP_PROD, EPI>(in, k, out, n, np, s, gc);
+            case KungFu_SUM: return launch_typed<T, OP_SUM, EPI>(in, k, out, n, np, s, gc, mode);
+            case KungFu_MIN: return launch_typed<T, OP_MIN, EPI>(in, k, out, n, np, s, gc, mode);
+            case KungFu_MAX: return launch_typed<T, OP_MAX, EPI>(in, k, out, n, np, s, gc, mode);
+            case KungFu_PROD: return launch_typed<T, OP_PROD, EPI>(in, k, out, n, np, s, gc, mode);
             default: return KF_ERR_OP;
             }
         }
@@ -237,33 +246,34 @@ int dispatch_op(const void *const *in, int k, void *out, size_t n, KungFu_Op op,
 }
 
 int dispatch_none(const void *const *in, int k, void *out, size_t n,
-                  KungFu_Datatype dt, KungFu_Op op, hipStream_t s, int gc = 0)
+                  KungFu_Datatype dt, KungFu_Op op, hipStream_t s, int gc = 0,
+                  int mode = LM_NONE)
 {
     switch (dt) {
-    case KungFu_UINT8: return dispatch_op<uint8_t, EPI_NONE>(in, k, out, n, op, 1, s, gc);
-    case KungFu_UINT16: return dispatch_op<uint16_t, EPI_NONE>(in, k, out, n, op, 1, s, gc);
-    case KungFu_UINT32: return dispatch_op<uint32_t, EPI_NONE>(in, k, out, n, op, 1, s, gc);
-    case KungFu_UINT64: return dispatch_op<uint64_t, EPI_NONE>(in, k, out, n, op, 1, s, gc);
-    case KungFu_INT8: return dispatch_op<int8_t, EPI_NONE>(in, k, out, n, op, 1, s, gc);
-    case KungFu_INT16: return dispatch_op<int16_t, EPI_NONE>(in, k, out, n, op, 1, s, gc);
-    case KungFu_INT32: return dispatch_op<int32_t, EPI_NONE>(in, k, out, n, op, 1, s, gc);
-    case KungFu_INT64: return dispatch_op<int64_t, EPI_NONE>(in, k, out, n, op, 1, s, gc);
-    case KungFu_FLOAT16: return dispatch_op<f16_t, EPI_NONE>(in, k, out, n, op, 1, s, gc);
-    case KungFu_FLOAT: return dispatch_op<float, EPI_NONE>(in, k, out, n, op, 1, s, gc);
-    case KungFu_DOUBLE: return dispatch_op<double, EPI_NONE>(in, k, out, n, op, 1, s, gc);
-    case KungFu_BFLOAT16: return dispatch_op<bf16_t, EPI_NONE>(in, k, out, n, op, 1, s, gc);
+    case KungFu_UINT8: return dispatch_op<uint8_t, EPI_NONE>(in, k, out, n, op, 1, s, gc, mode);
+    case KungFu_UINT16: return dispatch_op<uint16_t, EPI_NONE>(in, k, out, n, op, 1, s, gc, mode);
+    case KungFu_UINT32: return dispatch_op<uint32_t, EPI_NONE>(in, k, out, n, op, 1, s, gc, mode);
+    case KungFu_UINT64: return dispatch_op<uint64_t, EPI_NONE>(in, k, out, n, op, 1, s, gc, mode);
+    case KungFu_INT8: return dispatch_op<int8_t, EPI_NONE>(in, k, out, n, op, 1, s, gc, mode);
+    case KungFu_INT16: return dispatch_op<int16_t, EPI_NONE>(in, k, out, n, op, 1, s, gc, mode);
+    case KungFu_INT32: return dispatch_op<int32_t, EPI_NONE>(in, k, out, n, op, 1, s, gc, mode);
+    case KungFu_INT64: return dispatch_op<int64_t, EPI_NONE>(in, k, out, n, op, 1, s, gc, mode);
+    case KungFu_FLOAT16: return dispatch_op<f16_t, EPI_NONE>(in, k, out, n, op, 1, s, gc, mode);
+    case KungFu_FLOAT: return dispatch_op<float, EPI_NONE>(in, k, out, n, op, 1, s, gc, mode);
+    case KungFu_DOUBLE: return dispatch_op<double, EPI_NONE>(in, k, out, n, op, 1, s, gc, mode);
+    case KungFu_BFLOAT16: return dispatch_op<bf16_t, EPI_NONE>(in, k, out, n, op, 1, s, gc, mode);
     default: return KF_ERR_DTYPE;  // BOOL and unknown: op.cpp:88-89
     }
 }
 
 int dispatch_div(const void *const *in, int k, void *out, size_t n,
-                 KungFu_Datatype dt, int np, hipStream_t s)
+                 KungFu_Datatype dt, int np, hipStream_t s, int mode = LM_NONE)
 {
     switch (dt) {
-    case KungFu_FLOAT16: return dispatch_op<f16_t, EPI_DIV>(in, k, out, n, KungFu_SUM, np, s, 0);
-    case KungFu_FLOAT: return dispatch_op<float, EPI_DIV>(in, k, out, n, KungFu_SUM, np, s, 0);
-    case KungFu_DOUBLE: return dispatch_op<double, EPI_DIV>(in, k, out, n, KungFu_SUM, np, s, 0);
-    case KungFu_BFLOAT16: return dispatch_op<bf16_t, EPI_DIV>(in, k, out, n, KungFu_SUM, np, s, 0);
+    case KungFu_FLOAT16: return dispatch_op<f16_t, EPI_DIV>(in, k, out, n, KungFu_SUM, np, s, 0, mode);
+    case KungFu_FLOAT: return dispatch_op<float, EPI_DIV>(in, k, out, n, KungFu_SUM, np, s, 0, mode);
+    case KungFu_DOUBLE: return dispatch_op<double, EPI_DIV>(in, k, out, n, KungFu_SUM, np, s, 0, mode);
+    case KungFu_BFLOAT16: return dispatch_op<bf16_t, EPI_DIV>(in, k, out, n, KungFu_SUM, np, s, 0, mode);
     default: return KF_ERR_DTYPE;
     }
 }
@@ -534,6 +544,29 @@ int kf_sma_blend(void *v, const void *sum, size_t n, KungFu_Datatype dt, int np,
     case KungFu_BFLOAT16: return launch_sma<bf16_t, float>(v, sum, n, np, c1f, c2f, s);
     default: return KF_ERR_DTYPE;
     }
+}
+
+int kf_bucket_reduce_peers(const void *const *inputs, int k, void *out, size_t n,
+                           KungFu_Datatype dt, KungFu_Op op, int np, void *stream)
+{
+    int rc = check_args(inputs, k, out, n);
+    if (rc != KF_OK || n == 0) return rc;
+    const int sz = type_size(dt);
+    if (sz == 0 || dt == KungFu_BOOL) return KF_ERR_DTYPE;
+    if (np < 0) return KF_ERR_ARG;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (np > 0) {  // average: SUM then / np
+        if (!is_float(dt)) return KF_ERR_DTYPE;
+        if (op != KungFu_SUM) return KF_ERR_OP;
+        return dispatch_div(inputs, k, out, n, dt, np, s, LM_SPREAD);
+    }
+    if (op < KungFu_SUM || op > KungFu_PROD) return KF_ERR_OP;
+    if (dt == KungFu_FLOAT16 && op != KungFu_SUM) return KF_ERR_OP;
+    if (k == 1) {
+        if (out != inputs[0]) KF_HIP(hipMemcpyAsync(out, inputs[0], n * sz, hipMemcpyDefault, s));
+        return KF_OK;
+    }
+    return dispatch_none(inputs, k, out, n, dt, op, s, 0, LM_SPREAD);
 }
 
 int kf_set_geometry(int unroll, int grid_cap, int loadnt, int stplain)

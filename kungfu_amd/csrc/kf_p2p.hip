@@ -33,16 +33,19 @@ struct Segs {
     size_t len[KF_MAX_SEGMENTS];  // bytes, multiple of 16
 };
 
-// blockIdx.y = segment; each block copies 4 x 16 B per thread per tile,
-// non-temporal both ways (each byte moves once).
-__global__ void __launch_bounds__(256) gather_kernel(char *dst, Segs segs)
+// 1-D grid, segment = blockIdx.x % nseg: consecutive blocks (dispatched
+// together) pull from different peers, so every link is busy from the start
+// instead of one peer's segment after another. Each block copies 4 x 16 B per
+// thread per tile, non-temporal both ways (each byte moves once).
+__global__ void __launch_bounds__(256) gather_kernel(char *dst, Segs segs, int nseg)
 {
-    const int s       = blockIdx.y;
+    const int s       = static_cast<int>(blockIdx.x % nseg);
     const size_t nvec = segs.len[s] / 16;
     const u32x4 *src  = reinterpret_cast<const u32x4 *>(segs.src[s] + segs.off[s]);
     u32x4 *out        = reinterpret_cast<u32x4 *>(dst + segs.off[s]);
     const size_t tile = 256 * 4;
-    for (size_t t = blockIdx.x; t * tile < nvec; t += gridDim.x) {
+    const size_t nblk = gridDim.x / nseg;  // blocks per segment
+    for (size_t t = blockIdx.x / nseg; t * tile < nvec; t += nblk) {
         const size_t v0 = t * tile + threadIdx.x;
         u32x4 r[4];
 #pragma unroll
@@ -117,11 +120,11 @@ int kf_gather_segments(void *dst, const void *const *srcs, const size_t *offsets
         if (lens[i] > maxlen) maxlen = lens[i];
     }
     const size_t tile   = 256 * 4 * 16;
-    size_t bx           = (maxlen + tile - 1) / tile;
-    if (bx > 65535) bx = 65535;
+    size_t bx           = (maxlen + tile - 1) / tile;  // blocks per segment
+    if (bx > (size_t(1) << 16)) bx = size_t(1) << 16;
     if (bx < 1) bx = 1;
-    dim3 grid(static_cast<unsigned>(bx), static_cast<unsigned>(nseg));
-    gather_kernel<<<grid, 256, 0, static_cast<hipStream_t>(stream)>>>(static_cast<char *>(dst), segs);
+    gather_kernel<<<static_cast<unsigned>(bx * nseg), 256, 0, static_cast<hipStream_t>(stream)>>>(
+        static_cast<char *>(dst), segs, nseg);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "gather_kernel launch");
     return KF_OK;

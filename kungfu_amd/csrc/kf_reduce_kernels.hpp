@@ -427,6 +427,67 @@ __global__ void __launch_bounds__(BLOCK)
     }
 }
 
+// Fold for inputs that sit behind DIFFERENT links (the P2P shard fold reads
+// shard `rank` of every peer's bucket over that peer's xGMI link). The runtime
+// k loop above issues one input at a time, and since every resident block
+// walks the inputs in the same order, at any moment nearly all requests go to
+// one or two peers: the links would be used one after another. Here every
+// thread issues the loads of up to 8 inputs before the first add, so all links
+// carry traffic at once; the adds still run in input order (rank order), so
+// the result is the same left fold bit for bit. One 16-B vector per input per
+// thread per tile; k > 8 goes in groups of 8.
+template <typename T, int OP, int EPI, int BLOCK>
+__global__ void __launch_bounds__(BLOCK)
+    reduce_spread_kernel(InPtrs in, int k, void *out, size_t n, size_t head,
+                         size_t nvec, Div np)
+{
+    using S         = typename Elt<T>::S;
+    using Acc       = typename Elt<T>::Acc;
+    constexpr int V = Vec<S>::N;
+    constexpr int G = 8;
+    const size_t tid   = static_cast<size_t>(blockIdx.x) * BLOCK + threadIdx.x;
+    const size_t vend  = head + nvec * V;
+    const size_t nedge = head + (n - vend);
+    if (tid < nedge) {
+        const size_t i = tid < head ? tid : vend + (tid - head);
+        reinterpret_cast<S *>(out)[i] = fold_scalar<T, OP, EPI>(in, k, i, np);
+    }
+    char *obase = reinterpret_cast<char *>(out) + head * sizeof(S);
+    for (size_t vi = tid; vi < nvec; vi += static_cast<size_t>(gridDim.x) * BLOCK) {
+        Acc acc[V];
+        for (int j0 = 0; j0 < k; j0 += G) {
+            Vec<S> v[G];
+#pragma unroll
+            for (int j = 0; j < G; ++j) {
+                if (j0 + j < k) {
+                    v[j] = ld_vec<S, 1>(reinterpret_cast<const char *>(in.p[j0 + j]) +
+                                            head * sizeof(S), vi);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < G; ++j) {
+                if (j0 + j < k) {
+#pragma unroll
+                    for (int e = 0; e < V; ++e) {
+                        acc[e] = (j0 + j == 0) ? Elt<T>::load(v[j].e[e])
+                                               : Elt<T>::template combine<OP>(acc[e], v[j].e[e]);
+                    }
+                }
+            }
+        }
+        Vec<S> r;
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+            if constexpr (EPI == EPI_DIV) {
+                r.e[e] = Elt<T>::div(acc[e], np);
+            } else {
+                r.e[e] = finish<T, OP>(acc[e]);
+            }
+        }
+        st_vec<S>(obase, vi, r);
+    }
+}
+
 // Element-at-a-time kernel for inputs whose 16-B alignment residues differ
 // (e.g. host-side chunk slices at odd offsets). Still coalesced per element.
 template <typename T, int OP, int EPI, int BLOCK>

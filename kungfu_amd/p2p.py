@@ -8,10 +8,14 @@ once. One all-reduce is then:
                                     of all `world` buckets straight from the
                                     peers' HBM over their xGMI links, in rank
                                     order, and writes it (with the S-SGD /np
-                                    epilogue fused) into my own bucket;
+                                    epilogue fused) into my own bucket; the
+                                    loads of all peers are in flight together
+                                    (kf_bucket_reduce_peers) so every link
+                                    carries traffic at once;
   3. barrier                      — every shard is reduced;
   4. gather the other shards      — one kernel pulls shard r from rank r's
-                                    bucket for every r != rank;
+                                    bucket for every r != rank, consecutive
+                                    blocks on different peers;
   5. barrier                      — nobody rewrites a bucket a peer still reads.
 
 The fold order is fixed (rank 0, 1, ..., n-1), so results are deterministic and
@@ -89,12 +93,10 @@ class P2PExchange:
             off = rank * shard * isz
             ins = _lib.ptr_array([p + off for p in row])
             out = b.data_ptr() + off
-            if average:
-                rc = self.lib.kf_bucket_reduce_avg(ins, world, out, shard,
-                                                   int(kungfu_dtype(b)), world, s)
-            else:
-                rc = self.lib.kf_bucket_reduce(ins, world, out, shard, int(kungfu_dtype(b)),
-                                               int(OP_NAMES[op]), s)
+            # every peer's load in flight at once (all links busy), adds in
+            # rank order
+            rc = self.lib.kf_bucket_reduce_peers(ins, world, out, shard, int(kungfu_dtype(b)),
+                                                 int(OP_NAMES[op]), world if average else 0, s)
             _lib.check(rc, "p2p shard reduce")
         self._barrier()
         for b, row in zip(self.buckets, self.ptrs):

@@ -189,6 +189,47 @@ def test_k_input_ring_order_bit_exact(lib, orc, dev, k):
     assert np.array_equal(dev_reduce(lib, bs, 0x20209, 0, dev), orc.reduce_k(bs, "bf16"))
 
 
+@pytest.mark.parametrize("k", [2, 3, 5, 8, 9, 16])
+def test_peers_fold_bit_exact(lib, orc, dev, k):
+    # kf_bucket_reduce_peers (all inputs' loads in flight, the P2P shard fold):
+    # the same left fold in input order as the oracle, for plain ops and the
+    # fused / np, with a ragged tail and a co-misaligned head
+    from kungfu_amd import _lib
+    from oracle.oracle import DT
+    rng = np.random.default_rng(100 + k)
+    n = 65536 * 3 + 7
+    s = torch.cuda.current_stream().cuda_stream
+    cases = [("f32", [rng.standard_normal(n + 1).astype(np.float32) for _ in range(k)]),
+             ("i32", [rng.integers(-2**31, 2**31 - 1, size=n + 1, dtype=np.int32)
+                      for _ in range(k)]),
+             ("f16", [(rng.standard_normal(n + 1) * 30).astype(np.float16) for _ in range(k)]),
+             ("bf16", [orc.f32_to_bf16_bits(rng.standard_normal(n + 1).astype(np.float32))
+                       for _ in range(k)])]
+    for dt, xs in cases:
+        for head in (0, 1):
+            ts = [to_dev(x, dev) for x in xs]
+            isz = xs[0].itemsize
+            out = torch.zeros_like(ts[0])
+            ptrs = _lib.ptr_array([t.data_ptr() + head * isz for t in ts])
+            ops = ["sum"] if dt == "f16" else ["sum", "max"]
+            for op in ops:
+                rc = lib.kf_bucket_reduce_peers(ptrs, k, out.data_ptr() + head * isz, n, DT[dt],
+                                                {"sum": 0, "max": 2}[op], 0, s)
+                assert rc == 0, lib.kf_last_error()
+                torch.cuda.synchronize()
+                got = from_dev(out, xs[0])[head:head + n]
+                want = orc.reduce_k([x[head:head + n].copy() for x in xs], dt, op)
+                assert golden_io.same_bits_or_nan(got, want), (dt, op, head)
+            if dt != "i32":
+                rc = lib.kf_bucket_reduce_peers(ptrs, k, out.data_ptr() + head * isz, n, DT[dt],
+                                                0, k, s)
+                assert rc == 0, lib.kf_last_error()
+                torch.cuda.synchronize()
+                got = from_dev(out, xs[0])[head:head + n]
+                want = orc.reduce_avg([x[head:head + n].copy() for x in xs], dt, k)
+                assert golden_io.same_bits_or_nan(got, want), (dt, "avg", head)
+
+
 def test_schedule_all_reduce_matches_device_fold(lib, orc, dev):
     # Whole reference schedule (RING, np=4, 4 MiB bucket = 4 chunks with
     # hash-chosen roots): per chunk, the device fold in that chunk's ring order

@@ -45,6 +45,24 @@ def main():
         rows.append(dict(kernel=name, us=round(us, 2), algorithmic_bytes=algo_bytes,
                          GBps=round(gbps, 1), frac=round(gbps / PEAK, 4), **kw))
 
+    n = BYTES // 4
+    for k in (2, 4, 8):  # the P2P fold kernel (all loads in flight) on local HBM
+        sets = []
+        for _ in range(3):
+            ins = [torch.randn(n, device=dev) for _ in range(k)]
+            out = torch.empty_like(ins[0])
+            sets.append((_lib.ptr_array([t.data_ptr() for t in ins]), out, ins))
+
+        def run_p(ptrs, out, ins, k=k):
+            lib.kf_bucket_reduce_peers(ptrs, k, out.data_ptr(), out.numel(), 0x20408, 0, k, s)
+        report("reduce_peers avg k=%d (P2P fold, local HBM)" % k, (k + 1) * BYTES,
+               timeit(run_p, sets), dtype="torch.float32")
+        del sets
+        torch.cuda.empty_cache()
+    if "--peers-only" in sys.argv:
+        for r in rows:
+            print(json.dumps(r))
+        return
     for dtype, code in ((torch.float32, 0x20408), (torch.float16, 0x20208),
                         (torch.bfloat16, 0x20209), (torch.float64, 0x20808),
                         (torch.int32, 0x10408), (torch.int8, 0x10108)):
