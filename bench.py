@@ -398,6 +398,7 @@ def main():
         parallelism = "single GPU"
     else:
         from kungfu_amd.collective import Exchange, GradBuckets
+        _progress(rank, "C3 all-reduce, %d ranks" % world)
         ex = Exchange()
         # the 256 MiB gradient set as --buckets equal pipelined buckets
         gb = GradBuckets([n], torch.float32, dev, world, n_buckets=args.buckets)
@@ -465,6 +466,7 @@ def main():
         for key, fn in extra:
             if args.no_extra:
                 break
+            _progress(rank, "sub-benchmark %s" % key)
             try:
                 out[key] = fn()
             except Exception as e:  # keep the primary line; say what failed
@@ -517,6 +519,16 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def _progress(rank, what):
+    """One line on stderr per phase (rank 0), so a long multi-GPU run shows
+    it is alive; stdout carries only the JSON line."""
+    if rank == 0:
+        print("[bench] %.1f s: %s" % (time.perf_counter() - _T0, what), file=sys.stderr, flush=True)
+
+
+_T0 = time.perf_counter()
 
 
 def _models():
