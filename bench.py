@@ -75,7 +75,9 @@ def parse():
     ap.add_argument("--device-index", type=int, default=None,
                     help="rehearsal only: put every rank on this GPU")
     ap.add_argument("--no-extra", action="store_true",
-                    help="N>1: skip the C4/C5 sub-benchmarks")
+                    help="N>1: skip the C4/C5/P2P sub-benchmarks")
+    ap.add_argument("--extras", default="c4,c5,c3_ar,c3_p2p",
+                    help="N>1: which sub-benchmarks to run (comma list)")
     ap.add_argument("--config", default="default", choices=["default", "c1"],
                     help="c1: BASELINE configs[0], np=2 localhost all-reduce of "
                          "one 4 MiB fp32 bucket over the rchannel wire format")
@@ -451,8 +453,9 @@ def main():
             "per_bucket_ms_per_step": round(per_s * 1e3, 4),
             "per_bucket_busbw_GBps": round(2 * (world - 1) / world * s_bytes / per_s / 1e9, 2),
         }
-        workload = ("C3: S-SGD all-reduce of %d fp32 buckets (256 MiB) per rank, "
-                    "fused: RCCL reduce-scatter -> HIP /np -> RCCL all-gather" % len(pieces))
+        workload = ("C3: S-SGD all-reduce of %d fp32 buckets (%d MiB) per rank, "
+                    "fused: RCCL reduce-scatter -> HIP /np -> RCCL all-gather"
+                    % (len(pieces), s_bytes >> 20))
         parallelism = "dp%d" % world
         kt = torch.tensor([kernel_s], dtype=torch.float64, device=dev)
         dist.all_reduce(kt, op=dist.ReduceOp.MAX)
@@ -460,19 +463,22 @@ def main():
         # the other multi-GPU configs of BASELINE.json, reported beside `value`
         extra = (("c4", lambda: bench_c4(world, rank, dev, min(args.steps, 50), 5)),
                  ("c5", lambda: bench_c5(world, rank, dev, min(args.steps, 50), 5)),
+                 ("c3_ar", lambda: bench_c3_ar(world, rank, dev, min(args.steps, 50), 5, n, x)),
                  # last: the experimental peer-to-peer path
                  ("c3_p2p", lambda: bench_c3_p2p(world, rank, dev, min(args.steps, 50), 5,
                                                  n, x)))
         for key, fn in extra:
             if args.no_extra:
                 break
+            if key not in args.extras.split(","):
+                continue
             _progress(rank, "sub-benchmark %s" % key)
             try:
                 out[key] = fn()
             except Exception as e:  # keep the primary line; say what failed
                 out[key] = {"error": repr(e)[:300]}
 
-    traffic, tsrc = load_traffic()
+    traffic, tsrc = load_traffic() if n == BUCKET_ELEMS else (None, None)
     achieved = 3 * s_bytes / kernel_s / 1e9
     res = {
         "metric": METRIC,
@@ -606,6 +612,40 @@ def bench_c4(world, rank, dev, steps, warmup):
     return {"workload": "C4: ResNet-50 grads, 25,583,592 fp32 in %d buckets, S-SGD "
                         "(RCCL RS -> HIP /np -> RCCL AG)" % len(mine.buckets),
             "bytes": s_bytes, "ms_per_step": round(step_s * 1e3, 4),
+            "GiBps_per_gpu": round(s_bytes / step_s / 2**30, 3),
+            "busbw_GBps": round(busbw, 2),
+            "frac_of_xgmi": round(busbw / (153.0 * (world - 1)), 4)}
+
+
+def bench_c3_ar(world, rank, dev, steps, warmup, n, x):
+    """C3 as ONE RCCL all-reduce (sum) of the 256 MiB bucket, then the HIP
+    /np over the whole bucket: the alternative to RS -> /np on the shard -> AG,
+    reported beside it to pick the faster exchange per N."""
+    from kungfu_amd import ops
+    b = x.clone()
+    dist.all_reduce(b)
+    ops.bucket_div_(b, world)
+    allx = [torch.randn(n, device=dev, generator=torch.Generator(device=dev).manual_seed(2 * r))
+            for r in range(world)]
+    want = ops.bucket_reduce_avg(allx, world)
+    ok = bool(torch.equal(b, want)) if world == 2 else _within(b, want, sum(a.abs() for a in allx),
+                                                                world)
+    del allx, want
+    if not _agree(ok, dev):
+        return {"error": "all-reduce + /np check failed (N=2 bit-exact / N>2 bound)"}
+
+    def step():
+        b.copy_(x)
+        dist.all_reduce(b)
+        ops.bucket_div_(b, world)
+
+    step_s = _timed(step, steps, warmup, dev, world)
+    cp_s = _timed(lambda: b.copy_(x), steps, warmup, dev, world)  # refill, subtracted
+    step_s = max(step_s - cp_s, 1e-9)
+    s_bytes = n * 4
+    busbw = 2 * (world - 1) / world * s_bytes / step_s / 1e9
+    return {"workload": "C3 as RCCL all_reduce(sum) of the 256 MiB bucket + HIP /np over it",
+            "ms_per_step": round(step_s * 1e3, 4),
             "GiBps_per_gpu": round(s_bytes / step_s / 2**30, 3),
             "busbw_GBps": round(busbw, 2),
             "frac_of_xgmi": round(busbw / (153.0 * (world - 1)), 4)}

@@ -362,6 +362,7 @@ struct SendItem {  // one chunk to every fd in `fds` (the node's successors)
     const char *ptr;
     size_t bytes;
     void *stream;
+    hipEvent_t ready;  // device mode: recorded on `stream` when the chunk is final
 };
 
 }  // namespace
@@ -379,6 +380,9 @@ struct kf_session {
     std::unordered_map<int, int> out_fd, in_fd;  // peer -> fd
     kf_ingest_t *ingest = nullptr;
     void *tx            = nullptr;  // device mode: page-locked outgoing chunk (sender thread)
+    hipStream_t tx_stream = nullptr;  // sender's D2H stream
+    std::vector<hipEvent_t> ev_pool;  // free "chunk is final" events
+    std::mutex ev_mu;
     kf_host_reduce_fn host_fn = nullptr;
     std::vector<char> scratch;  // host-mode landing buffer (one chunk)
     int batch_fold = 1;         // device mode: k-input fold at multi-predecessor nodes
@@ -415,6 +419,8 @@ struct kf_session {
         if (listen_tcp >= 0) ::close(listen_tcp);
         if (ingest) kf_ingest_destroy(ingest);
         if (tx) (void)hipHostFree(tx);
+        for (auto e : ev_pool) (void)hipEventDestroy(e);
+        if (tx_stream) (void)hipStreamDestroy(tx_stream);
         if (stage) (void)hipFree(stage);
     }
 
@@ -446,17 +452,45 @@ struct kf_session {
     // Device mode: ONE copy of the chunk to page-locked memory, then the same
     // bytes to every successor (a star root sends its reduced chunk to np-1
     // peers). The stream sync also orders the copy after the chunk's fold.
+    // An event marking "this chunk is final on the caller's stream" (its fold
+    // was queued before), so the sender waits for that chunk only, not for
+    // the folds of later chunks queued on the same stream meanwhile.
+    hipEvent_t chunk_ready(void *stream)
+    {
+        hipEvent_t e = nullptr;
+        {
+            std::lock_guard<std::mutex> l(ev_mu);
+            if (!ev_pool.empty()) {
+                e = ev_pool.back();
+                ev_pool.pop_back();
+            }
+        }
+        if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+        if (hipEventRecord(e, static_cast<hipStream_t>(stream)) != hipSuccess) {
+            (void)hipEventDestroy(e);
+            return nullptr;
+        }
+        return e;
+    }
+
     int send_item(const SendItem &it, std::string *err)
     {
         const char *src = it.ptr;
         if (device_mode) {
-            hipStream_t st = static_cast<hipStream_t>(it.stream);
             if (it.bytes > kChunk + 4096) {
                 *err = "chunk larger than the tx buffer";
                 return KF_ERR_ARG;
             }
-            if (hipMemcpyAsync(tx, it.ptr, it.bytes, hipMemcpyDeviceToHost, st) != hipSuccess ||
-                hipStreamSynchronize(st) != hipSuccess) {
+            const bool ok = it.ready &&
+                            hipStreamWaitEvent(tx_stream, it.ready, 0) == hipSuccess &&
+                            hipMemcpyAsync(tx, it.ptr, it.bytes, hipMemcpyDeviceToHost,
+                                           tx_stream) == hipSuccess &&
+                            hipStreamSynchronize(tx_stream) == hipSuccess;
+            if (it.ready) {
+                std::lock_guard<std::mutex> l(ev_mu);
+                ev_pool.push_back(it.ready);
+            }
+            if (!ok) {
                 *err = "D2H of an outgoing chunk failed";
                 return KF_ERR_HIP;
             }
@@ -742,7 +776,8 @@ int kf_session::all_reduce(const char *send, char *recv, size_t count, KungFu_Da
         std::vector<int> fds;
         for (int p : c.st->bcast.next[rank]) fds.push_back(out_fd[p]);
         if (!fds.empty()) {
-            enqueue({fds, c.name, KF_RCH_WAIT_RECV_BUF, effective(i), clen(i), stream});
+            enqueue({fds, c.name, KF_RCH_WAIT_RECV_BUF, effective(i), clen(i), stream,
+                     device_mode ? chunk_ready(stream) : nullptr});
         }
         c.bcast_done = true;
     };
@@ -751,7 +786,8 @@ int kf_session::all_reduce(const char *send, char *recv, size_t count, KungFu_Da
         std::vector<int> fds;
         for (int p : c.st->reduce.next[rank]) fds.push_back(out_fd[p]);
         if (!fds.empty()) {
-            enqueue({fds, c.name, KF_RCH_NO_FLAG, effective(i), clen(i), stream});
+            enqueue({fds, c.name, KF_RCH_NO_FLAG, effective(i), clen(i), stream,
+                     device_mode ? chunk_ready(stream) : nullptr});
         }
         if (c.st->bcast.prev[rank].empty()) finish_bcast(i);
     };
@@ -964,7 +1000,10 @@ kf_session_t *create_session(int rank, std::vector<PeerAddr> peers, const char *
     if (s->device_mode) {
         s->ingest = kf_ingest_create(kChunk + 4096, 8);
         if (hipHostMalloc(&s->tx, kChunk + 4096, hipHostMallocDefault) != hipSuccess) s->tx = nullptr;
-        if (!s->ingest || !s->tx) {
+        if (hipStreamCreateWithFlags(&s->tx_stream, hipStreamNonBlocking) != hipSuccess) {
+            s->tx_stream = nullptr;
+        }
+        if (!s->ingest || !s->tx || !s->tx_stream) {
             t_sess_error = "kf_ingest_create failed";
             delete s;
             return nullptr;

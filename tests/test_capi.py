@@ -121,3 +121,17 @@ def test_device_api_arg_errors(lib):
     assert lib.kf_bucket_reduce_avg(_lib.ptr_array([8, 8]), 2, 8, 16, 0x10408, 2,
                                     None) == 1  # ints have no /np epilogue
     assert lib.kf_bucket_div(8, 16, 0x20408, 0, None) == 3
+
+
+def test_peers_fold_arg_errors(lib):
+    # kf_bucket_reduce_peers: B2 contract (status codes, no device touched)
+    from kungfu_amd import _lib
+    arr = _lib.ptr_array([8, 8])
+    assert lib.kf_bucket_reduce_peers(arr, 2, 8, 0, 0x20408, 0, 0, None) == 0  # n = 0
+    assert lib.kf_bucket_reduce_peers(arr, 0, 8, 16, 0x20408, 0, 0, None) == 3
+    assert lib.kf_bucket_reduce_peers(arr, 17, 8, 16, 0x20408, 0, 0, None) == 3
+    assert lib.kf_bucket_reduce_peers(arr, 2, 8, 16, 0x10408, 0, 2, None) == 1  # int avg
+    assert lib.kf_bucket_reduce_peers(arr, 2, 8, 16, 0x20408, 1, 2, None) == 2  # avg needs SUM
+    assert lib.kf_bucket_reduce_peers(arr, 2, 8, 16, 0x20208, 1, 0, None) == 2  # f16 MIN
+    assert lib.kf_bucket_reduce_peers(arr, 2, 8, 16, 0x30108, 0, 0, None) == 1  # BOOL
+    assert lib.kf_bucket_reduce_peers(arr, 2, 8, 16, 0x20408, 0, -1, None) == 3
