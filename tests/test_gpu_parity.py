@@ -511,3 +511,69 @@ def test_dropin_vs_reference_build(lib, dt):
         ref.std_transform_2(x.ctypes.data, y.ctypes.data, want.ctypes.data, n, DT[dt], code)
         lib.std_transform_2(x.ctypes.data, y.ctypes.data, got.ctypes.data, n, DT[dt], code)
         assert golden_io.same_bits_or_nan(got, want), (dt, op)
+
+
+# ---- maximum sizes: 64-bit element indices and the drop-in's int n limit ---
+
+def _windows(n, w=4099):
+    """Index windows that straddle the 2^31 / 2^32 element and byte edges."""
+    edges = [0, (1 << 31) - w // 2, (1 << 32) - w // 2, n - w]
+    return [(max(0, a), min(n, a + w)) for a in edges if a < n]
+
+
+def test_device_u8_beyond_2pow32(lib, orc, dev):
+    # 4 GiB + 37 per input: element (and byte) indices past 2^32 in the vector
+    # body and the scalar tail; bit-exact vs the oracle on windows around
+    # every 2^31/2^32 edge, and vs u8 wrap-around add over the whole bucket
+    from kungfu_amd import _lib
+    n = (1 << 32) + 37
+    g = torch.Generator(device=dev).manual_seed(7)
+    x = torch.randint(0, 256, (n,), dtype=torch.uint8, device=dev, generator=g)
+    y = torch.randint(0, 256, (n,), dtype=torch.uint8, device=dev, generator=g)
+    z = torch.empty_like(x)
+    rc = lib.kf_bucket_reduce(_lib.ptr_array([x.data_ptr(), y.data_ptr()]), 2,
+                              z.data_ptr(), n, 0x00108, 0,
+                              torch.cuda.current_stream().cuda_stream)
+    assert rc == 0, lib.kf_last_error()
+    torch.cuda.synchronize()
+    assert torch.equal(z, x + y)
+    for a, b in _windows(n):
+        xh, yh = x[a:b].cpu().numpy(), y[a:b].cpu().numpy()
+        assert np.array_equal(z[a:b].cpu().numpy(), orc.transform2(xh, yh, "u8", "sum")), (a, b)
+    del x, y, z
+    torch.cuda.empty_cache()
+
+
+def test_device_f32_beyond_2pow31_with_avg(lib, orc, dev):
+    # 8 GiB + 20 B per input, k = 3 fold (byte offsets past 2^33): the SUM
+    # over the whole bucket equals (x + y) + w added in order (each add
+    # correctly rounded, so torch's adds are an exact check), and the fused
+    # /np fold is bit-exact vs the oracle on windows around every edge
+    from kungfu_amd import ops
+    n = (1 << 31) + 5
+    g = torch.Generator(device=dev).manual_seed(8)
+    ins = [torch.randn(n, device=dev, generator=g) for _ in range(3)]
+    z = ops.bucket_reduce(ins)
+    torch.cuda.synchronize()
+    assert torch.equal(z, (ins[0] + ins[1]) + ins[2])
+    ops.bucket_reduce_avg(ins, 3, out=z)
+    torch.cuda.synchronize()
+    for a, b in _windows(n):
+        hs = [t[a:b].cpu().numpy() for t in ins]
+        assert np.array_equal(z[a:b].cpu().numpy(), orc.reduce_avg(hs, "f32", 3)), (a, b)
+    del ins, z
+    torch.cuda.empty_cache()
+
+
+def test_dropin_int_max_n(lib, orc):
+    # B1's n is a C int (op.h:17-19): the largest call the reference can make,
+    # n = 2^31 - 1 u8 elements through pageable host buffers
+    n = (1 << 31) - 1
+    rng = np.random.default_rng(9)
+    x = rng.integers(0, 256, size=n, dtype=np.uint8)
+    y = rng.integers(0, 256, size=n, dtype=np.uint8)
+    got = np.empty_like(x)
+    lib.std_transform_2(x.ctypes.data, y.ctypes.data, got.ctypes.data, n, 0x00108, 0)
+    assert np.array_equal(got, x + y)
+    for a, b in _windows(n):
+        assert np.array_equal(got[a:b], orc.transform2(x[a:b], y[a:b], "u8", "sum")), (a, b)
