@@ -135,3 +135,24 @@ def test_peers_fold_arg_errors(lib):
     assert lib.kf_bucket_reduce_peers(arr, 2, 8, 16, 0x20208, 1, 0, None) == 2  # f16 MIN
     assert lib.kf_bucket_reduce_peers(arr, 2, 8, 16, 0x30108, 0, 0, None) == 1  # BOOL
     assert lib.kf_bucket_reduce_peers(arr, 2, 8, 16, 0x20408, 0, -1, None) == 3
+
+
+def test_go_overlay_binds_declared_symbols():
+    # go/kungfu/base/*.go (the cgo drop-in, compiled nowhere here: no Go
+    # toolchain) may only call C names the header declares
+    import glob
+    import re
+    with open(os.path.join(ROOT, "include", "kungfu_amd.h")) as f:
+        header = f.read()
+    libc = {"malloc", "free", "GoString", "int", "size_t", "double", "KungFu_Op",
+            "KungFu_Datatype"}
+    files = glob.glob(os.path.join(ROOT, "go", "kungfu", "base", "*.go"))
+    assert files
+    for path in files:
+        with open(path) as f:
+            src = f.read()
+        assert src.startswith("//go:build kungfu_amd"), path
+        for name in set(re.findall(r"\bC\.([A-Za-z_][A-Za-z0-9_]*)", src)):
+            if name in libc:
+                continue
+            assert re.search(r"\b%s\b" % re.escape(name), header), (path, name)
