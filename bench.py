@@ -37,6 +37,7 @@ import ctypes
 import json
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -78,6 +79,9 @@ def parse():
                     help="N>1: skip the C4/C5/P2P sub-benchmarks")
     ap.add_argument("--extras", default="c4,c5,c3_ar,c3_p2p",
                     help="N>1: which sub-benchmarks to run (comma list)")
+    ap.add_argument("--extras-timeout", type=float, default=240.0,
+                    help="N>1: seconds for all sub-benchmarks together; past it the "
+                         "line is printed with what finished and the ranks exit")
     ap.add_argument("--config", default="default", choices=["default", "c1"],
                     help="c1: BASELINE configs[0], np=2 localhost all-reduce of "
                          "one 4 MiB fp32 bucket over the rchannel wire format")
@@ -467,20 +471,53 @@ def main():
                  # last: the experimental peer-to-peer path
                  ("c3_p2p", lambda: bench_c3_p2p(world, rank, dev, min(args.steps, 50), 5,
                                                  n, x)))
+        # The primary number is measured by now: a sub-benchmark that hangs
+        # (a peer mapping refused in a way that blocks, a stuck collective)
+        # must not take it down. Past --extras-timeout every rank stops; rank 0
+        # first prints the line with what was measured so far.
+        prim = dict(value=value, step_s=step_s, kernel_s=kernel_s, workload=workload,
+                    parallelism=parallelism)
+        dog = threading.Timer(args.extras_timeout, _extras_timeout,
+                              (args, rank, world, sets, s_bytes, n, hot_s, prim, out))
+        dog.daemon = True
+        dog.start()
         for key, fn in extra:
             if args.no_extra:
                 break
             if key not in args.extras.split(","):
                 continue
             _progress(rank, "sub-benchmark %s" % key)
+            out["_running"] = key
             try:
                 out[key] = fn()
             except Exception as e:  # keep the primary line; say what failed
                 out[key] = {"error": repr(e)[:300]}
+        out.pop("_running", None)
+        dog.cancel()
 
+    res = _result(args, world, sets, s_bytes, n, hot_s,
+                  dict(value=value, step_s=step_s, kernel_s=kernel_s, workload=workload,
+                       parallelism=parallelism))
+    res.update(out)
+    if rank == 0 and world == 1:
+        if not args.no_host_staged:
+            res["host_staged"] = host_staged(lib, x, y)
+        if not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(x, y, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def _result(args, world, sets, s_bytes, n, hot_s, prim):
+    """The bench line's primary fields (everything but the sub-benchmarks)."""
+    value, step_s, kernel_s = prim["value"], prim["step_s"], prim["kernel_s"]
+    workload, parallelism = prim["workload"], prim["parallelism"]
     traffic, tsrc = load_traffic() if n == BUCKET_ELEMS else (None, None)
     achieved = 3 * s_bytes / kernel_s / 1e9
-    res = {
+    return {
         "metric": METRIC,
         "value": round(value, 3),
         "unit": "GiB/s",
@@ -514,17 +551,20 @@ def main():
             "same_buffer_GBps": round(3 * s_bytes / hot_s / 1e9, 1),
         },
     }
+
+
+def _extras_timeout(args, rank, world, sets, s_bytes, n, hot_s, prim, out):
+    """Watchdog of the N>1 sub-benchmarks (a thread): print the line with the
+    primary number and whatever finished, then end this rank at once."""
+    res = _result(args, world, sets, s_bytes, n, hot_s, prim)
+    stuck = out.pop("_running", "?")
     res.update(out)
-    if rank == 0 and world == 1:
-        if not args.no_host_staged:
-            res["host_staged"] = host_staged(lib, x, y)
-        if not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(x, y, args.cpu_seconds)
+    res[stuck] = {"error": "not finished within --extras-timeout %.0f s; stopped" %
+                  args.extras_timeout}
     if rank == 0:
         print(json.dumps(res), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+    sys.stderr.flush()
+    os._exit(0)
 
 
 def _progress(rank, what):
