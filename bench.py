@@ -77,7 +77,7 @@ def parse():
                     help="rehearsal only: put every rank on this GPU")
     ap.add_argument("--no-extra", action="store_true",
                     help="N>1: skip the C4/C5/P2P sub-benchmarks")
-    ap.add_argument("--extras", default="c4,c5,c3_ar,c3_p2p",
+    ap.add_argument("--extras", default="c4,c5,c3_ar,c3_p2p,c3_p2p_push",
                     help="N>1: which sub-benchmarks to run (comma list)")
     ap.add_argument("--extras-timeout", type=float, default=240.0,
                     help="N>1: seconds for all sub-benchmarks together; past it the "
@@ -468,9 +468,11 @@ def main():
         extra = (("c4", lambda: bench_c4(world, rank, dev, min(args.steps, 50), 5)),
                  ("c5", lambda: bench_c5(world, rank, dev, min(args.steps, 50), 5)),
                  ("c3_ar", lambda: bench_c3_ar(world, rank, dev, min(args.steps, 50), 5, n, x)),
-                 # last: the experimental peer-to-peer path
+                 # last: the experimental peer-to-peer paths
                  ("c3_p2p", lambda: bench_c3_p2p(world, rank, dev, min(args.steps, 50), 5,
-                                                 n, x)))
+                                                 n, x)),
+                 ("c3_p2p_push", lambda: bench_c3_p2p(world, rank, dev, min(args.steps, 50),
+                                                      5, n, x, mode="push")))
         # The primary number is measured by now: a sub-benchmark that hangs
         # (a peer mapping refused in a way that blocks, a stuck collective)
         # must not take it down. Past --extras-timeout every rank stops; rank 0
@@ -691,11 +693,15 @@ def bench_c3_ar(world, rank, dev, steps, warmup, n, x):
             "frac_of_xgmi": round(busbw / (153.0 * (world - 1)), 4)}
 
 
-def bench_c3_p2p(world, rank, dev, steps, warmup, n, x):
-    """C3 over xGMI peer mappings instead of RCCL (kungfu_amd/p2p.py): each
-    rank folds its shard straight from every peer's HBM in rank order, then
-    gathers the other shards. Deterministic, so checked bit-exact against a
-    local fold of every rank's regenerated inputs at every N."""
+def bench_c3_p2p(world, rank, dev, steps, warmup, n, x, mode="pull"):
+    """C3 over xGMI peer mappings instead of RCCL (kungfu_amd/p2p.py). pull:
+    each rank folds its shard straight from every peer's HBM in rank order,
+    then gathers the other shards (remote reads, 3 barriers); push: shards
+    are written into the owners' inboxes, folded locally, and written back
+    into every peer's bucket (remote writes, 2 barriers). Deterministic, so
+    checked bit-exact against a local fold of every rank's regenerated inputs
+    at every N — before timing, and again after it on two fresh inputs (no
+    shard may be served stale from a previous step)."""
     from kungfu_amd import ops
     from kungfu_amd.collective import GradBuckets
     from kungfu_amd.p2p import P2PExchange
@@ -703,32 +709,40 @@ def bench_c3_p2p(world, rank, dev, steps, warmup, n, x):
     gb.views[0].copy_(x)
     ex, err = None, ""
     try:
-        ex = P2PExchange(gb.buckets)
+        ex = P2PExchange(gb.buckets, mode=mode)
     except Exception as e:  # e.g. IPC mapping refused on this node
         err = repr(e)[:300]
     if not _agree(ex is not None, dev):
         return {"error": "P2P setup failed on some rank: " + err}
-    ex.all_reduce_(average=True)
-    allx = [torch.randn(n, device=dev, generator=torch.Generator(device=dev).manual_seed(2 * r))
-            for r in range(world)]
-    ok = bool(torch.equal(gb.views[0], ops.bucket_reduce_avg(allx, world)))
-    del allx
-    if not _agree(ok, dev):
+
+    def check(seed):
+        g = lambda r: torch.Generator(device=dev).manual_seed(seed + r)  # noqa: E731
+        gb.views[0].copy_(torch.randn(n, device=dev, generator=g(rank)))
+        ex.all_reduce_(average=True)
+        want = ops.bucket_reduce_avg([torch.randn(n, device=dev, generator=g(r))
+                                      for r in range(world)], world)
+        return _agree(bool(torch.equal(gb.views[0], want)), dev)
+
+    if not check(9000):
         ex.close()
         return {"error": "P2P all-reduce not bit-exact against the rank-order fold"}
     gb.views[0].copy_(x)
     step_s = _timed(lambda: ex.all_reduce_(average=True), steps, warmup, dev, world)
+    after = check(9100) and check(9200)
     ex.close()
     s_bytes = n * 4
     busbw = 2 * (world - 1) / world * s_bytes / step_s / 1e9
-    return {"workload": "C3 via xGMI peer mappings: shard fold from all peers' HBM "
-                        "(HIP k-input, rank order, fused /np) -> gather kernel; "
-                        "3 barriers per step",
+    how = ("shard fold from all peers' HBM (HIP k-input, rank order, fused /np) -> "
+           "gather kernel; 3 barriers per step" if mode == "pull" else
+           "shards written into the owners' inboxes -> local HIP k-input fold (rank "
+           "order, fused /np) -> reduced shard written into every peer; 2 barriers per step")
+    return {"workload": "C3 via xGMI peer mappings (%s): %s" % (mode, how),
             "ms_per_step": round(step_s * 1e3, 4),
             "GiBps_per_gpu": round(s_bytes / step_s / 2**30, 3),
             "busbw_GBps": round(busbw, 2),
             "frac_of_xgmi": round(busbw / (153.0 * (world - 1)), 4),
-            "parity": "bit-exact vs rank-order fold (checked)"}
+            "parity": "bit-exact vs rank-order fold before timing: yes; after timing, "
+                      "two fresh inputs: %s" % ("yes" if after else "NO")}
 
 
 def bench_c5(world, rank, dev, steps, warmup, alpha=0.1):

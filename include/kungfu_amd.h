@@ -303,6 +303,12 @@ int kf_ipc_close(void *base);
  * over xGMI); every offset, length and pointer 16-byte aligned. */
 int kf_gather_segments(void *dst, const void *const *srcs, const size_t *offsets,
                        const size_t *lens, int nseg, void *stream);
+/* One launch copying nseg byte ranges dsts[j][0, lens[j]) <- srcs[j][0,
+ * lens[j]), any of them in a peer's HBM (the push exchange writes shards into
+ * peers' buckets over xGMI); pointers and lengths 16-byte aligned. Blocks
+ * alternate between segments so every link carries traffic at once. */
+int kf_copy_segments(void *const *dsts, const void *const *srcs, const size_t *lens, int nseg,
+                     void *stream);
 const char *kf_p2p_last_error(void);
 
 #pragma GCC visibility pop

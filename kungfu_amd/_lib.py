@@ -52,6 +52,7 @@ EXPORTED = (
     "kf_ipc_import",
     "kf_ipc_close",
     "kf_gather_segments",
+    "kf_copy_segments",
     "kf_p2p_last_error",
 )
 
@@ -187,6 +188,9 @@ def load():
                                        ctypes.POINTER(c_size_t), ctypes.POINTER(c_size_t),
                                        c_int, c_void_p]
     lib.kf_gather_segments.restype = c_int
+    lib.kf_copy_segments.argtypes = [ctypes.POINTER(c_void_p), ctypes.POINTER(c_void_p),
+                                     ctypes.POINTER(c_size_t), c_int, c_void_p]
+    lib.kf_copy_segments.restype = c_int
     lib.kf_p2p_last_error.argtypes = []
     lib.kf_p2p_last_error.restype = ctypes.c_char_p
     _lib = lib

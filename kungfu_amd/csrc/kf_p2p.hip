@@ -59,6 +59,36 @@ __global__ void __launch_bounds__(256) gather_kernel(char *dst, Segs segs, int n
     }
 }
 
+// Per-segment source AND destination (the push exchange writes into peers'
+// HBM over their links): same block interleave and tile as gather_kernel.
+struct CopySegs {
+    const char *src[KF_MAX_SEGMENTS];
+    char *dst[KF_MAX_SEGMENTS];
+    size_t len[KF_MAX_SEGMENTS];  // bytes, multiple of 16
+};
+
+__global__ void __launch_bounds__(256) copy_kernel(CopySegs segs, int nseg)
+{
+    const int s       = static_cast<int>(blockIdx.x % nseg);
+    const size_t nvec = segs.len[s] / 16;
+    const u32x4 *src  = reinterpret_cast<const u32x4 *>(segs.src[s]);
+    u32x4 *out        = reinterpret_cast<u32x4 *>(segs.dst[s]);
+    const size_t tile = 256 * 4;
+    const size_t nblk = gridDim.x / nseg;
+    for (size_t t = blockIdx.x / nseg; t * tile < nvec; t += nblk) {
+        const size_t v0 = t * tile + threadIdx.x;
+        u32x4 r[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (v0 + u * 256 < nvec) r[u] = __builtin_nontemporal_load(src + v0 + u * 256);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (v0 + u * 256 < nvec) __builtin_nontemporal_store(r[u], out + v0 + u * 256);
+        }
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -127,6 +157,37 @@ int kf_gather_segments(void *dst, const void *const *srcs, const size_t *offsets
         static_cast<char *>(dst), segs, nseg);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "gather_kernel launch");
+    return KF_OK;
+}
+
+int kf_copy_segments(void *const *dsts, const void *const *srcs, const size_t *lens, int nseg,
+                     void *stream)
+{
+    if (nseg < 0 || nseg > KF_MAX_SEGMENTS) return KF_ERR_ARG;
+    if (nseg == 0) return KF_OK;
+    if (!dsts || !srcs || !lens) return KF_ERR_ARG;
+    CopySegs segs;
+    size_t maxlen = 0;
+    for (int i = 0; i < nseg; ++i) {
+        if (!srcs[i] || !dsts[i] || (lens[i] % 16) ||
+            (reinterpret_cast<uintptr_t>(srcs[i]) % 16) ||
+            (reinterpret_cast<uintptr_t>(dsts[i]) % 16)) {
+            t_p2p_error = "kf_copy_segments: segments must be 16-byte aligned";
+            return KF_ERR_ARG;
+        }
+        segs.src[i] = static_cast<const char *>(srcs[i]);
+        segs.dst[i] = static_cast<char *>(dsts[i]);
+        segs.len[i] = lens[i];
+        if (lens[i] > maxlen) maxlen = lens[i];
+    }
+    if (maxlen == 0) return KF_OK;
+    const size_t tile = 256 * 4 * 16;
+    size_t bx         = (maxlen + tile - 1) / tile;  // blocks per segment
+    if (bx > (size_t(1) << 16)) bx = size_t(1) << 16;
+    copy_kernel<<<static_cast<unsigned>(bx * nseg), 256, 0, static_cast<hipStream_t>(stream)>>>(
+        segs, nseg);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "copy_kernel launch");
     return KF_OK;
 }
 

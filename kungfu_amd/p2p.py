@@ -24,6 +24,25 @@ world size — unlike a ring/tree collective whose order depends on the shard.
 On a fully connected 8-GPU MI355X node each phase spreads its reads over all 7
 links. Experimental in round 1: bench.py reports it beside the RCCL path
 (``c3_p2p``); DESIGN.md §6.
+
+mode="push" moves the same bytes as remote WRITES instead of reads (posted
+over the fabric, no round trip per request), through a per-bucket inbox of
+`world` shard slots:
+
+  1. scatter   — one kernel writes my shard j of every bucket into rank j's
+                 inbox slot `rank`, for every j != rank (kf_copy_segments);
+  2. barrier   — every push into my inbox has landed;
+  3. reduce    — the k-input fold over (inbox slot j, or my own shard for
+                 j == rank) in rank order, /np fused, into my shard — local
+                 HBM only;
+  4. all-gather — one kernel writes my reduced shard into every peer's
+                 bucket at offset `rank`;
+  5. barrier   — every peer's shard has landed in my bucket.
+
+Two barriers instead of three: the scatter reads only local data, and the
+previous call's last barrier already ordered every peer's fold (its inbox
+reads) before this call's pushes. Same rank-order fold, so the same bits as
+mode="pull". Extra HBM: one inbox per bucket ((world-1)/world of it used).
 """
 import ctypes
 
@@ -35,7 +54,10 @@ from .ops import kungfu_dtype
 
 
 class P2PExchange:
-    def __init__(self, buckets, group=None):
+    def __init__(self, buckets, group=None, mode="pull"):
+        if mode not in ("pull", "push"):
+            raise ValueError("mode must be 'pull' or 'push'")
+        self.mode = mode
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
@@ -46,18 +68,28 @@ class P2PExchange:
                 raise ValueError("P2P buckets must be flat contiguous GPU tensors")
             if b.numel() % self.world or (b.numel() // self.world * b.element_size()) % 16:
                 raise ValueError("bucket does not split into 16-B aligned shards")
+        # push mode: one inbox of `world` shard slots per bucket (slot `rank`
+        # unused: my own shard is read in place)
+        self.inboxes = ([torch.empty_like(b) for b in self.buckets]
+                        if mode == "push" else [])
+        self._bases = {}  # (rank, handle) -> mapped base (one mapping per allocation)
+        self.ptrs = self._share(self.buckets)         # ptrs[j][r]: bucket j of rank r
+        self.inbox_ptrs = self._share(self.inboxes)   # same for the inboxes
+
+    def _share(self, tensors):
+        """Export my tensors, import every peer's: rows[j][r] = address of
+        rank r's tensor j as seen from this process."""
         mine = []
-        for b in self.buckets:
+        for b in tensors:
             h = (ctypes.c_char * 64)()
             off = ctypes.c_size_t()
             _lib.check(self.lib.kf_ipc_export(b.data_ptr(), h, ctypes.byref(off)),
                        "kf_ipc_export")
             mine.append((bytes(h), off.value))
         everyone = [None] * self.world
-        dist.all_gather_object(everyone, mine, group=group)
-        self._bases = {}  # handle -> mapped base (one mapping per allocation)
-        self.ptrs = []    # ptrs[j][r]: bucket j of rank r, as seen from here
-        for j, b in enumerate(self.buckets):
+        dist.all_gather_object(everyone, mine, group=self.group)
+        rows = []
+        for j, b in enumerate(tensors):
             row = []
             for r in range(self.world):
                 if r == self.rank:
@@ -70,7 +102,8 @@ class P2PExchange:
                     _lib.check(self.lib.kf_ipc_import(h, ctypes.byref(base)), "kf_ipc_import")
                     self._bases[key] = base.value
                 row.append(self._bases[key] + off)
-            self.ptrs.append(row)
+            rows.append(row)
+        return rows
 
     def close(self):
         for base in self._bases.values():
@@ -83,6 +116,8 @@ class P2PExchange:
 
     def all_reduce_(self, op="sum", average=False):
         """In place on the buckets given at construction."""
+        if self.mode == "push":
+            return self._all_reduce_push(op, average)
         from .base import OP_NAMES
         world, rank = self.world, self.rank
         s = torch.cuda.current_stream().cuda_stream
@@ -108,5 +143,44 @@ class P2PExchange:
             lens = (ctypes.c_size_t * len(peers))(*[nbytes] * len(peers))
             _lib.check(self.lib.kf_gather_segments(b.data_ptr(), srcs, offs, lens,
                                                    len(peers), s), "kf_gather_segments")
+        self._barrier()
+        return self.buckets
+
+    def _all_reduce_push(self, op, average):
+        from .base import OP_NAMES
+        world, rank = self.world, self.rank
+        s = torch.cuda.current_stream().cuda_stream
+        peers = [r for r in range(world) if r != rank]
+
+        def copy(dsts, srcs, nbytes):
+            _lib.check(self.lib.kf_copy_segments(
+                _lib.ptr_array(dsts), _lib.ptr_array(srcs),
+                (ctypes.c_size_t * len(dsts))(*[nbytes] * len(dsts)), len(dsts), s),
+                "kf_copy_segments")
+
+        for b, ibox in zip(self.buckets, self.inbox_ptrs):
+            nbytes = b.numel() // world * b.element_size()
+            # my shard j -> rank j's inbox slot `rank`
+            copy([ibox[r] + rank * nbytes for r in peers],
+                 [b.data_ptr() + r * nbytes for r in peers], nbytes)
+        self._barrier()
+        for b, ib in zip(self.buckets, self.inboxes):
+            shard = b.numel() // world
+            nbytes = shard * b.element_size()
+            mine = b.data_ptr() + rank * nbytes
+            ins = _lib.ptr_array([mine if r == rank else ib.data_ptr() + r * nbytes
+                                  for r in range(world)])
+            if average:
+                rc = self.lib.kf_bucket_reduce_avg(ins, world, mine, shard,
+                                                   int(kungfu_dtype(b)), world, s)
+            else:
+                rc = self.lib.kf_bucket_reduce(ins, world, mine, shard, int(kungfu_dtype(b)),
+                                               int(OP_NAMES[op]), s)
+            _lib.check(rc, "p2p shard reduce")
+        for b, row in zip(self.buckets, self.ptrs):
+            nbytes = b.numel() // world * b.element_size()
+            # my reduced shard -> every peer's bucket at offset `rank`
+            copy([row[r] + rank * nbytes for r in peers],
+                 [b.data_ptr() + rank * nbytes] * len(peers), nbytes)
         self._barrier()
         return self.buckets

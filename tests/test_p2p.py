@@ -17,7 +17,7 @@ ROOT = os.path.dirname(HERE)
 pytestmark = pytest.mark.gpu
 
 
-def _body(rank, world, port, errq):
+def _body(rank, world, port, errq, mode):
     sys.path[:0] = [ROOT, HERE]
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -29,18 +29,19 @@ def _body(rank, world, port, errq):
         dev = torch.device("cuda:0")
         sizes = [100003, 5000, 777777, 64]
         gb = GradBuckets(sizes, torch.float32, dev, world, n_buckets=4)
-        xs = [[np.random.default_rng(1000 * r + i).standard_normal(n).astype(np.float32)
-               for i, n in enumerate(sizes)] for r in range(world)]
-        for v, x in zip(gb.views, xs[rank]):
-            v.copy_(torch.from_numpy(x))
-        ex = P2PExchange(gb.buckets)
-        ex.all_reduce_(average=True)
-        for i, v in enumerate(gb.views):
-            want = oracle.reduce_avg([xs[r][i] for r in range(world)], "f32", world)
-            assert np.array_equal(v.cpu().numpy(), want), i
+        ex = P2PExchange(gb.buckets, mode=mode)
+        for step in range(3):  # fresh data every step: no stale shard survives
+            xs = [[np.random.default_rng(1000 * r + 100 * step + i).standard_normal(n)
+                   .astype(np.float32) for i, n in enumerate(sizes)] for r in range(world)]
+            for v, x in zip(gb.views, xs[rank]):
+                v.copy_(torch.from_numpy(x))
+            ex.all_reduce_(average=True)
+            for i, v in enumerate(gb.views):
+                want = oracle.reduce_avg([xs[r][i] for r in range(world)], "f32", world)
+                assert np.array_equal(v.cpu().numpy(), want), (step, i)
         # int32 MAX, a second exchange on other buckets, twice (buffer reuse)
         gi = GradBuckets([4099], torch.int32, dev, world, n_buckets=1)
-        ex2 = P2PExchange(gi.buckets)
+        ex2 = P2PExchange(gi.buckets, mode=mode)
         for step in range(2):
             gi.views[0].copy_(torch.arange(4099, dtype=torch.int32, device=dev) * (rank + 1 + step))
             ex2.all_reduce_(op="max")
@@ -53,8 +54,9 @@ def _body(rank, world, port, errq):
         errq.put("rank %d: %s" % (rank, traceback.format_exc()))
 
 
+@pytest.mark.parametrize("mode", ["pull", "push"])
 @pytest.mark.parametrize("world", [2, 3, 4])
-def test_p2p_all_reduce_bit_exact(world):
+def test_p2p_all_reduce_bit_exact(world, mode):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     import socket
@@ -64,7 +66,7 @@ def test_p2p_all_reduce_bit_exact(world):
     s.close()
     ctx = mp.get_context("spawn")
     errq = ctx.SimpleQueue()
-    ps = [ctx.Process(target=_body, args=(r, world, port, errq)) for r in range(world)]
+    ps = [ctx.Process(target=_body, args=(r, world, port, errq, mode)) for r in range(world)]
     for p in ps:
         p.start()
     for p in ps:
