@@ -361,3 +361,32 @@ def body_sync_sgd_overlap(rank, world, use_gpu):
 @pytest.mark.parametrize("world", [2, 3])
 def test_sync_sgd_overlap(world):
     run_world("body_sync_sgd_overlap", world)
+
+
+def body_torch_sync_sgd_sums(rank, world, use_gpu):
+    # kungfu.torch.optimizers.SynchronousSGDOptimizer sums the gradients and
+    # does not divide by np (reference torch/optimizers/sync_sgd.py:12-22);
+    # named_parameters is required as there (sync_sgd.py:31)
+    from kungfu_amd.torch.optimizers import SynchronousSGDOptimizer
+    w = torch.nn.Parameter(torch.zeros(5))
+    opt = SynchronousSGDOptimizer(torch.optim.SGD([w], lr=1.0), [("w", w)])
+    w.grad = torch.full((5,), float(rank + 1))
+    opt.step()
+    # w = 0 - lr * sum_r (r + 1)
+    assert torch.equal(w.detach(), torch.full((5,), -world * (world + 1) / 2.0))
+    w2 = torch.nn.Parameter(torch.zeros(3))
+    opt2 = SynchronousSGDOptimizer(torch.optim.SGD([w2], lr=1.0), [("w2", w2)], op="max")
+    w2.grad = torch.full((3,), float(rank))
+    opt2.step()
+    assert torch.equal(w2.detach(), torch.full((3,), -(world - 1.0)))
+    try:
+        SynchronousSGDOptimizer(torch.optim.SGD([w], lr=1.0))
+    except TypeError:
+        pass
+    else:
+        raise AssertionError("named_parameters must be required")
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_torch_sync_sgd_sums_like_reference(world):
+    run_world("body_torch_sync_sgd_sums", world)
