@@ -77,7 +77,7 @@ def parse():
                     help="rehearsal only: put every rank on this GPU")
     ap.add_argument("--no-extra", action="store_true",
                     help="N>1: skip the C4/C5/P2P sub-benchmarks")
-    ap.add_argument("--extras", default="c4,c5,c3_ar,c3_p2p,c3_p2p_push",
+    ap.add_argument("--extras", default="c4,c5,c3_ar,c3_p2p,c3_p2p_push,c3_p2p_hostbar",
                     help="N>1: which sub-benchmarks to run (comma list)")
     ap.add_argument("--extras-timeout", type=float, default=240.0,
                     help="N>1: seconds for all sub-benchmarks together; past it the "
@@ -472,7 +472,9 @@ def main():
                  ("c3_p2p", lambda: bench_c3_p2p(world, rank, dev, min(args.steps, 50), 5,
                                                  n, x)),
                  ("c3_p2p_push", lambda: bench_c3_p2p(world, rank, dev, min(args.steps, 50),
-                                                      5, n, x, mode="push")))
+                                                      5, n, x, mode="push")),
+                 ("c3_p2p_hostbar", lambda: bench_c3_p2p(world, rank, dev, min(args.steps, 50),
+                                                         5, n, x, barrier="host")))
         # The primary number is measured by now: a sub-benchmark that hangs
         # (a peer mapping refused in a way that blocks, a stuck collective)
         # must not take it down. Past --extras-timeout every rank stops; rank 0
@@ -693,7 +695,7 @@ def bench_c3_ar(world, rank, dev, steps, warmup, n, x):
             "frac_of_xgmi": round(busbw / (153.0 * (world - 1)), 4)}
 
 
-def bench_c3_p2p(world, rank, dev, steps, warmup, n, x, mode="pull"):
+def bench_c3_p2p(world, rank, dev, steps, warmup, n, x, mode="pull", barrier="device"):
     """C3 over xGMI peer mappings instead of RCCL (kungfu_amd/p2p.py). pull:
     each rank folds its shard straight from every peer's HBM in rank order,
     then gathers the other shards (remote reads, 3 barriers); push: shards
@@ -709,7 +711,7 @@ def bench_c3_p2p(world, rank, dev, steps, warmup, n, x, mode="pull"):
     gb.views[0].copy_(x)
     ex, err = None, ""
     try:
-        ex = P2PExchange(gb.buckets, mode=mode)
+        ex = P2PExchange(gb.buckets, mode=mode, barrier=barrier, timeout_s=5.0)
     except Exception as e:  # e.g. IPC mapping refused on this node
         err = repr(e)[:300]
     if not _agree(ex is not None, dev):
@@ -724,11 +726,14 @@ def bench_c3_p2p(world, rank, dev, steps, warmup, n, x, mode="pull"):
         return _agree(bool(torch.equal(gb.views[0], want)), dev)
 
     if not check(9000):
+        st = ex.status()
         ex.close()
-        return {"error": "P2P all-reduce not bit-exact against the rank-order fold"}
+        return {"error": "P2P all-reduce not bit-exact against the rank-order fold"
+                         + (" (device barrier status %d)" % st if st else "")}
     gb.views[0].copy_(x)
     step_s = _timed(lambda: ex.all_reduce_(average=True), steps, warmup, dev, world)
     after = check(9100) and check(9200)
+    st = ex.status()
     ex.close()
     s_bytes = n * 4
     busbw = 2 * (world - 1) / world * s_bytes / step_s / 1e9
@@ -736,7 +741,11 @@ def bench_c3_p2p(world, rank, dev, steps, warmup, n, x, mode="pull"):
            "gather kernel; 3 barriers per step" if mode == "pull" else
            "shards written into the owners' inboxes -> local HIP k-input fold (rank "
            "order, fused /np) -> reduced shard written into every peer; 2 barriers per step")
+    how += ("; barriers on the device (kf_peer_barrier: epoch stores into the peers' "
+            "signal words over xGMI, bounded spin, no host sync)" if barrier == "device" else
+            "; barriers on the host (torch.cuda.synchronize + dist.barrier)")
     return {"workload": "C3 via xGMI peer mappings (%s): %s" % (mode, how),
+            "barrier": barrier, "barrier_status": st,
             "ms_per_step": round(step_s * 1e3, 4),
             "GiBps_per_gpu": round(s_bytes / step_s / 2**30, 3),
             "busbw_GBps": round(busbw, 2),

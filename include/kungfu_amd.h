@@ -107,6 +107,7 @@ enum KF_Status {
     KF_ERR_NO_DEVICE   = 5, /* no usable gfx950 device                */
     KF_ERR_IO          = 6, /* socket read/write failed               */
     KF_ERR_PROTO       = 7, /* rchannel framing/length/token mismatch  */
+    KF_ERR_TIMEOUT     = 8, /* a device-side peer barrier gave up      */
 };
 
 /* Largest k accepted by kf_bucket_reduce*. */
@@ -309,6 +310,25 @@ int kf_gather_segments(void *dst, const void *const *srcs, const size_t *offsets
  * alternate between segments so every link carries traffic at once. */
 int kf_copy_segments(void *const *dsts, const void *const *srcs, const size_t *lens, int nseg,
                      void *stream);
+/* Signal words for the device-side peer barrier: nwords zeroed 64-bit
+ * words. host == 0: fine-grained, uncached device memory, exportable with
+ * kf_ipc_export (every peer stores its arrival into it over xGMI); host == 1:
+ * page-locked host memory the device can store into (the barrier's status
+ * word, readable by the host without a sync). */
+int kf_signal_alloc(size_t nwords, int host, void **ptr);
+int kf_signal_free(void *ptr, int host);
+/* Device-side barrier of `world` GPUs of one node, enqueued on `stream` (no
+ * host round trip, no host sync): one 64-lane workgroup stores `epoch` into
+ * word `rank` of every peer's signal array sigs[r] (system scope, over
+ * xGMI), then waits until every word r != rank of its own array sigs[rank]
+ * holds >= epoch. Stream order makes the work queued before it visible to the
+ * peers (end-of-kernel release) and the work queued after it start after
+ * every peer's arrival. Bounded: after timeout_us it stops waiting and stores
+ * KF_ERR_TIMEOUT into status[0] (a host == 1 signal word), so a missing peer
+ * cannot leave a wave spinning. epoch grows by one per barrier on every rank;
+ * world <= 64. */
+int kf_peer_barrier(void *const *sigs, int world, int rank, uint64_t epoch,
+                    uint32_t timeout_us, void *status, void *stream);
 const char *kf_p2p_last_error(void);
 
 #pragma GCC visibility pop

@@ -53,6 +53,9 @@ EXPORTED = (
     "kf_ipc_close",
     "kf_gather_segments",
     "kf_copy_segments",
+    "kf_signal_alloc",
+    "kf_signal_free",
+    "kf_peer_barrier",
     "kf_p2p_last_error",
 )
 
@@ -65,6 +68,7 @@ STATUS = {
     5: "KF_ERR_NO_DEVICE",
     6: "KF_ERR_IO",
     7: "KF_ERR_PROTO",
+    8: "KF_ERR_TIMEOUT",
 }
 
 MAX_INPUTS = 16
@@ -191,6 +195,13 @@ def load():
     lib.kf_copy_segments.argtypes = [ctypes.POINTER(c_void_p), ctypes.POINTER(c_void_p),
                                      ctypes.POINTER(c_size_t), c_int, c_void_p]
     lib.kf_copy_segments.restype = c_int
+    lib.kf_signal_alloc.argtypes = [c_size_t, c_int, ctypes.POINTER(c_void_p)]
+    lib.kf_signal_alloc.restype = c_int
+    lib.kf_signal_free.argtypes = [c_void_p, c_int]
+    lib.kf_signal_free.restype = c_int
+    lib.kf_peer_barrier.argtypes = [ctypes.POINTER(c_void_p), c_int, c_int, ctypes.c_uint64,
+                                    ctypes.c_uint32, c_void_p, c_void_p]
+    lib.kf_peer_barrier.restype = c_int
     lib.kf_p2p_last_error.argtypes = []
     lib.kf_p2p_last_error.restype = ctypes.c_char_p
     _lib = lib

@@ -8,6 +8,13 @@
 // the other shards from their owners with kf_gather_segments. On MI355X every
 // GPU has a direct xGMI link to each of the 7 others, so both phases spread
 // their reads over all links at once.
+//
+// Between the phases every rank must know that its peers are done. The host
+// way (sync + dist.barrier) costs a round trip through the host and RCCL per
+// phase; kf_peer_barrier does it on the device instead, in stream order: one
+// workgroup stores the barrier's epoch into each peer's signal array over
+// xGMI and spins on its own (fine-grained, uncached) array until every peer
+// has arrived, with a wall-clock bound so that no wave can spin forever.
 #include <hip/hip_runtime.h>
 
 #include <cstring>
@@ -86,6 +93,38 @@ __global__ void __launch_bounds__(256) copy_kernel(CopySegs segs, int nseg)
         for (int u = 0; u < 4; ++u) {
             if (v0 + u * 256 < nvec) __builtin_nontemporal_store(r[u], out + v0 + u * 256);
         }
+    }
+}
+
+struct PeerSigs {
+    unsigned long long *p[64];  // p[r]: rank r's signal array, as mapped here
+};
+
+// One 64-lane workgroup. Lane r (r != rank, r < world) first stores `epoch`
+// into word `rank` of rank r's array (a posted write over xGMI), then waits
+// for word r of this rank's own array to reach `epoch`. The release store at
+// system scope orders it after every store of this kernel; the work queued
+// before the barrier on this stream has already been released at its kernel
+// end. The acquire loads bypass the caches (uncached memory, system scope).
+// s_memrealtime ticks at the device's wall-clock rate; past `limit` ticks the
+// lane stops and records KF_ERR_TIMEOUT in the host-visible status word.
+__global__ void __launch_bounds__(64) peer_barrier_kernel(PeerSigs sigs, int world, int rank,
+                                                          unsigned long long epoch,
+                                                          unsigned long long limit,
+                                                          unsigned long long *status)
+{
+    const int r = static_cast<int>(threadIdx.x);
+    if (r >= world || r == rank) return;
+    __hip_atomic_store(sigs.p[r] + rank, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    unsigned long long *mine = sigs.p[rank] + r;
+    const unsigned long long t0 = wall_clock64();
+    while (__hip_atomic_load(mine, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
+        if (wall_clock64() - t0 > limit) {
+            __hip_atomic_store(status, static_cast<unsigned long long>(KF_ERR_TIMEOUT),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            return;
+        }
+        __builtin_amdgcn_s_sleep(2);
     }
 }
 
@@ -188,6 +227,74 @@ int kf_copy_segments(void *const *dsts, const void *const *srcs, const size_t *l
         segs, nseg);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "copy_kernel launch");
+    return KF_OK;
+}
+
+int kf_signal_alloc(size_t nwords, int host, void **ptr)
+{
+    if (!ptr || nwords == 0) return KF_ERR_ARG;
+    *ptr            = nullptr;
+    const size_t sz = nwords * sizeof(unsigned long long);
+    hipError_t e;
+    if (host) {
+        e = hipHostMalloc(ptr, sz, hipHostMallocMapped | hipHostMallocCoherent);
+        if (e != hipSuccess) return hip_fail(e, "hipHostMalloc(signal)");
+        std::memset(*ptr, 0, sz);
+        return KF_OK;
+    }
+    // uncached fine-grained device memory: peers' stores land in HBM, the
+    // spinning loads never hit a stale cache line
+    e = hipExtMallocWithFlags(ptr, sz, hipDeviceMallocUncached);
+    if (e != hipSuccess) return hip_fail(e, "hipExtMallocWithFlags(uncached signal)");
+    e = hipMemset(*ptr, 0, sz);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess) {
+        (void)hipFree(*ptr);
+        *ptr = nullptr;
+        return hip_fail(e, "hipMemset(signal)");
+    }
+    return KF_OK;
+}
+
+int kf_signal_free(void *ptr, int host)
+{
+    if (!ptr) return KF_ERR_ARG;
+    hipError_t e = host ? hipHostFree(ptr) : hipFree(ptr);
+    if (e != hipSuccess) return hip_fail(e, "signal free");
+    return KF_OK;
+}
+
+int kf_peer_barrier(void *const *sigs, int world, int rank, uint64_t epoch, uint32_t timeout_us,
+                    void *status, void *stream)
+{
+    if (!sigs || !status || world < 1 || world > 64 || rank < 0 || rank >= world) {
+        t_p2p_error = "kf_peer_barrier: bad arguments";
+        return KF_ERR_ARG;
+    }
+    if (world == 1) return KF_OK;
+    PeerSigs ps;
+    for (int r = 0; r < world; ++r) {
+        if (!sigs[r] || (reinterpret_cast<uintptr_t>(sigs[r]) % 8)) {
+            t_p2p_error = "kf_peer_barrier: signal arrays must be non-null, 8-byte aligned";
+            return KF_ERR_ARG;
+        }
+        ps.p[r] = static_cast<unsigned long long *>(sigs[r]);
+    }
+    static thread_local int khz = 0;  // wall-clock rate, kHz (100 MHz on MI355X)
+    if (khz == 0) {
+        int dev      = 0;
+        hipError_t e = hipGetDevice(&dev);
+        if (e == hipSuccess) e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
+        if (e != hipSuccess) return hip_fail(e, "hipDeviceAttributeWallClockRate");
+        if (khz <= 0) khz = 100000;
+    }
+    const unsigned long long limit =
+        static_cast<unsigned long long>(timeout_us) * static_cast<unsigned long long>(khz) / 1000;
+    peer_barrier_kernel<<<1, 64, 0, static_cast<hipStream_t>(stream)>>>(
+        ps, world, rank, static_cast<unsigned long long>(epoch), limit,
+        static_cast<unsigned long long *>(status));
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "peer_barrier_kernel launch");
     return KF_OK;
 }
 

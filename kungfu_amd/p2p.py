@@ -43,6 +43,16 @@ Two barriers instead of three: the scatter reads only local data, and the
 previous call's last barrier already ordered every peer's fold (its inbox
 reads) before this call's pushes. Same rank-order fold, so the same bits as
 mode="pull". Extra HBM: one inbox per bucket ((world-1)/world of it used).
+
+barrier="device" (default) runs every barrier on the GPU, in stream order
+(kf_peer_barrier): one workgroup stores the barrier's epoch into each peer's
+signal array over xGMI (fine-grained, uncached memory mapped like the
+buckets) and spins on its own until every peer has arrived. No host sync and
+no RCCL round trip, so a whole all-reduce is queued without blocking the host.
+The wait is bounded (timeout_s): a peer that never arrives makes the barrier
+record KF_ERR_TIMEOUT in a host-visible status word, which the next call (or
+check()) raises. barrier="host" is the torch.cuda.synchronize() +
+dist.barrier() of the first version, kept for comparison.
 """
 import ctypes
 
@@ -54,10 +64,14 @@ from .ops import kungfu_dtype
 
 
 class P2PExchange:
-    def __init__(self, buckets, group=None, mode="pull"):
+    def __init__(self, buckets, group=None, mode="pull", barrier="device", timeout_s=10.0):
         if mode not in ("pull", "push"):
             raise ValueError("mode must be 'pull' or 'push'")
+        if barrier not in ("device", "host"):
+            raise ValueError("barrier must be 'device' or 'host'")
         self.mode = mode
+        self.barrier = barrier
+        self.timeout_us = int(timeout_s * 1e6)
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
@@ -73,27 +87,35 @@ class P2PExchange:
         self.inboxes = ([torch.empty_like(b) for b in self.buckets]
                         if mode == "push" else [])
         self._bases = {}  # (rank, handle) -> mapped base (one mapping per allocation)
-        self.ptrs = self._share(self.buckets)         # ptrs[j][r]: bucket j of rank r
-        self.inbox_ptrs = self._share(self.inboxes)   # same for the inboxes
+        self.ptrs = self._share([b.data_ptr() for b in self.buckets])  # ptrs[j][r]: bucket j of rank r
+        self.inbox_ptrs = self._share([b.data_ptr() for b in self.inboxes])  # same for inboxes
+        self.epoch = 0
+        self._sig = self._status = None
+        if barrier == "device":
+            sig, st = ctypes.c_void_p(), ctypes.c_void_p()
+            _lib.check(self.lib.kf_signal_alloc(64, 0, ctypes.byref(sig)), "kf_signal_alloc")
+            self._sig = sig.value
+            _lib.check(self.lib.kf_signal_alloc(1, 1, ctypes.byref(st)), "kf_signal_alloc")
+            self._status = st.value
+            self.sig_ptrs = _lib.ptr_array(self._share([self._sig])[0])
 
-    def _share(self, tensors):
-        """Export my tensors, import every peer's: rows[j][r] = address of
-        rank r's tensor j as seen from this process."""
+    def _share(self, ptrs):
+        """Export my allocations, import every peer's: rows[j][r] = address of
+        rank r's buffer j as seen from this process."""
         mine = []
-        for b in tensors:
+        for p in ptrs:
             h = (ctypes.c_char * 64)()
             off = ctypes.c_size_t()
-            _lib.check(self.lib.kf_ipc_export(b.data_ptr(), h, ctypes.byref(off)),
-                       "kf_ipc_export")
+            _lib.check(self.lib.kf_ipc_export(p, h, ctypes.byref(off)), "kf_ipc_export")
             mine.append((bytes(h), off.value))
         everyone = [None] * self.world
         dist.all_gather_object(everyone, mine, group=self.group)
         rows = []
-        for j, b in enumerate(tensors):
+        for j, p in enumerate(ptrs):
             row = []
             for r in range(self.world):
                 if r == self.rank:
-                    row.append(b.data_ptr())
+                    row.append(p)
                     continue
                 h, off = everyone[r][j]
                 key = (r, h)
@@ -106,16 +128,44 @@ class P2PExchange:
         return rows
 
     def close(self):
+        torch.cuda.synchronize()
         for base in self._bases.values():
             self.lib.kf_ipc_close(base)
         self._bases = {}
+        if self._sig is not None:
+            # every peer's store into my array landed before my last barrier
+            # returned, and no peer reads it: free once my stream is idle
+            self.lib.kf_signal_free(self._sig, 0)
+            self.lib.kf_signal_free(self._status, 1)
+            self._sig = self._status = None
+
+    def status(self):
+        """KF_OK, or KF_ERR_TIMEOUT once a device barrier gave up (no sync)."""
+        if self._status is None:
+            return 0
+        return ctypes.c_uint64.from_address(self._status).value
+
+    def check(self):
+        st = self.status()
+        if st:
+            raise _lib.KungFuAMDError("P2P device barrier: %s after %.1f s (a peer never "
+                                      "arrived)" % (_lib.STATUS.get(st, st),
+                                                    self.timeout_us / 1e6))
 
     def _barrier(self):
-        torch.cuda.synchronize()
-        dist.barrier(group=self.group)
+        if self.barrier == "host":
+            torch.cuda.synchronize()
+            dist.barrier(group=self.group)
+            return
+        self.epoch += 1
+        s = torch.cuda.current_stream().cuda_stream
+        _lib.check(self.lib.kf_peer_barrier(self.sig_ptrs, self.world, self.rank, self.epoch,
+                                            self.timeout_us, self._status, s),
+                   "kf_peer_barrier")
 
     def all_reduce_(self, op="sum", average=False):
         """In place on the buckets given at construction."""
+        self.check()
         if self.mode == "push":
             return self._all_reduce_push(op, average)
         from .base import OP_NAMES

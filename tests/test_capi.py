@@ -137,6 +137,24 @@ def test_peers_fold_arg_errors(lib):
     assert lib.kf_bucket_reduce_peers(arr, 2, 8, 16, 0x20408, 0, -1, None) == 3
 
 
+def test_peer_barrier_arg_errors(lib):
+    # kf_peer_barrier / kf_signal_alloc: argument checks before any HIP call
+    import ctypes
+    from kungfu_amd import _lib
+    sigs = _lib.ptr_array([8, 16])
+    st = ctypes.c_void_p(8)
+    assert lib.kf_peer_barrier(sigs, 1, 0, 1, 1000, st, None) == 0  # world 1: nothing
+    assert lib.kf_peer_barrier(sigs, 0, 0, 1, 1000, st, None) == 3
+    assert lib.kf_peer_barrier(sigs, 65, 0, 1, 1000, st, None) == 3
+    assert lib.kf_peer_barrier(sigs, 2, 2, 1, 1000, st, None) == 3  # rank out of range
+    assert lib.kf_peer_barrier(sigs, 2, 0, 1, 1000, None, None) == 3  # no status word
+    assert lib.kf_peer_barrier(_lib.ptr_array([8, 0]), 2, 0, 1, 1000, st, None) == 3
+    assert lib.kf_peer_barrier(_lib.ptr_array([8, 12]), 2, 0, 1, 1000, st, None) == 3
+    assert lib.kf_signal_alloc(0, 0, ctypes.byref(ctypes.c_void_p())) == 3
+    assert lib.kf_signal_alloc(4, 0, None) == 3
+    assert lib.kf_signal_free(None, 0) == 3
+
+
 def test_go_overlay_binds_declared_symbols():
     # go/kungfu/base/*.go (the cgo drop-in, compiled nowhere here: no Go
     # toolchain) may only call C names the header declares

@@ -17,7 +17,7 @@ ROOT = os.path.dirname(HERE)
 pytestmark = pytest.mark.gpu
 
 
-def _body(rank, world, port, errq, mode):
+def _body(rank, world, port, errq, mode, barrier="device"):
     sys.path[:0] = [ROOT, HERE]
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -29,7 +29,7 @@ def _body(rank, world, port, errq, mode):
         dev = torch.device("cuda:0")
         sizes = [100003, 5000, 777777, 64]
         gb = GradBuckets(sizes, torch.float32, dev, world, n_buckets=4)
-        ex = P2PExchange(gb.buckets, mode=mode)
+        ex = P2PExchange(gb.buckets, mode=mode, barrier=barrier)
         for step in range(3):  # fresh data every step: no stale shard survives
             xs = [[np.random.default_rng(1000 * r + 100 * step + i).standard_normal(n)
                    .astype(np.float32) for i, n in enumerate(sizes)] for r in range(world)]
@@ -41,7 +41,7 @@ def _body(rank, world, port, errq, mode):
                 assert np.array_equal(v.cpu().numpy(), want), (step, i)
         # int32 MAX, a second exchange on other buckets, twice (buffer reuse)
         gi = GradBuckets([4099], torch.int32, dev, world, n_buckets=1)
-        ex2 = P2PExchange(gi.buckets, mode=mode)
+        ex2 = P2PExchange(gi.buckets, mode=mode, barrier=barrier)
         for step in range(2):
             gi.views[0].copy_(torch.arange(4099, dtype=torch.int32, device=dev) * (rank + 1 + step))
             ex2.all_reduce_(op="max")
@@ -54,11 +54,7 @@ def _body(rank, world, port, errq, mode):
         errq.put("rank %d: %s" % (rank, traceback.format_exc()))
 
 
-@pytest.mark.parametrize("mode", ["pull", "push"])
-@pytest.mark.parametrize("world", [2, 3, 4])
-def test_p2p_all_reduce_bit_exact(world, mode):
-    if not torch.cuda.is_available():
-        pytest.skip("no GPU")
+def _run(target, world, *args):
     import socket
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -66,7 +62,7 @@ def test_p2p_all_reduce_bit_exact(world, mode):
     s.close()
     ctx = mp.get_context("spawn")
     errq = ctx.SimpleQueue()
-    ps = [ctx.Process(target=_body, args=(r, world, port, errq, mode)) for r in range(world)]
+    ps = [ctx.Process(target=target, args=(r, world, port, errq) + args) for r in range(world)]
     for p in ps:
         p.start()
     for p in ps:
@@ -76,3 +72,49 @@ def test_p2p_all_reduce_bit_exact(world, mode):
         errs.append(errq.get())
     assert not errs, "\n".join(errs)
     assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+
+
+@pytest.mark.parametrize("barrier", ["device", "host"])
+@pytest.mark.parametrize("mode", ["pull", "push"])
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_p2p_all_reduce_bit_exact(world, mode, barrier):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _run(_body, world, mode, barrier)
+
+
+def _timeout_body(rank, world, port, errq):
+    sys.path[:0] = [ROOT, HERE]
+    import time
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from kungfu_amd._lib import KungFuAMDError
+        from kungfu_amd.collective import GradBuckets
+        from kungfu_amd.p2p import P2PExchange
+        dev = torch.device("cuda:0")
+        gb = GradBuckets([4096], torch.float32, dev, world, n_buckets=1)
+        ex = P2PExchange(gb.buckets, timeout_s=0.2)
+        if rank == 0:
+            # rank 1 never joins: the device barrier must give up on its own
+            t0 = time.perf_counter()
+            ex.all_reduce_()
+            torch.cuda.synchronize()
+            assert time.perf_counter() - t0 < 5.0
+            assert ex.status() == 8  # KF_ERR_TIMEOUT
+            with pytest.raises(KungFuAMDError):
+                ex.all_reduce_()
+        dist.barrier()
+        ex.close()
+        dist.destroy_process_group()
+    except Exception:
+        errq.put("rank %d: %s" % (rank, traceback.format_exc()))
+
+
+def test_p2p_device_barrier_times_out():
+    """A peer that never arrives: the bounded wait ends, the status word says
+    KF_ERR_TIMEOUT, the next call raises (no wave left spinning)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _run(_timeout_body, 2)
