@@ -234,3 +234,64 @@ class P2PExchange:
                  [b.data_ptr() + rank * nbytes] * len(peers), nbytes)
         self._barrier()
         return self.buckets
+
+
+class PeerExchange:
+    """The optimizers' exchange interface (``all_reduce_(buckets, op, average)``,
+    ``sma_(buckets, alpha)``, ``world``; see collective.Exchange) over
+    P2PExchange, so ``SynchronousSGDOptimizer(opt, exchange=PeerExchange())``
+    and ``SynchronousAveragingOptimizer(...)`` reduce over xGMI peer mappings
+    instead of RCCL.
+
+    The optimizers hand over the same persistent buckets every step
+    (collective.GradBuckets), so each distinct bucket list is mapped once (a
+    collective call: every rank meets the same lists in the same order) and
+    reused. Results are the rank-order fold, bit-identical at every world
+    size. SMA sums into a persistent workspace copy of the variables, then
+    runs the fused blend (sma_sgd.py:60-65)."""
+
+    def __init__(self, group=None, mode="pull", barrier="device", timeout_s=10.0):
+        from .collective import HipEpilogue
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.kw = dict(mode=mode, barrier=barrier, timeout_s=timeout_s)
+        self.epilogue = HipEpilogue()
+        self._ex = {}
+        self._sums = {}
+
+    def _get(self, buckets):
+        key = tuple((b.data_ptr(), b.numel(), b.dtype) for b in buckets)
+        ex = self._ex.get(key)
+        if ex is None:
+            ex = P2PExchange(buckets, group=self.group, **self.kw)
+            self._ex[key] = ex
+        return ex
+
+    def all_reduce_(self, buckets, op="sum", average=False, coalesce=True):
+        buckets = list(buckets)
+        if average and op != "sum":
+            raise ValueError("average requires op='sum'")
+        if self.world > 1:
+            self._get(buckets).all_reduce_(op=op, average=average)
+        return buckets
+
+    def sma_(self, buckets, alpha):
+        buckets = list(buckets)
+        key = tuple(b.data_ptr() for b in buckets)
+        sums = self._sums.get(key)
+        if sums is None:
+            sums = [torch.empty_like(b) for b in buckets]
+            self._sums[key] = sums
+        for s, b in zip(sums, buckets):
+            s.copy_(b)
+        if self.world > 1:
+            self._get(sums).all_reduce_(op="sum")
+        for b, s in zip(buckets, sums):
+            self.epilogue.sma_blend_(b, s, self.world, alpha)
+        return buckets
+
+    def close(self):
+        for ex in self._ex.values():
+            ex.close()
+        self._ex = {}

@@ -118,3 +118,84 @@ def test_p2p_device_barrier_times_out():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     _run(_timeout_body, 2)
+
+
+def _opt_body(rank, world, port, errq):
+    """SynchronousSGDOptimizer / SynchronousAveragingOptimizer over the P2P
+    exchange: rank-order sum / np (S-SGD) and the SMA blend, bit-exact
+    against the same arithmetic done locally on every rank's regenerated
+    gradients / variables."""
+    sys.path[:0] = [ROOT, HERE]
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from kungfu_amd import ops
+        from kungfu_amd.optimizers import (SynchronousAveragingOptimizer,
+                                           SynchronousSGDOptimizer)
+        from kungfu_amd.p2p import PeerExchange
+        dev = torch.device("cuda:0")
+
+        def model(seed):
+            torch.manual_seed(seed)
+            return torch.nn.Sequential(torch.nn.Linear(33, 65), torch.nn.Tanh(),
+                                       torch.nn.Linear(65, 7)).to(dev)
+
+        def loss(m, r, step):
+            g = torch.Generator(device=dev).manual_seed(100 * step + r)
+            return (m(torch.randn(16, 33, device=dev, generator=g)) ** 2).mean()
+
+        for mode in ("pull", "push"):
+            ex = PeerExchange(mode=mode)
+            m = model(0)
+            opt = SynchronousSGDOptimizer(torch.optim.SGD(m.parameters(), lr=0.1),
+                                          named_parameters=m.named_parameters(), exchange=ex)
+            for step in range(3):
+                snap = [p.detach().clone() for p in m.parameters()]
+                grads = []
+                for r in range(world):
+                    mr = model(0)
+                    with torch.no_grad():
+                        for a, b in zip(mr.parameters(), snap):
+                            a.copy_(b)
+                    loss(mr, r, step).backward()
+                    grads.append([p.grad.detach().clone() for p in mr.parameters()])
+                opt.zero_grad()
+                loss(m, rank, step).backward()
+                opt.step()
+                for j, p in enumerate(m.parameters()):
+                    avg = ops.bucket_reduce_avg([grads[r][j].reshape(-1)
+                                                 for r in range(world)], world).view_as(p)
+                    assert torch.equal(p.grad, avg), (mode, step, j)  # the exchange: exact
+                    assert torch.allclose(p.detach(), snap[j] - 0.1 * avg, rtol=0, atol=1e-6)
+                flat = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu()
+                allf = [torch.empty_like(flat) for _ in range(world)]
+                dist.all_gather(allf, flat)
+                assert all(torch.equal(f, flat) for f in allf), (mode, step)
+            ex.close()
+
+        ex = PeerExchange()
+        alpha = 0.1
+        m = model(rank)
+        allp = [[p.detach().clone() for p in model(r).parameters()] for r in range(world)]
+        opt = SynchronousAveragingOptimizer(torch.optim.SGD(m.parameters(), lr=0.0),
+                                            alpha=alpha, exchange=ex)
+        loss(m, rank, 0).backward()
+        opt.step()
+        for j, p in enumerate(m.parameters()):
+            s = ops.bucket_reduce([allp[r][j].reshape(-1) for r in range(world)])
+            want = allp[rank][j].reshape(-1).clone()
+            ops.sma_blend_(want, s, world, alpha)
+            assert torch.equal(p.detach().reshape(-1), want), j
+        ex.close()
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:
+        errq.put("rank %d: %s" % (rank, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_p2p_optimizers(world):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _run(_opt_body, world)
