@@ -285,6 +285,23 @@ int kf_session_set_host_reduce(kf_session_t *s, kf_host_reduce_fn fn);
 int kf_session_all_reduce(kf_session_t *s, const void *send, void *recv,
                           size_t count, KungFu_Datatype dt, KungFu_Op op,
                           const char *name, void *stream);
+/* GoKungfuAllReduce with done != nil (srcs/go/libkungfu-comm/collective.go:
+ * 34-45, main.go:184-191): queue the all-reduce on the session's worker
+ * thread and return KF_OK at once; done(status, arg) runs on that thread when
+ * it has finished (the reference drops the error, main.go:188; here it is
+ * passed on). Queued all-reduces run one after another in submission order,
+ * so every peer submits the same names in the same order (the rule RCCL has
+ * too; the reference's goroutine per call does not need it). Buffers stay
+ * valid and untouched until done; the name is copied. A synchronous
+ * kf_session_all_reduce first waits for everything queued before it. */
+typedef void (*kf_done_fn)(int status, void *arg);
+int kf_session_all_reduce_async(kf_session_t *s, const void *send, void *recv,
+                                size_t count, KungFu_Datatype dt, KungFu_Op op,
+                                const char *name, void *stream, kf_done_fn done,
+                                void *arg);
+/* Block until every queued all-reduce has finished; the first failure since
+ * the previous wait (its message in kf_session_last_error), else KF_OK. */
+int kf_session_wait_all(kf_session_t *s);
 void kf_session_destroy(kf_session_t *s);
 const char *kf_session_last_error(void);
 

@@ -46,6 +46,8 @@ EXPORTED = (
     "kf_session_set_strategy",
     "kf_session_set_host_reduce",
     "kf_session_all_reduce",
+    "kf_session_all_reduce_async",
+    "kf_session_wait_all",
     "kf_session_destroy",
     "kf_session_last_error",
     "kf_ipc_export",
@@ -72,6 +74,9 @@ STATUS = {
 }
 
 MAX_INPUTS = 16
+
+# kf_done_fn: void (*)(int status, void *arg)
+DONE_FN = ctypes.CFUNCTYPE(None, ctypes.c_int, ctypes.c_void_p)
 
 _lib = None
 
@@ -180,6 +185,12 @@ def load():
     lib.kf_session_all_reduce.restype = c_int
     lib.kf_session_destroy.argtypes = [c_void_p]
     lib.kf_session_destroy.restype = None
+    lib.kf_session_all_reduce_async.argtypes = [c_void_p, c_void_p, c_void_p, c_size_t, c_int,
+                                                c_int, ctypes.c_char_p, c_void_p, DONE_FN,
+                                                c_void_p]
+    lib.kf_session_all_reduce_async.restype = c_int
+    lib.kf_session_wait_all.argtypes = [c_void_p]
+    lib.kf_session_wait_all.restype = c_int
     lib.kf_session_last_error.argtypes = []
     lib.kf_session_last_error.restype = ctypes.c_char_p
     lib.kf_ipc_export.argtypes = [c_void_p, c_void_p, ctypes.POINTER(c_size_t)]

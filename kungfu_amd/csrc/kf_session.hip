@@ -367,6 +367,19 @@ struct SendItem {  // one chunk to every fd in `fds` (the node's successors)
 
 }  // namespace
 
+// One queued kf_session_all_reduce_async call.
+struct AsyncOp {
+    const char *send;
+    char *recv;
+    size_t count;
+    KungFu_Datatype dt;
+    KungFu_Op op;
+    std::string name;
+    void *stream;
+    kf_done_fn done;
+    void *arg;
+};
+
 struct kf_session {
     int rank = 0, size = 1;
     std::string dir;
@@ -400,8 +413,76 @@ struct kf_session {
     int send_rc     = KF_OK;
     std::string send_err;
 
+    // async all-reduces: one worker thread runs them in submission order
+    std::thread aworker;
+    std::mutex amu;
+    std::condition_variable acv, aidle;
+    std::deque<AsyncOp> aq;
+    size_t apending = 0;  // queued + running
+    bool astop      = false;
+    int arc         = KF_OK;  // first failure since the last wait_all
+    std::string aerr;
+
+    void async_loop()
+    {
+        for (;;) {
+            AsyncOp op;
+            {
+                std::unique_lock<std::mutex> l(amu);
+                acv.wait(l, [&] { return astop || !aq.empty(); });
+                if (aq.empty()) return;
+                op = aq.front();
+                aq.pop_front();
+            }
+            t_sess_error.clear();
+            const int rc = all_reduce(op.send, op.recv, op.count, op.dt, op.op, op.name, op.stream);
+            {
+                std::lock_guard<std::mutex> l(amu);
+                if (rc != KF_OK && arc == KF_OK) {
+                    arc  = rc;
+                    aerr = op.name + ": " + t_sess_error;
+                }
+            }
+            if (op.done) op.done(rc, op.arg);
+            {
+                std::lock_guard<std::mutex> l(amu);
+                if (--apending == 0) aidle.notify_all();
+            }
+        }
+    }
+
+    int submit(const AsyncOp &op)
+    {
+        std::lock_guard<std::mutex> l(amu);
+        if (astop) return KF_ERR_ARG;
+        if (!aworker.joinable()) aworker = std::thread([this] { async_loop(); });
+        aq.push_back(op);
+        ++apending;
+        acv.notify_one();
+        return KF_OK;
+    }
+
+    int wait_all()
+    {
+        std::unique_lock<std::mutex> l(amu);
+        aidle.wait(l, [&] { return apending == 0; });
+        const int rc = arc;
+        if (rc != KF_OK) t_sess_error = aerr;
+        arc = KF_OK;
+        aerr.clear();
+        return rc;
+    }
+
     ~kf_session()
     {
+        if (aworker.joinable()) {  // drain the queued all-reduces first
+            {
+                std::lock_guard<std::mutex> l(amu);
+                astop = true;
+            }
+            acv.notify_all();
+            aworker.join();
+        }
         if (sender.joinable()) {
             {
                 std::lock_guard<std::mutex> l(mu);
@@ -965,10 +1046,6 @@ int kf_session::all_reduce(const char *send, char *recv, size_t count, KungFu_Da
     return KF_OK;
 }
 
-extern "C" {
-
-}  // extern "C"
-
 namespace
 {
 kf_session_t *create_session(int rank, std::vector<PeerAddr> peers, const char *sock_dir,
@@ -1082,8 +1159,35 @@ int kf_session_all_reduce(kf_session_t *s, const void *send, void *recv, size_t 
     if (!s || !name || (count > 0 && (!send || !recv))) return KF_ERR_ARG;
     if (dt == KungFu_BOOL || (dt == KungFu_FLOAT16 && op != KungFu_SUM)) return KF_ERR_OP;
     t_sess_error.clear();
+    // after every all-reduce submitted before it (one message order per peer)
+    const int rc = s->wait_all();
+    if (rc != KF_OK) return rc;
     return s->all_reduce(static_cast<const char *>(send), static_cast<char *>(recv), count, dt,
                          op, name, stream);
+}
+
+int kf_session_all_reduce_async(kf_session_t *s, const void *send, void *recv, size_t count,
+                                KungFu_Datatype dt, KungFu_Op op, const char *name, void *stream,
+                                kf_done_fn done, void *arg)
+{
+    if (!s || !name || (count > 0 && (!send || !recv))) return KF_ERR_ARG;
+    if (dt == KungFu_BOOL || (dt == KungFu_FLOAT16 && op != KungFu_SUM)) return KF_ERR_OP;
+    switch (dt) {  // checked here: kungfu_type_size exits on an unknown code
+    case KungFu_UINT8: case KungFu_UINT16: case KungFu_UINT32: case KungFu_UINT64:
+    case KungFu_INT8: case KungFu_INT16: case KungFu_INT32: case KungFu_INT64:
+    case KungFu_FLOAT16: case KungFu_FLOAT: case KungFu_DOUBLE: case KungFu_BFLOAT16: break;
+    default: return KF_ERR_DTYPE;
+    }
+    if (static_cast<unsigned>(op) > KungFu_PROD) return KF_ERR_OP;
+    AsyncOp a{static_cast<const char *>(send), static_cast<char *>(recv), count, dt, op, name,
+              stream, done, arg};
+    return s->submit(a);
+}
+
+int kf_session_wait_all(kf_session_t *s)
+{
+    if (!s) return KF_ERR_ARG;
+    return s->wait_all();
 }
 
 void kf_session_destroy(kf_session_t *s) { delete s; }

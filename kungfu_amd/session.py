@@ -17,6 +17,7 @@ Modes:
             kf_host_reduce_fn signature (bench.py's CPU baseline leg).
 """
 import ctypes
+import threading
 
 from . import _lib
 from .base import OP, OP_NAMES
@@ -64,6 +65,7 @@ class Session:
             _lib.check(self.lib.kf_session_set_strategy(
                 self._h, STRATEGIES[strategy], 1 if hash_method == "NAME" else 0),
                 "kf_session_set_strategy")
+        self._pending = []  # async handles: keep buffers and callbacks alive
         if host_reduce_fn is not None:
             if mode != "host":
                 raise ValueError("host_reduce_fn needs mode='host'")
@@ -80,8 +82,9 @@ class Session:
 
     def close(self):
         if self._h:
-            self.lib.kf_session_destroy(self._h)
+            self.lib.kf_session_destroy(self._h)  # runs what is still queued
             self._h = None
+            self._pending = []
 
     def __del__(self):
         try:
@@ -115,6 +118,65 @@ class Session:
                                             name.encode(), stream)
         _lib.check(rc, "kf_session_all_reduce")
         return recv
+
+    def all_reduce_async(self, send, recv, name, op="sum", callback=None):
+        """Queue an all-reduce and return at once (GoKungfuAllReduce with a
+        done callback, libkungfu-comm/collective.go:34-45): the session's
+        worker thread runs queued all-reduces in submission order, so every
+        peer submits the same names in the same order. ``callback(status)``
+        runs on that thread when the all-reduce is done; ``handle.wait()``
+        blocks until then and raises on failure. send/recv must not be touched
+        before that."""
+        red = OP_NAMES[op] if isinstance(op, str) else OP(op)
+        count, dt, sp = self._meta(send)
+        rcount, rdt, rp = self._meta(recv)
+        if (rcount, rdt) != (count, dt):
+            raise ValueError("send/recv mismatch")
+        stream = None
+        if self.mode == "device":
+            import torch
+            stream = torch.cuda.current_stream(send.device).cuda_stream
+        h = AsyncHandle(send, recv, name, callback)
+        rc = self.lib.kf_session_all_reduce_async(self._h, sp, rp, count, dt, int(red),
+                                                  name.encode(), stream, h._cfn, None)
+        _lib.check(rc, "kf_session_all_reduce_async")
+        self._pending = [p for p in self._pending if not p.done()] + [h]
+        return h
+
+    def wait_all(self):
+        """Block until every queued all-reduce has finished."""
+        rc = self.lib.kf_session_wait_all(self._h)
+        self._pending = [p for p in self._pending if not p.done()]
+        _lib.check(rc, "kf_session_wait_all")
+
+
+class AsyncHandle:
+    """One queued all-reduce (Session.all_reduce_async)."""
+
+    def __init__(self, send, recv, name, callback):
+        self.bufs = (send, recv)
+        self.name = name
+        self.status = None
+        self._cb = callback
+        self._ev = threading.Event()
+        self._cfn = _lib.DONE_FN(self._done)
+
+    def _done(self, status, _arg):
+        self.status = status
+        try:
+            if self._cb is not None:
+                self._cb(status)
+        finally:
+            self._ev.set()
+
+    def done(self):
+        return self._ev.is_set()
+
+    def wait(self, timeout=None):
+        if not self._ev.wait(timeout):
+            raise TimeoutError("all-reduce %r not done" % self.name)
+        _lib.check(self.status, "all-reduce %r" % self.name)
+        return self.bufs[1]
 
 
 def c_reduce_fn(addr):

@@ -339,3 +339,101 @@ def test_session_next_step_message_waits_for_its_call():
     for c, (b, e) in enumerate(parts):
         for step in range(2):
             assert np.array_equal(got[names[c]][step], (x0[step] + x1[step])[b:e])
+
+
+def _async_body(rank, size, sock_dir, mode, errq):
+    """GoKungfuAllReduce with a done callback: several named all-reduces
+    queued at once (ints, an exact-in-fp32 float bucket of 3 chunks, an
+    in-place one), then a synchronous one behind them."""
+    sys.path[:0] = [ROOT, HERE]
+    try:
+        from kungfu_amd.session import Session
+        specs = [("grad/a", "iota", 37), ("grad/b", "c1", (3 << 20) // 4 + 9),
+                 ("grad/c", "iota", 4099)]
+        xs = [inputs(rank, n, kind) for _, kind, n in specs]
+        if mode == "device":
+            import torch
+            dev = torch.device("cuda:0")
+            sends = [torch.from_numpy(x).to(dev) for x in xs]
+            recvs = [torch.zeros_like(t) for t in sends[:2]] + [sends[2]]  # c in place
+            s = Session(rank, size, sock_dir, mode="device")
+        else:
+            sends = [x.copy() for x in xs]
+            recvs = [np.zeros_like(x) for x in xs[:2]] + [sends[2]]
+            s = Session(rank, size, sock_dir, mode="host", host_reduce_fn=oracle_reduce_fn())
+        seen = []
+        hs = [s.all_reduce_async(snd, rcv, name, callback=lambda st, name=name:
+                                 seen.append((name, st)))
+              for (name, _, _), snd, rcv in zip(specs, sends, recvs)]
+        z = inputs(rank, 11, "iota")
+        zr = np.zeros_like(z)
+        if mode == "device":
+            z, zr = torch.from_numpy(z).to(dev), torch.zeros(11, dtype=torch.int32, device=dev)
+        s.all_reduce(z, zr, "after")  # waits for the queued ones first
+        assert all(h.done() for h in hs)
+        outs = [h.wait() for h in hs]
+        s.wait_all()
+        assert [n for n, _ in seen] == [n for n, _, _ in specs]  # submission order
+        assert all(st == 0 for _, st in seen)
+        s.close()
+        if mode == "device":
+            outs = [o.cpu().numpy() for o in outs]
+            zr = zr.cpu().numpy()
+        for (_, kind, n), got in zip(specs, outs):
+            check(rank, size, kind, n, got)
+        assert np.array_equal(zr, np.arange(11, dtype=np.int32) * size)
+    except Exception:
+        errq.put("rank %d: %s" % (rank, traceback.format_exc()))
+
+
+def _run_async(size, mode):
+    ctx = mp.get_context("spawn")
+    errq = ctx.SimpleQueue()
+    with tempfile.TemporaryDirectory() as d:
+        ps = [ctx.Process(target=_async_body, args=(r, size, d, mode, errq))
+              for r in range(size)]
+        for p in ps:
+            p.start()
+        for p in ps:
+            p.join(timeout=300)
+    errs = []
+    while not errq.empty():
+        errs.append(errq.get())
+    assert not errs, "\n".join(errs)
+    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+
+
+@pytest.mark.parametrize("size", [2, 3])
+def test_session_async_host(size):
+    _run_async(size, "host")
+
+
+@pytest.mark.gpu
+def test_session_async_device():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _run_async(3, "device")
+
+
+def test_session_async_arg_errors():
+    import ctypes
+    from kungfu_amd import _lib
+    lib = _lib.load()
+    cb = _lib.DONE_FN(lambda st, arg: None)
+    assert lib.kf_session_all_reduce_async(None, None, None, 0, 0x20408, 0, b"x", None,
+                                           cb, None) == 3
+    assert lib.kf_session_wait_all(None) == 3
+    with tempfile.TemporaryDirectory() as d:
+        from kungfu_amd.session import Session
+        s = Session(0, 1, d, mode="host", host_reduce_fn=oracle_reduce_fn())
+        buf = np.zeros(4, dtype=np.int32)
+        p = buf.ctypes.data
+        assert lib.kf_session_all_reduce_async(s._h, p, p, 4, 0x12345, 0, b"x", None,
+                                               cb, None) == 1  # unknown dtype: no exit
+        assert lib.kf_session_all_reduce_async(s._h, p, p, 4, 0x30108, 0, b"x", None,
+                                               cb, None) == 2  # BOOL
+        assert lib.kf_session_all_reduce_async(s._h, p, p, 4, 0x10408, 7, b"x", None,
+                                               cb, None) == 2  # unknown op
+        s.close()
+    del ctypes
