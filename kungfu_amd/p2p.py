@@ -49,7 +49,8 @@ barrier="device" (default) runs every barrier on the GPU, in stream order
 signal array over xGMI (fine-grained, uncached memory mapped like the
 buckets) and spins on its own until every peer has arrived. No host sync and
 no RCCL round trip, so a whole all-reduce is queued without blocking the host.
-The wait is bounded (timeout_s): a peer that never arrives makes the barrier
+The wait is bounded (timeout_s, 60 s by default: a peer may legitimately
+still be in its forward/backward pass): a peer that never arrives makes the barrier
 record KF_ERR_TIMEOUT in a host-visible status word, which the next call (or
 check()) raises. barrier="host" is the torch.cuda.synchronize() +
 dist.barrier() of the first version, kept for comparison.
@@ -64,7 +65,7 @@ from .ops import kungfu_dtype
 
 
 class P2PExchange:
-    def __init__(self, buckets, group=None, mode="pull", barrier="device", timeout_s=10.0):
+    def __init__(self, buckets, group=None, mode="pull", barrier="device", timeout_s=60.0):
         if mode not in ("pull", "push"):
             raise ValueError("mode must be 'pull' or 'push'")
         if barrier not in ("device", "host"):
@@ -250,7 +251,7 @@ class PeerExchange:
     size. SMA sums into a persistent workspace copy of the variables, then
     runs the fused blend (sma_sgd.py:60-65)."""
 
-    def __init__(self, group=None, mode="pull", barrier="device", timeout_s=10.0):
+    def __init__(self, group=None, mode="pull", barrier="device", timeout_s=60.0):
         from .collective import HipEpilogue
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
