@@ -308,6 +308,13 @@ def body_torch_ops(rank, world, use_gpu):
     assert torch.all(sd["w"] == 0)
     g = ops.all_gather(torch.tensor([rank, rank * 10]))
     assert g.shape == (world, 2) and g[world - 1, 1].item() == (world - 1) * 10
+    # package-level peer queries (kungfu/torch/__init__.py:1-16)
+    import kungfu_amd.torch as kf
+    assert (kf.current_rank(), kf.current_cluster_size()) == (rank, world)
+    assert (kf.current_local_rank(), kf.current_local_size()) == (rank, world)  # one host
+    assert kf.get_cuda_index() == kf.current_local_rank()
+    assert kf.nccl_built() is False
+    kf.run_barrier()
 
 
 @pytest.mark.parametrize("world", [2, 3])
