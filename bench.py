@@ -77,7 +77,8 @@ def parse():
                     help="rehearsal only: put every rank on this GPU")
     ap.add_argument("--no-extra", action="store_true",
                     help="N>1: skip the C4/C5/P2P sub-benchmarks")
-    ap.add_argument("--extras", default="c4,c5,c3_ar,c3_p2p,c3_p2p_push,c3_p2p_hostbar",
+    ap.add_argument("--extras", default="c4,c5,c3_ar,c3_p2p,c3_p2p_push,c3_p2p_hostbar,"
+                                        "c4_p2p,c5_p2p",
                     help="N>1: which sub-benchmarks to run (comma list)")
     ap.add_argument("--extras-timeout", type=float, default=240.0,
                     help="N>1: seconds for all sub-benchmarks together; past it the "
@@ -474,7 +475,11 @@ def main():
                  ("c3_p2p_push", lambda: bench_c3_p2p(world, rank, dev, min(args.steps, 50),
                                                       5, n, x, mode="push")),
                  ("c3_p2p_hostbar", lambda: bench_c3_p2p(world, rank, dev, min(args.steps, 50),
-                                                         5, n, x, barrier="host")))
+                                                         5, n, x, barrier="host")),
+                 ("c4_p2p", lambda: bench_c4(world, rank, dev, min(args.steps, 50), 5,
+                                             exchange="p2p")),
+                 ("c5_p2p", lambda: bench_c5(world, rank, dev, min(args.steps, 50), 5,
+                                             exchange="p2p")))
         # The primary number is measured by now: a sub-benchmark that hangs
         # (a peer mapping refused in a way that blocks, a stuck collective)
         # must not take it down. Past --extras-timeout every rank stops; rank 0
@@ -625,13 +630,24 @@ def _fill(gb, rank_seed, dev, dtype):
         v.copy_(torch.randn(v.numel(), device=dev, generator=g).to(dtype))
 
 
-def bench_c4(world, rank, dev, steps, warmup):
+def _exchange(kind):
+    """rccl: RS -> HIP epilogue -> AG (collective.Exchange); p2p: the xGMI
+    peer-mapped pull exchange with device barriers (p2p.PeerExchange), whose
+    rank-order fold is bit-exact at every N."""
+    if kind == "p2p":
+        from kungfu_amd.p2p import PeerExchange
+        return PeerExchange(timeout_s=5.0)
+    from kungfu_amd.collective import Exchange
+    return Exchange()
+
+
+def bench_c4(world, rank, dev, steps, warmup, exchange="rccl"):
     """C4: ResNet-50 gradient set (214 tensors, 25,583,592 fp32) fused into 16
     buckets (EvenPartition), S-SGD all-reduce."""
     from kungfu_amd import ops
-    from kungfu_amd.collective import Exchange, GradBuckets
+    from kungfu_amd.collective import GradBuckets
     sizes = _models()["resnet50-imagenet"]
-    ex = Exchange()
+    ex = _exchange(exchange)
     gbs = [GradBuckets(sizes, torch.float32, dev, world, n_buckets=16) for _ in range(world)]
     for r, gb in enumerate(gbs):  # every rank's gradients, regenerated locally
         _fill(gb, 500 + r, dev, torch.float32)
@@ -642,19 +658,23 @@ def bench_c4(world, rank, dev, steps, warmup):
     ex.all_reduce_(mine.buckets, average=True)
     ok = True
     for b, w, ab, sp in zip(mine.buckets, want, absums, mine.spans):
-        if world == 2:
+        if world == 2 or exchange == "p2p":
             ok &= bool(torch.equal(b[:sp], w[:sp]))
         else:
             ok &= _within(b[:sp], w[:sp], ab[:sp], world)
     del want, absums
     gbs.clear()
     if not _agree(ok, dev):
-        return {"error": "C4 parity check failed (N=2 bit-exact / N>2 bound)"}
+        return {"error": "C4 parity check failed (N=2 or P2P bit-exact / N>2 bound)"}
     s_bytes = sum(sizes) * 4
     step_s = _timed(lambda: ex.all_reduce_(mine.buckets, average=True), steps, warmup, dev, world)
+    if exchange == "p2p":
+        ex.close()
     busbw = 2 * (world - 1) / world * s_bytes / step_s / 1e9
+    how = ("RCCL RS -> HIP /np -> RCCL AG" if exchange == "rccl" else
+           "xGMI P2P pull: rank-order shard fold from peers' HBM + gather, device barriers")
     return {"workload": "C4: ResNet-50 grads, 25,583,592 fp32 in %d buckets, S-SGD "
-                        "(RCCL RS -> HIP /np -> RCCL AG)" % len(mine.buckets),
+                        "(%s)" % (len(mine.buckets), how),
             "bytes": s_bytes, "ms_per_step": round(step_s * 1e3, 4),
             "GiBps_per_gpu": round(s_bytes / step_s / 2**30, 3),
             "busbw_GBps": round(busbw, 2),
@@ -754,14 +774,14 @@ def bench_c3_p2p(world, rank, dev, steps, warmup, n, x, mode="pull", barrier="de
                       "two fresh inputs: %s" % ("yes" if after else "NO")}
 
 
-def bench_c5(world, rank, dev, steps, warmup, alpha=0.1):
+def bench_c5(world, rank, dev, steps, warmup, alpha=0.1, exchange="rccl"):
     """C5: BERT-base (first 201 tensors of the fake model, 109,483,778
     params) in bf16 with SynchronousAveragingOptimizer semantics (sum, /np,
     alpha-blend), buckets pipelined."""
     from kungfu_amd import ops
-    from kungfu_amd.collective import Exchange, GradBuckets
+    from kungfu_amd.collective import GradBuckets
     sizes = _models()["bert"][:201]
-    ex = Exchange()
+    ex = _exchange(exchange)
     mine = GradBuckets(sizes, torch.bfloat16, dev, world, bucket_bytes=16 << 20)
     _fill(mine, 700 + rank, dev, torch.bfloat16)
     # expected after one SMA step: local fp32 fold of every rank's variables
@@ -779,21 +799,29 @@ def bench_c5(world, rank, dev, steps, warmup, alpha=0.1):
         want = ops.sma_blend_(v0[i].clone(), s, world, alpha)
         absum = sum(gb.buckets[i].float().abs() for gb in others)
         bound = alpha * (world - 1) * 2.0 ** -8 * absum / world + 2 * 2.0 ** -8 * want.float().abs()
-        ok &= bool(((b.float() - want.float()).abs() <= 2 * bound + 1e-30).all())
+        if exchange == "p2p":  # the same k-input bf16 fold (one rounding), rank order
+            ok &= bool(torch.equal(b, want))
+        else:
+            ok &= bool(((b.float() - want.float()).abs() <= 2 * bound + 1e-30).all())
     del others, v0
     if not _agree(ok, dev):
         return {"error": "C5 check failed (outside the bf16 bound)"}
     s_bytes = sum(sizes) * 2
     step_s = _timed(lambda: ex.sma_(mine.buckets, alpha), steps, warmup, dev, world)
+    if exchange == "p2p":
+        ex.close()
     busbw = 2 * (world - 1) / world * s_bytes / step_s / 1e9
+    how = ("RCCL RS -> RCCL AG -> HIP blend" if exchange == "rccl" else
+           "xGMI P2P pull sum, device barriers -> HIP blend")
     return {"workload": "C5: BERT-base 109,483,778 params bf16, SMA alpha=%.2f, %d "
-                        "pipelined buckets (RCCL RS -> RCCL AG -> HIP blend)"
-                        % (alpha, len(mine.buckets)),
+                        "pipelined buckets (%s)" % (alpha, len(mine.buckets), how),
             "bytes": s_bytes, "ms_per_step": round(step_s * 1e3, 4),
             "GiBps_per_gpu": round(s_bytes / step_s / 2**30, 3),
             "busbw_GBps": round(busbw, 2),
             "frac_of_xgmi": round(busbw / (153.0 * (world - 1)), 4),
-            "parity": "bf16 unpinned (DESIGN.md); checked within bound"}
+            "parity": "bf16 unpinned (DESIGN.md); " + (
+                "bit-exact vs the local rank-order fold + blend" if exchange == "p2p"
+                else "checked within bound")}
 
 
 

@@ -65,7 +65,8 @@ from .ops import kungfu_dtype
 
 
 class P2PExchange:
-    def __init__(self, buckets, group=None, mode="pull", barrier="device", timeout_s=60.0):
+    def __init__(self, buckets, group=None, mode="pull", barrier="device", timeout_s=60.0,
+                 coalesce=True):
         if mode not in ("pull", "push"):
             raise ValueError("mode must be 'pull' or 'push'")
         if barrier not in ("device", "host"):
@@ -77,7 +78,13 @@ class P2PExchange:
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.lib = _lib.load()
-        self.buckets = list(buckets)
+        self.given = list(buckets)
+        # buckets that lie back to back in one storage are exchanged as one:
+        # every element's result is the same rank-order fold whichever rank
+        # owns its shard, so the bits do not change, and a run costs one fold
+        # and one gather launch instead of one per bucket
+        from .collective import coalesce_runs
+        self.buckets = coalesce_runs(self.given) if coalesce else list(self.given)
         for b in self.buckets:
             if not b.is_cuda or b.dim() != 1 or not b.is_contiguous():
                 raise ValueError("P2P buckets must be flat contiguous GPU tensors")
@@ -195,7 +202,7 @@ class P2PExchange:
             _lib.check(self.lib.kf_gather_segments(b.data_ptr(), srcs, offs, lens,
                                                    len(peers), s), "kf_gather_segments")
         self._barrier()
-        return self.buckets
+        return self.given
 
     def _all_reduce_push(self, op, average):
         from .base import OP_NAMES
@@ -234,7 +241,7 @@ class P2PExchange:
             copy([row[r] + rank * nbytes for r in peers],
                  [b.data_ptr() + rank * nbytes] * len(peers), nbytes)
         self._barrier()
-        return self.buckets
+        return self.given
 
 
 class PeerExchange:
@@ -278,19 +285,30 @@ class PeerExchange:
         return buckets
 
     def sma_(self, buckets, alpha):
-        buckets = list(buckets)
-        key = tuple(b.data_ptr() for b in buckets)
+        from .collective import coalesce_runs
+        runs = coalesce_runs(list(buckets))  # copy and blend once per run
+        key = tuple(b.data_ptr() for b in runs)
         sums = self._sums.get(key)
         if sums is None:
-            sums = [torch.empty_like(b) for b in buckets]
+            if all(b.dtype == runs[0].dtype and b.device == runs[0].device for b in runs):
+                # one flat workspace laid out like the runs, so the P2P sum
+                # of it is a single run as well
+                flat = torch.empty(sum(b.numel() for b in runs), dtype=runs[0].dtype,
+                                   device=runs[0].device)
+                sums, off = [], 0
+                for b in runs:
+                    sums.append(flat[off:off + b.numel()])
+                    off += b.numel()
+            else:
+                sums = [torch.empty_like(b) for b in runs]
             self._sums[key] = sums
-        for s, b in zip(sums, buckets):
+        for s, b in zip(sums, runs):
             s.copy_(b)
         if self.world > 1:
             self._get(sums).all_reduce_(op="sum")
-        for b, s in zip(buckets, sums):
+        for b, s in zip(runs, sums):
             self.epilogue.sma_blend_(b, s, self.world, alpha)
-        return buckets
+        return list(buckets)
 
     def close(self):
         for ex in self._ex.values():
