@@ -314,3 +314,119 @@ class PeerExchange:
         for ex in self._ex.values():
             ex.close()
         self._ex = {}
+
+
+def _same_host(group=None):
+    """True when every rank of the group runs on this host (the P2P exchange
+    maps peers' HBM through HIP IPC, which only reaches the node's GPUs)."""
+    import socket
+    names = [None] * dist.get_world_size(group)
+    dist.all_gather_object(names, socket.gethostname(), group=group)
+    return len(set(names)) == 1
+
+
+class AutoExchange:
+    """Exchange that picks, per bucket list, the faster of RCCL
+    (collective.Exchange: RS -> HIP epilogue -> AG) and the xGMI P2P exchange
+    (PeerExchange) by timing both on the real buckets the first time it sees
+    them — the way RCCL itself tunes its algorithm per size, lifted one level.
+
+    The trial runs `trials` exchanges with each candidate on the buckets, then
+    restores their contents from a snapshot, so the first call returns the
+    same values as any later one. The choice is rank-agreed (the slowest
+    rank's time decides), so every rank keeps issuing the same collectives.
+    P2P is a candidate only for GPU buckets with every rank on one host; if
+    its setup fails on any rank, RCCL is used. ``picked`` maps each bucket
+    list (by address) to "rccl" or "p2p"."""
+
+    def __init__(self, group=None, trials=3, mode="pull", epilogue=None):
+        from .collective import Exchange, HipEpilogue
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.trials = int(trials)
+        self.epilogue = epilogue if epilogue is not None else HipEpilogue()
+        self.rccl = Exchange(group, epilogue=self.epilogue)
+        self.mode = mode
+        self._p2p = None
+        self._host_ok = None
+        self.picked = {}
+        self._choice = {}
+
+    def _p2p_candidate(self, buckets):
+        if self.world == 1 or not all(b.is_cuda for b in buckets):
+            return None
+        if self._host_ok is None:
+            self._host_ok = _same_host(self.group)
+        if not self._host_ok:
+            return None
+        if self._p2p is None:
+            self._p2p = PeerExchange(self.group, mode=self.mode)
+        return self._p2p
+
+    def _agree_all(self, flag):
+        flags = [None] * self.world
+        dist.all_gather_object(flags, bool(flag), group=self.group)
+        return all(flags)
+
+    def _pick(self, buckets, step):
+        import time
+        key = tuple((b.data_ptr(), b.numel(), b.dtype) for b in buckets)
+        ex = self._choice.get(key)
+        if ex is not None:
+            return ex
+        cands = [("rccl", self.rccl)]
+        p2p = self._p2p_candidate(buckets)
+        if p2p is not None:
+            cands.append(("p2p", p2p))
+        if len(cands) > 1:
+            snap = [b.clone() for b in buckets]
+            times = []
+            for name, cand in cands:
+                ok = True
+                try:
+                    step(cand)  # warm-up; maps the buckets for P2P
+                    torch.cuda.synchronize()
+                except Exception:
+                    ok = False
+                if not self._agree_all(ok):
+                    times.append(float("inf"))
+                    continue
+                dist.barrier(group=self.group)
+                t0 = time.perf_counter()
+                for _ in range(self.trials):
+                    step(cand)
+                torch.cuda.synchronize()
+                times.append(time.perf_counter() - t0)
+            every = [None] * self.world
+            dist.all_gather_object(every, times, group=self.group)
+            worst = [max(t[i] for t in every) for i in range(len(cands))]
+            best = min(range(len(cands)), key=lambda i: worst[i])
+            for b, s in zip(buckets, snap):
+                b.copy_(s)
+            del snap
+        else:
+            best = 0
+        self.picked[key] = cands[best][0]
+        self._choice[key] = cands[best][1]
+        return cands[best][1]
+
+    def all_reduce_(self, buckets, op="sum", average=False, coalesce=True):
+        buckets = list(buckets)
+        if self.world == 1:
+            return self.rccl.all_reduce_(buckets, op=op, average=average)
+        ex = self._pick(buckets, lambda e: e.all_reduce_(buckets, op=op, average=average))
+        ex.all_reduce_(buckets, op=op, average=average)
+        return buckets
+
+    def sma_(self, buckets, alpha):
+        buckets = list(buckets)
+        if self.world == 1:
+            return self.rccl.sma_(buckets, alpha)
+        ex = self._pick(buckets, lambda e: e.sma_(buckets, alpha))
+        ex.sma_(buckets, alpha)
+        return buckets
+
+    def close(self):
+        if self._p2p is not None:
+            self._p2p.close()

@@ -397,3 +397,37 @@ def body_torch_sync_sgd_sums(rank, world, use_gpu):
 @pytest.mark.parametrize("world", [2, 3])
 def test_torch_sync_sgd_sums_like_reference(world):
     run_world("body_torch_sync_sgd_sums", world)
+
+
+def body_auto_exchange_cpu(rank, world, use_gpu):
+    # AutoExchange on host tensors: P2P is no candidate, RCCL's path (gloo
+    # here) is picked, S-SGD values as with Exchange
+    from kungfu_amd.optimizers import SynchronousSGDOptimizer
+    from kungfu_amd.p2p import AutoExchange
+    ex = AutoExchange(epilogue=_epilogue(use_gpu))
+    m = _model()
+    opt = SynchronousSGDOptimizer(torch.optim.SGD(m.parameters(), lr=0.1),
+                                  named_parameters=m.named_parameters(), exchange=ex)
+    grads = []
+    for r in range(world):
+        mr = _model()
+        _loss(mr, r).backward()
+        grads.append([p.grad.clone() for p in mr.parameters()])
+    opt.zero_grad()
+    _loss(m, rank).backward()
+    opt.step()
+    ref = _model()
+    with torch.no_grad():
+        for j, p in enumerate(ref.parameters()):
+            s = grads[0][j].clone()
+            for r in range(1, world):
+                s = s + grads[r][j]
+            p -= 0.1 * (s / world)
+    for p, q in zip(m.parameters(), ref.parameters()):
+        assert torch.allclose(p, q, rtol=0, atol=1e-6)
+    assert set(ex.picked.values()) == {"rccl"}
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_auto_exchange_host_buckets(world):
+    run_world("body_auto_exchange_cpu", world)

@@ -200,3 +200,50 @@ def test_p2p_optimizers(world):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     _run(_opt_body, world)
+
+
+def _auto_body(rank, world, port, errq):
+    """AutoExchange on GPU buckets: both RCCL's path (gloo here) and P2P are
+    timed on the first call, whose result must still be the plain all-reduce
+    (the trial restores the buckets); the pick is the same on every rank; the
+    P2P pick is bit-exact at any world, the gloo path at world 2."""
+    sys.path[:0] = [ROOT, HERE]
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from kungfu_amd import ops
+        from kungfu_amd.collective import GradBuckets
+        from kungfu_amd.p2p import AutoExchange
+        dev = torch.device("cuda:0")
+        sizes = [70001, 333, 120000]
+        gb = GradBuckets(sizes, torch.float32, dev, world, n_buckets=3)
+        ex = AutoExchange(trials=2)
+        for step in range(2):
+            xs = [[torch.randn(n, device=dev, generator=torch.Generator(device=dev)
+                               .manual_seed(1000 * r + 10 * step + i)) for i, n in enumerate(sizes)]
+                  for r in range(world)]
+            for v, x in zip(gb.views, xs[rank]):
+                v.copy_(x)
+            ex.all_reduce_(gb.buckets, average=True)
+            for i, v in enumerate(gb.views):
+                want = ops.bucket_reduce_avg([xs[r][i] for r in range(world)], world)
+                if world == 2 or ex.picked[next(iter(ex.picked))] == "p2p":
+                    assert torch.equal(v, want), (step, i)
+                else:
+                    assert torch.allclose(v, want, rtol=0, atol=1e-5), (step, i)
+        picks = [None] * world
+        dist.all_gather_object(picks, sorted(ex.picked.values()))
+        assert all(p == picks[0] for p in picks), picks
+        ex.close()
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:
+        errq.put("rank %d: %s" % (rank, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_auto_exchange_gpu(world):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _run(_auto_body, world)
