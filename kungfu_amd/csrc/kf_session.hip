@@ -363,6 +363,7 @@ struct SendItem {  // one chunk to every fd in `fds` (the node's successors)
     size_t bytes;
     void *stream;
     hipEvent_t ready;  // device mode: recorded on `stream` when the chunk is final
+    bool slot_ok = false;  // device mode: its D2H into a tx slot was queued
 };
 
 }  // namespace
@@ -392,7 +393,12 @@ struct kf_session {
     int listen_unix = -1, listen_tcp = -1;
     std::unordered_map<int, int> out_fd, in_fd;  // peer -> fd
     kf_ingest_t *ingest = nullptr;
-    void *tx            = nullptr;  // device mode: page-locked outgoing chunk (sender thread)
+    // device mode: page-locked outgoing chunk slots (sender thread). The
+    // sender copies the next queued chunks' bytes out of HBM while it writes
+    // the current one to its sockets, so a chunk's D2H is off the critical
+    // path of the one before it (KUNGFU_AMD_TX_SLOTS, 1 = copy, send, copy...)
+    std::vector<void *> tx;
+    std::vector<hipEvent_t> tx_done;  // one per slot: its D2H has landed
     hipStream_t tx_stream = nullptr;  // sender's D2H stream
     std::vector<hipEvent_t> ev_pool;  // free "chunk is final" events
     std::mutex ev_mu;
@@ -499,7 +505,8 @@ struct kf_session {
         }
         if (listen_tcp >= 0) ::close(listen_tcp);
         if (ingest) kf_ingest_destroy(ingest);
-        if (tx) (void)hipHostFree(tx);
+        for (auto p : tx) (void)hipHostFree(p);
+        for (auto e : tx_done) (void)hipEventDestroy(e);
         for (auto e : ev_pool) (void)hipEventDestroy(e);
         if (tx_stream) (void)hipStreamDestroy(tx_stream);
         if (stage) (void)hipFree(stage);
@@ -507,18 +514,43 @@ struct kf_session {
 
     void sender_loop()
     {
+        // device mode: items whose D2H into slot (first_slot + i) % nslot
+        // has been issued, oldest first
+        std::deque<SendItem> staged;
+        size_t first_slot = 0;
+        const size_t nslot = device_mode ? tx.size() : 0;
         for (;;) {
             SendItem it;
             {
                 std::unique_lock<std::mutex> l(mu);
-                cv_work.wait(l, [&] { return stopping || !queue.empty(); });
-                if (queue.empty()) return;
-                it = queue.front();
-                queue.pop_front();
+                if (staged.empty()) cv_work.wait(l, [&] { return stopping || !queue.empty(); });
+                // issue the D2H of every queued chunk that has a free slot
+                while (device_mode && staged.size() < nslot && !queue.empty()) {
+                    SendItem q = queue.front();
+                    queue.pop_front();
+                    l.unlock();
+                    const size_t slot = (first_slot + staged.size()) % nslot;
+                    q.slot_ok = send_rc == KF_OK && stage_d2h(q, slot);
+                    staged.push_back(std::move(q));
+                    l.lock();
+                }
+                if (staged.empty() && queue.empty()) return;  // stopping, nothing left
+                if (!device_mode) {
+                    it = queue.front();
+                    queue.pop_front();
+                }
             }
             int rc = KF_OK;
             std::string err;
-            if (send_rc == KF_OK) rc = send_item(it, &err);
+            if (device_mode) {
+                it = std::move(staged.front());
+                staged.pop_front();
+                const size_t slot = first_slot;
+                first_slot        = (first_slot + 1) % nslot;
+                if (send_rc == KF_OK) rc = send_staged(it, slot, &err);
+            } else if (send_rc == KF_OK) {
+                rc = send_item(it, &err);
+            }
             {
                 std::lock_guard<std::mutex> l(mu);
                 if (rc != KF_OK && send_rc == KF_OK) {
@@ -528,6 +560,41 @@ struct kf_session {
                 if (--inflight == 0) cv_idle.notify_all();
             }
         }
+    }
+
+    // Queue the D2H of a device chunk into tx slot `slot` behind the event that
+    // marks the chunk final on the caller's stream; tx_done[slot] marks it landed.
+    bool stage_d2h(SendItem &it, size_t slot)
+    {
+        bool ok = it.ready && it.bytes <= kChunk + 4096 &&
+                  hipStreamWaitEvent(tx_stream, it.ready, 0) == hipSuccess &&
+                  hipMemcpyAsync(tx[slot], it.ptr, it.bytes, hipMemcpyDeviceToHost, tx_stream) ==
+                      hipSuccess &&
+                  hipEventRecord(tx_done[slot], tx_stream) == hipSuccess;
+        if (it.ready) {
+            std::lock_guard<std::mutex> l(ev_mu);
+            ev_pool.push_back(it.ready);
+            it.ready = nullptr;
+        }
+        return ok;
+    }
+
+    int send_staged(const SendItem &it, size_t slot, std::string *err)
+    {
+        if (!it.slot_ok || hipEventSynchronize(tx_done[slot]) != hipSuccess) {
+            *err = "D2H of an outgoing chunk failed";
+            return KF_ERR_HIP;
+        }
+        for (int fd : it.fds) {
+            const int rc = kf_rch_send(fd, it.name.c_str(), it.flags,
+                                       static_cast<const char *>(tx[slot]),
+                                       static_cast<uint32_t>(it.bytes));
+            if (rc != KF_OK) {
+                *err = kf_ingest_last_error();
+                return rc;
+            }
+        }
+        return KF_OK;
     }
 
     // Device mode: ONE copy of the chunk to page-locked memory, then the same
@@ -554,31 +621,10 @@ struct kf_session {
         return e;
     }
 
-    int send_item(const SendItem &it, std::string *err)
+    int send_item(const SendItem &it, std::string *err)  // host mode
     {
-        const char *src = it.ptr;
-        if (device_mode) {
-            if (it.bytes > kChunk + 4096) {
-                *err = "chunk larger than the tx buffer";
-                return KF_ERR_ARG;
-            }
-            const bool ok = it.ready &&
-                            hipStreamWaitEvent(tx_stream, it.ready, 0) == hipSuccess &&
-                            hipMemcpyAsync(tx, it.ptr, it.bytes, hipMemcpyDeviceToHost,
-                                           tx_stream) == hipSuccess &&
-                            hipStreamSynchronize(tx_stream) == hipSuccess;
-            if (it.ready) {
-                std::lock_guard<std::mutex> l(ev_mu);
-                ev_pool.push_back(it.ready);
-            }
-            if (!ok) {
-                *err = "D2H of an outgoing chunk failed";
-                return KF_ERR_HIP;
-            }
-            src = static_cast<const char *>(tx);
-        }
         for (int fd : it.fds) {
-            const int rc = kf_rch_send(fd, it.name.c_str(), it.flags, src,
+            const int rc = kf_rch_send(fd, it.name.c_str(), it.flags, it.ptr,
                                        static_cast<uint32_t>(it.bytes));
             if (rc != KF_OK) {
                 *err = kf_ingest_last_error();
@@ -1076,11 +1122,21 @@ kf_session_t *create_session(int rank, std::vector<PeerAddr> peers, const char *
     s->sl = strategy_list(s->strategy, s->hosts());
     if (s->device_mode) {
         s->ingest = kf_ingest_create(kChunk + 4096, 8);
-        if (hipHostMalloc(&s->tx, kChunk + 4096, hipHostMallocDefault) != hipSuccess) s->tx = nullptr;
+        int nslot = 4;
+        if (const char *e = std::getenv("KUNGFU_AMD_TX_SLOTS")) nslot = std::max(1, std::atoi(e));
+        bool tx_ok = true;
+        for (int i = 0; i < nslot && tx_ok; ++i) {
+            void *p      = nullptr;
+            hipEvent_t e = nullptr;
+            tx_ok = hipHostMalloc(&p, kChunk + 4096, hipHostMallocDefault) == hipSuccess;
+            if (tx_ok) s->tx.push_back(p);
+            tx_ok = tx_ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+            if (tx_ok) s->tx_done.push_back(e);
+        }
         if (hipStreamCreateWithFlags(&s->tx_stream, hipStreamNonBlocking) != hipSuccess) {
             s->tx_stream = nullptr;
         }
-        if (!s->ingest || !s->tx || !s->tx_stream) {
+        if (!s->ingest || !tx_ok || !s->tx_stream) {
             t_sess_error = "kf_ingest_create failed";
             delete s;
             return nullptr;
