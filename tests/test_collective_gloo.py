@@ -431,3 +431,17 @@ def body_auto_exchange_cpu(rank, world, use_gpu):
 @pytest.mark.parametrize("world", [2, 3])
 def test_auto_exchange_host_buckets(world):
     run_world("body_auto_exchange_cpu", world)
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_more_ranks_all_reduce(world):
+    # the N = 4 / 8 shapes of the driver's multi-GPU run, rehearsed on CPU:
+    # fp32 within the order bound, int32 / MAX bit-exact, ResNet-50's 16
+    # buckets (C4 layout), the fake_agent KATs, S-SGD
+    run_world("body_all_reduce", world)
+    run_world("body_group_all_reduce", world)
+
+
+def test_eight_ranks_resnet50_and_sgd():
+    run_world("body_resnet50_buckets", 8)
+    run_world("body_sync_sgd", 8)
