@@ -293,7 +293,9 @@ int kf_session_all_reduce(kf_session_t *s, const void *send, void *recv,
  * so every peer submits the same names in the same order (the rule RCCL has
  * too; the reference's goroutine per call does not need it). Buffers stay
  * valid and untouched until done; the name is copied. A synchronous
- * kf_session_all_reduce first waits for everything queued before it. */
+ * kf_session_all_reduce first waits for everything queued before it; from
+ * inside a done callback it (and kf_session_wait_all) returns KF_ERR_ARG
+ * instead of waiting for itself. */
 typedef void (*kf_done_fn)(int status, void *arg);
 int kf_session_all_reduce_async(kf_session_t *s, const void *send, void *recv,
                                 size_t count, KungFu_Datatype dt, KungFu_Op op,

@@ -1215,6 +1215,10 @@ int kf_session_all_reduce(kf_session_t *s, const void *send, void *recv, size_t 
     if (!s || !name || (count > 0 && (!send || !recv))) return KF_ERR_ARG;
     if (dt == KungFu_BOOL || (dt == KungFu_FLOAT16 && op != KungFu_SUM)) return KF_ERR_OP;
     t_sess_error.clear();
+    if (s->aworker.joinable() && std::this_thread::get_id() == s->aworker.get_id()) {
+        // from a done callback: waiting for the queue would wait for itself
+        return fail(KF_ERR_ARG, "synchronous all-reduce from a done callback");
+    }
     // after every all-reduce submitted before it (one message order per peer)
     const int rc = s->wait_all();
     if (rc != KF_OK) return rc;
@@ -1243,6 +1247,9 @@ int kf_session_all_reduce_async(kf_session_t *s, const void *send, void *recv, s
 int kf_session_wait_all(kf_session_t *s)
 {
     if (!s) return KF_ERR_ARG;
+    if (s->aworker.joinable() && std::this_thread::get_id() == s->aworker.get_id()) {
+        return fail(KF_ERR_ARG, "kf_session_wait_all from a done callback");
+    }
     return s->wait_all();
 }
 

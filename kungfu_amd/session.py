@@ -66,6 +66,7 @@ class Session:
                 self._h, STRATEGIES[strategy], 1 if hash_method == "NAME" else 0),
                 "kf_session_set_strategy")
         self._pending = []  # async handles: keep buffers and callbacks alive
+        self._plock = threading.Lock()
         if host_reduce_fn is not None:
             if mode != "host":
                 raise ValueError("host_reduce_fn needs mode='host'")
@@ -140,13 +141,15 @@ class Session:
         rc = self.lib.kf_session_all_reduce_async(self._h, sp, rp, count, dt, int(red),
                                                   name.encode(), stream, h._cfn, None)
         _lib.check(rc, "kf_session_all_reduce_async")
-        self._pending = [p for p in self._pending if not p.done()] + [h]
+        with self._plock:
+            self._pending = [p for p in self._pending if not p.done()] + [h]
         return h
 
     def wait_all(self):
         """Block until every queued all-reduce has finished."""
         rc = self.lib.kf_session_wait_all(self._h)
-        self._pending = [p for p in self._pending if not p.done()]
+        with self._plock:
+            self._pending = [p for p in self._pending if not p.done()]
         _lib.check(rc, "kf_session_wait_all")
 
 

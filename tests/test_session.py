@@ -362,8 +362,17 @@ def _async_body(rank, size, sock_dir, mode, errq):
             recvs = [np.zeros_like(x) for x in xs[:2]] + [sends[2]]
             s = Session(rank, size, sock_dir, mode="host", host_reduce_fn=oracle_reduce_fn())
         seen = []
-        hs = [s.all_reduce_async(snd, rcv, name, callback=lambda st, name=name:
-                                 seen.append((name, st)))
+        nested = []
+
+        def cb(st, name):
+            seen.append((name, st))
+            if name == "grad/a":  # a blocking call from the worker must not hang
+                try:
+                    s.wait_all()
+                except Exception as e:
+                    nested.append(str(e))
+
+        hs = [s.all_reduce_async(snd, rcv, name, callback=lambda st, name=name: cb(st, name))
               for (name, _, _), snd, rcv in zip(specs, sends, recvs)]
         z = inputs(rank, 11, "iota")
         zr = np.zeros_like(z)
@@ -375,6 +384,7 @@ def _async_body(rank, size, sock_dir, mode, errq):
         s.wait_all()
         assert [n for n, _ in seen] == [n for n, _, _ in specs]  # submission order
         assert all(st == 0 for _, st in seen)
+        assert len(nested) == 1 and "KF_ERR_ARG" in nested[0], nested
         s.close()
         if mode == "device":
             outs = [o.cpu().numpy() for o in outs]
