@@ -577,3 +577,19 @@ def test_dropin_int_max_n(lib, orc):
     assert np.array_equal(got, x + y)
     for a, b in _windows(n):
         assert np.array_equal(got[a:b], orc.transform2(x[a:b], y[a:b], "u8", "sum")), (a, b)
+
+
+@pytest.mark.gpu
+def test_bf16_two_input_sum_matches_torch_gpu(dev):
+    """Independent cross-check of the bf16 definition (parity unpinned, no
+    reference): the HIP two-input bf16 SUM equals torch's own bf16 add on the
+    GPU bit for bit (fp32 add, one round to nearest even), incl. the 16-B
+    vector path and a ragged tail."""
+    from kungfu_amd import ops
+    g = torch.Generator(device=dev).manual_seed(5)
+    for n in (7, 65536 * 4 + 13):
+        x = (torch.randn(n, device=dev, generator=g) * 100).bfloat16()
+        y = torch.randn(n, device=dev, generator=g).bfloat16()
+        got = ops.bucket_reduce([x, y])
+        want = x + y
+        assert torch.equal(got.view(torch.int16), want.view(torch.int16)), n

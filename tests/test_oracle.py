@@ -136,6 +136,41 @@ def test_bf16_build_semantics(oracle_mod):
     assert np.all(np.isnan(oracle_mod.bf16_bits_to_f32(oracle_mod.f32_to_bf16_bits(f))))
 
 
+def test_bf16_two_input_matches_torch(oracle_mod):
+    """bf16 has no reference reduce (parity unpinned); its
+    two-input SUM / MIN / MAX are cross-checked against an independent
+    implementation, torch's CPU bfloat16 ops, on random values and every pair
+    of specials (NaN compared by position)."""
+    import torch
+    rng = np.random.default_rng(11)
+    vals = np.concatenate([rng.standard_normal(4000).astype(np.float32) * 10,
+                           rng.standard_normal(1000).astype(np.float32) * 1e30,
+                           rng.standard_normal(1000).astype(np.float32) * 1e-39])
+    sp = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1e-40, -1e-40, 3.3895e38, 1.0],
+                  np.float32)
+    a = np.concatenate([vals, np.repeat(sp, len(sp))])
+    b = np.concatenate([vals[::-1].copy(), np.tile(sp, len(sp))])
+    ab, bb = oracle_mod.f32_to_bf16_bits(a), oracle_mod.f32_to_bf16_bits(b)
+    ta = torch.from_numpy(ab.view(np.int16)).view(torch.bfloat16)
+    tb = torch.from_numpy(bb.view(np.int16)).view(torch.bfloat16)
+    for op, fn in (("sum", torch.add), ("min", torch.minimum), ("max", torch.maximum)):
+        got = oracle_mod.transform2(ab, bb, "bf16", op)
+        want = fn(ta, tb).view(torch.int16).numpy().view(np.uint16)
+        gf = oracle_mod.bf16_bits_to_f32(got)
+        wf = oracle_mod.bf16_bits_to_f32(want)
+        nan = np.isnan(wf)
+        if op == "sum":
+            assert np.array_equal(np.isnan(gf), nan)
+            assert np.array_equal(got[~nan], want[~nan])
+        else:
+            # torch propagates NaN from either side and orders -0 < +0; the
+            # build selects an input like std::min/max (op.cpp:22-43), which
+            # keeps the first of two equal zeros — the only other difference
+            fa, fb = oracle_mod.bf16_bits_to_f32(ab), oracle_mod.bf16_bits_to_f32(bb)
+            ok = ~(np.isnan(fa) | np.isnan(fb) | ((fa == 0) & (fb == 0)))
+            assert np.array_equal(got[ok], want[ok]), op
+
+
 @pytest.mark.parametrize("dt", ["u8", "u16", "u32", "u64", "i8", "i16", "i32", "i64",
                                 "f16", "f32", "f64"])
 def test_oracle_vs_reference_build_random(oracle_mod, dt):
