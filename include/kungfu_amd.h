@@ -285,6 +285,19 @@ int kf_session_set_host_reduce(kf_session_t *s, kf_host_reduce_fn fn);
 int kf_session_all_reduce(kf_session_t *s, const void *send, void *recv,
                           size_t count, KungFu_Datatype dt, KungFu_Op op,
                           const char *name, void *stream);
+/* GoKungfuReduce (srcs/go/libkungfu-comm/collective.go:109-120) ->
+ * Session.Reduce (srcs/go/kungfu/session/session.go:159-162): the reduce graph
+ * of the session's first strategy only. The graph's root ends with the
+ * reduction in recv; an inner node with its partial fold; a leaf's recv is
+ * left as it was (runGraphs forwards only in a graph without self loops),
+ * unless the peer is alone. Same fold order rules as the all-reduce. */
+int kf_session_reduce(kf_session_t *s, const void *send, void *recv, size_t count,
+                      KungFu_Datatype dt, KungFu_Op op, const char *name, void *stream);
+/* GoKungfuBroadcast (collective.go:122-132) -> Session.Broadcast
+ * (session.go:164-167): the first strategy's bcast graph; every peer's recv
+ * becomes the root's send (the root forwards its own). */
+int kf_session_broadcast(kf_session_t *s, const void *send, void *recv, size_t count,
+                         KungFu_Datatype dt, const char *name, void *stream);
 /* GoKungfuAllReduce with done != nil (srcs/go/libkungfu-comm/collective.go:
  * 34-45, main.go:184-191): queue the all-reduce on the session's worker
  * thread and return KF_OK at once; done(status, arg) runs on that thread when

@@ -47,6 +47,8 @@ EXPORTED = (
     "kf_session_set_host_reduce",
     "kf_session_all_reduce",
     "kf_session_all_reduce_async",
+    "kf_session_reduce",
+    "kf_session_broadcast",
     "kf_session_wait_all",
     "kf_session_destroy",
     "kf_session_last_error",
@@ -189,6 +191,12 @@ def load():
                                                 c_int, ctypes.c_char_p, c_void_p, DONE_FN,
                                                 c_void_p]
     lib.kf_session_all_reduce_async.restype = c_int
+    lib.kf_session_reduce.argtypes = [c_void_p, c_void_p, c_void_p, c_size_t, c_int, c_int,
+                                      ctypes.c_char_p, c_void_p]
+    lib.kf_session_reduce.restype = c_int
+    lib.kf_session_broadcast.argtypes = [c_void_p, c_void_p, c_void_p, c_size_t, c_int,
+                                         ctypes.c_char_p, c_void_p]
+    lib.kf_session_broadcast.restype = c_int
     lib.kf_session_wait_all.argtypes = [c_void_p]
     lib.kf_session_wait_all.restype = c_int
     lib.kf_session_last_error.argtypes = []

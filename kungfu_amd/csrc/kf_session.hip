@@ -821,12 +821,17 @@ struct kf_session {
         return KF_OK;
     }
 
+    // kind: kAllReduce (both graphs of the chunk's strategy), kReduce (the
+    // first strategy's reduce graph only, Session.Reduce session.go:159-162),
+    // kBroadcast (its bcast graph only, Session.Broadcast session.go:164-167)
     int all_reduce(const char *send, char *recv, size_t count, KungFu_Datatype dt,
-                   KungFu_Op op, const std::string &name, void *stream);
+                   KungFu_Op op, const std::string &name, void *stream, int kind = 0);
 };
 
+enum { kAllReduce = 0, kReduce = 1, kBroadcast = 2 };
+
 int kf_session::all_reduce(const char *send, char *recv, size_t count, KungFu_Datatype dt,
-                           KungFu_Op op, const std::string &name, void *stream)
+                           KungFu_Op op, const std::string &name, void *stream, int kind)
 {
     const size_t isz   = kungfu_type_size(dt);
     const bool inplace = send == recv;
@@ -847,6 +852,16 @@ int kf_session::all_reduce(const char *send, char *recv, size_t count, KungFu_Da
     }
     const size_t k   = (bytes + kChunk - 1) / kChunk;
     const auto parts = even_partition(count, k);
+    // Reduce / Broadcast: one graph of the first strategy for every chunk (the
+    // reference sends the workspace as one message; chunking it the same way
+    // as the all-reduce changes no element's result)
+    Strategy single{kind == kBroadcast ? Graph(size) : sl[0].reduce,
+                    kind == kReduce ? Graph(size) : sl[0].bcast};
+    // runGraphs forwards SendBuf only in a graph without self loops (the bcast
+    // graph) or when the node is isolated in every graph it runs
+    const bool isolated = single.reduce.prev[rank].empty() && single.reduce.next[rank].empty() &&
+                          single.bcast.prev[rank].empty() && single.bcast.next[rank].empty();
+    const bool may_forward = kind != kReduce || isolated;
     struct Chunk {
         std::string name;
         const Strategy *st;
@@ -864,7 +879,7 @@ int kf_session::all_reduce(const char *send, char *recv, size_t count, KungFu_Da
         c.name  = "part::" + name + "[" + std::to_string(parts[i].first) + ":" +
                  std::to_string(parts[i].second) + "]";
         const uint64_t h = hash_name ? name_hash(c.name) : static_cast<uint64_t>(i);
-        c.st             = &sl[h % sl.size()];
+        c.st             = kind == kAllReduce ? &sl[h % sl.size()] : &single;
         c.pending_reduce = c.st->reduce.prev[rank].size();
         c.waiting        = c.st->reduce.prev[rank];
         c.recv_count     = 0;
@@ -891,7 +906,7 @@ int kf_session::all_reduce(const char *send, char *recv, size_t count, KungFu_Da
     };
     auto finish_bcast = [&](size_t i) {  // after recvInto or at the bcast root
         auto &c = chunks[i];
-        if (c.st->bcast.prev[rank].empty() && c.recv_count == 0 && !inplace) {
+        if (may_forward && c.st->bcast.prev[rank].empty() && c.recv_count == 0 && !inplace) {
             // w.Forward(): nothing received in either graph
             if (device_mode) {  // errors surface at the final stream sync
                 (void)hipMemcpyAsync(const_cast<char *>(cptr(recv, i)), cptr(send, i), clen(i),
@@ -1224,6 +1239,43 @@ int kf_session_all_reduce(kf_session_t *s, const void *send, void *recv, size_t 
     if (rc != KF_OK) return rc;
     return s->all_reduce(static_cast<const char *>(send), static_cast<char *>(recv), count, dt,
                          op, name, stream);
+}
+
+static int blocking_collective(kf_session_t *s, const void *send, void *recv, size_t count,
+                               KungFu_Datatype dt, KungFu_Op op, const char *name, void *stream,
+                               int kind)
+{
+    if (!s || !name || (count > 0 && (!send || !recv))) return KF_ERR_ARG;
+    if (dt == KungFu_BOOL || (dt == KungFu_FLOAT16 && op != KungFu_SUM)) return KF_ERR_OP;
+    t_sess_error.clear();
+    if (s->aworker.joinable() && std::this_thread::get_id() == s->aworker.get_id()) {
+        return fail(KF_ERR_ARG, "blocking collective from a done callback");
+    }
+    const int rc = s->wait_all();
+    if (rc != KF_OK) return rc;
+    return s->all_reduce(static_cast<const char *>(send), static_cast<char *>(recv), count, dt,
+                         op, name, stream, kind);
+}
+
+int kf_session_reduce(kf_session_t *s, const void *send, void *recv, size_t count,
+                      KungFu_Datatype dt, KungFu_Op op, const char *name, void *stream)
+{
+    return blocking_collective(s, send, recv, count, dt, op, name, stream, kReduce);
+}
+
+int kf_session_broadcast(kf_session_t *s, const void *send, void *recv, size_t count,
+                         KungFu_Datatype dt, const char *name, void *stream)
+{
+    // no fold: any dtype the wire can carry (BOOL included, as the reference)
+    if (!s || !name || (count > 0 && (!send || !recv))) return KF_ERR_ARG;
+    t_sess_error.clear();
+    if (s->aworker.joinable() && std::this_thread::get_id() == s->aworker.get_id()) {
+        return fail(KF_ERR_ARG, "blocking collective from a done callback");
+    }
+    const int rc = s->wait_all();
+    if (rc != KF_OK) return rc;
+    return s->all_reduce(static_cast<const char *>(send), static_cast<char *>(recv), count, dt,
+                         KungFu_SUM, name, stream, kBroadcast);
 }
 
 int kf_session_all_reduce_async(kf_session_t *s, const void *send, void *recv, size_t count,

@@ -120,6 +120,37 @@ class Session:
         _lib.check(rc, "kf_session_all_reduce")
         return recv
 
+    def _stream(self, t):
+        if self.mode != "device":
+            return None
+        import torch
+        return torch.cuda.current_stream(t.device).cuda_stream
+
+    def reduce(self, send, recv, name, op="sum"):
+        """Session.Reduce (session.go:159-162): the first strategy's reduce
+        graph only; its root's recv holds the reduction."""
+        red = OP_NAMES[op] if isinstance(op, str) else OP(op)
+        count, dt, sp = self._meta(send)
+        rcount, rdt, rp = self._meta(recv)
+        if (rcount, rdt) != (count, dt):
+            raise ValueError("send/recv mismatch")
+        _lib.check(self.lib.kf_session_reduce(self._h, sp, rp, count, dt, int(red),
+                                              name.encode(), self._stream(send)),
+                   "kf_session_reduce")
+        return recv
+
+    def broadcast(self, send, recv, name):
+        """Session.Broadcast (session.go:164-167): every recv becomes the
+        first strategy's root's send."""
+        count, dt, sp = self._meta(send)
+        rcount, rdt, rp = self._meta(recv)
+        if (rcount, rdt) != (count, dt):
+            raise ValueError("send/recv mismatch")
+        _lib.check(self.lib.kf_session_broadcast(self._h, sp, rp, count, dt, name.encode(),
+                                                 self._stream(send)),
+                   "kf_session_broadcast")
+        return recv
+
     def all_reduce_async(self, send, recv, name, op="sum", callback=None):
         """Queue an all-reduce and return at once (GoKungfuAllReduce with a
         done callback, libkungfu-comm/collective.go:34-45): the session's

@@ -297,6 +297,32 @@ def all_reduce(inputs, dt, op="sum", strategy="BINARY_TREE_STAR", hosts=None,
     return recv
 
 
+def reduce(inputs, dt, op="sum", strategy="BINARY_TREE_STAR", hosts=None, arrival=None,
+           initial=None):
+    """Session.Reduce (session.go:159-162): runGraphs(w, strategies[0].reduceGraph)
+    on the whole workspace, every rank; recv starts as `initial` (per rank) so
+    what runGraphs leaves untouched shows."""
+    k = len(inputs)
+    hosts = hosts if hosts is not None else ["127.0.0.1"] * k
+    rg, _ = strategy_list(strategy, hosts)[0]
+    send = [np.array(x, copy=True) for x in inputs]
+    recv = [np.array(x, copy=True) for x in initial] if initial is not None else \
+        [np.zeros_like(x) for x in inputs]
+    run_graphs(send, recv, dt, op, [rg], arrival=arrival)
+    return recv
+
+
+def broadcast(inputs, strategy="BINARY_TREE_STAR", hosts=None):
+    """Session.Broadcast (session.go:164-167): runGraphs(w, strategies[0].bcastGraph)."""
+    k = len(inputs)
+    hosts = hosts if hosts is not None else ["127.0.0.1"] * k
+    _, bg = strategy_list(strategy, hosts)[0]
+    send = [np.array(x, copy=True) for x in inputs]
+    recv = [np.zeros_like(x) for x in inputs]
+    run_graphs(send, recv, None, None, [bg])
+    return recv
+
+
 def chunk_roots(count, itemsize, k, strategy="RING", name="NegotiatedGrad_0/AllReduce",
                 hash_method="NAME"):
     """Per-chunk (begin, end, strategy index) as runStrategiesWithHash picks."""

@@ -447,3 +447,74 @@ def test_session_async_arg_errors():
                                                cb, None) == 2  # unknown op
         s.close()
     del ctypes
+
+
+def _rb_body(rank, size, sock_dir, mode, strategy, errq):
+    """Session.Reduce / Session.Broadcast (session.go:159-167) against the
+    schedule oracle's runGraphs over the first strategy's one graph: the
+    root's reduction, inner nodes' partial folds, leaves' recv untouched (a
+    sentinel), and the root's send everywhere after the broadcast. The c1
+    values are exact in fp32, so every arrival order gives the same bits."""
+    sys.path[:0] = [ROOT, HERE]
+    try:
+        from kungfu_amd.session import Session
+        from oracle import schedule
+        n = (3 << 20) // 4 + 5  # 4 chunks
+        xs = [inputs(r, n, "c1") for r in range(size)]
+        init = np.full(n, -7.0, np.float32)
+        want_r = schedule.reduce(xs, "f32", "sum", strategy=strategy, initial=[init] * size)[rank]
+        want_b = schedule.broadcast(xs, strategy=strategy)[rank]
+        if mode == "device":
+            import torch
+            dev = torch.device("cuda:0")
+            s = Session(rank, size, sock_dir, mode="device", strategy=strategy)
+            x = torch.from_numpy(xs[rank]).to(dev)
+            y = torch.from_numpy(init).to(dev)
+            s.reduce(x, y, "red")
+            z = torch.zeros_like(x)
+            s.broadcast(x, z, "bc")
+            y, z = y.cpu().numpy(), z.cpu().numpy()
+        else:
+            s = Session(rank, size, sock_dir, mode="host", host_reduce_fn=oracle_reduce_fn(),
+                        strategy=strategy)
+            y = init.copy()
+            s.reduce(xs[rank], y, "red")
+            z = np.zeros_like(xs[rank])
+            s.broadcast(xs[rank], z, "bc")
+        s.close()
+        assert np.array_equal(y, want_r), ("reduce", strategy, rank)
+        assert np.array_equal(z, want_b), ("broadcast", strategy, rank)
+    except Exception:
+        errq.put("rank %d: %s" % (rank, traceback.format_exc()))
+
+
+def _run_rb(size, mode, strategy):
+    ctx = mp.get_context("spawn")
+    errq = ctx.SimpleQueue()
+    with tempfile.TemporaryDirectory() as d:
+        ps = [ctx.Process(target=_rb_body, args=(r, size, d, mode, strategy, errq))
+              for r in range(size)]
+        for p in ps:
+            p.start()
+        for p in ps:
+            p.join(timeout=300)
+    errs = []
+    while not errq.empty():
+        errs.append(errq.get())
+    assert not errs, "\n".join(errs)
+    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+
+
+@pytest.mark.parametrize("strategy", ["STAR", "BINARY_TREE", "RING", "CLIQUE"])
+@pytest.mark.parametrize("size", [3, 4])
+def test_session_reduce_broadcast_host(size, strategy):
+    _run_rb(size, "host", strategy)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("strategy", ["STAR", "BINARY_TREE", "RING"])
+def test_session_reduce_broadcast_device(strategy):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _run_rb(4, "device", strategy)
