@@ -285,6 +285,16 @@ int kf_session_set_host_reduce(kf_session_t *s, kf_host_reduce_fn fn);
 int kf_session_all_reduce(kf_session_t *s, const void *send, void *recv,
                           size_t count, KungFu_Datatype dt, KungFu_Op op,
                           const char *name, void *stream);
+/* GoKungfuSubsetAllReduce (srcs/go/libkungfu-comm/collective.go:47-60) ->
+ * Session.SubsetAllReduce (srcs/go/kungfu/session/allreduce.go:14-24): every
+ * tree of the forest all-reduces within itself. forest[i] = i's father, a
+ * root is its own (graph.go:46-62); size entries. Chunked like the
+ * all-reduce, one strategy (reduce = reversed tree with self loops, bcast =
+ * the tree). A lone node forwards its send. KF_ERR_ARG for an index out of
+ * range or a cycle. */
+int kf_session_subset_all_reduce(kf_session_t *s, const void *send, void *recv, size_t count,
+                                 KungFu_Datatype dt, KungFu_Op op, const int32_t *forest,
+                                 const char *name, void *stream);
 /* GoKungfuReduce (srcs/go/libkungfu-comm/collective.go:109-120) ->
  * Session.Reduce (srcs/go/kungfu/session/session.go:159-162): the reduce graph
  * of the session's first strategy only. The graph's root ends with the

@@ -47,6 +47,7 @@ EXPORTED = (
     "kf_session_set_host_reduce",
     "kf_session_all_reduce",
     "kf_session_all_reduce_async",
+    "kf_session_subset_all_reduce",
     "kf_session_reduce",
     "kf_session_broadcast",
     "kf_session_wait_all",
@@ -191,6 +192,10 @@ def load():
                                                 c_int, ctypes.c_char_p, c_void_p, DONE_FN,
                                                 c_void_p]
     lib.kf_session_all_reduce_async.restype = c_int
+    lib.kf_session_subset_all_reduce.argtypes = [c_void_p, c_void_p, c_void_p, c_size_t, c_int,
+                                                 c_int, ctypes.POINTER(ctypes.c_int32),
+                                                 ctypes.c_char_p, c_void_p]
+    lib.kf_session_subset_all_reduce.restype = c_int
     lib.kf_session_reduce.argtypes = [c_void_p, c_void_p, c_void_p, c_size_t, c_int, c_int,
                                       ctypes.c_char_p, c_void_p]
     lib.kf_session_reduce.restype = c_int

@@ -824,15 +824,20 @@ struct kf_session {
     // kind: kAllReduce (both graphs of the chunk's strategy), kReduce (the
     // first strategy's reduce graph only, Session.Reduce session.go:159-162),
     // kBroadcast (its bcast graph only, Session.Broadcast session.go:164-167)
+    // slist: the strategies to pick from per chunk instead of the session's
+    // (SubsetAllReduce's single forest strategy)
     int all_reduce(const char *send, char *recv, size_t count, KungFu_Datatype dt,
-                   KungFu_Op op, const std::string &name, void *stream, int kind = 0);
+                   KungFu_Op op, const std::string &name, void *stream, int kind = 0,
+                   const std::vector<Strategy> *slist = nullptr);
 };
 
 enum { kAllReduce = 0, kReduce = 1, kBroadcast = 2 };
 
 int kf_session::all_reduce(const char *send, char *recv, size_t count, KungFu_Datatype dt,
-                           KungFu_Op op, const std::string &name, void *stream, int kind)
+                           KungFu_Op op, const std::string &name, void *stream, int kind,
+                           const std::vector<Strategy> *slist)
 {
+    const std::vector<Strategy> &L = slist ? *slist : sl;
     const size_t isz   = kungfu_type_size(dt);
     const bool inplace = send == recv;
     const size_t bytes = count * isz;
@@ -855,8 +860,8 @@ int kf_session::all_reduce(const char *send, char *recv, size_t count, KungFu_Da
     // Reduce / Broadcast: one graph of the first strategy for every chunk (the
     // reference sends the workspace as one message; chunking it the same way
     // as the all-reduce changes no element's result)
-    Strategy single{kind == kBroadcast ? Graph(size) : sl[0].reduce,
-                    kind == kReduce ? Graph(size) : sl[0].bcast};
+    Strategy single{kind == kBroadcast ? Graph(size) : L[0].reduce,
+                    kind == kReduce ? Graph(size) : L[0].bcast};
     // runGraphs forwards SendBuf only in a graph without self loops (the bcast
     // graph) or when the node is isolated in every graph it runs
     const bool isolated = single.reduce.prev[rank].empty() && single.reduce.next[rank].empty() &&
@@ -879,7 +884,7 @@ int kf_session::all_reduce(const char *send, char *recv, size_t count, KungFu_Da
         c.name  = "part::" + name + "[" + std::to_string(parts[i].first) + ":" +
                  std::to_string(parts[i].second) + "]";
         const uint64_t h = hash_name ? name_hash(c.name) : static_cast<uint64_t>(i);
-        c.st             = kind == kAllReduce ? &sl[h % sl.size()] : &single;
+        c.st             = kind == kAllReduce ? &L[h % L.size()] : &single;
         c.pending_reduce = c.st->reduce.prev[rank].size();
         c.waiting        = c.st->reduce.prev[rank];
         c.recv_count     = 0;
@@ -1255,6 +1260,34 @@ static int blocking_collective(kf_session_t *s, const void *send, void *recv, si
     if (rc != KF_OK) return rc;
     return s->all_reduce(static_cast<const char *>(send), static_cast<char *>(recv), count, dt,
                          op, name, stream, kind);
+}
+
+int kf_session_subset_all_reduce(kf_session_t *s, const void *send, void *recv, size_t count,
+                                 KungFu_Datatype dt, KungFu_Op op, const int32_t *forest,
+                                 const char *name, void *stream)
+{
+    if (!s || !forest || !name || (count > 0 && (!send || !recv))) return KF_ERR_ARG;
+    if (dt == KungFu_BOOL || (dt == KungFu_FLOAT16 && op != KungFu_SUM)) return KF_ERR_OP;
+    t_sess_error.clear();
+    Graph bg(s->size);  // FromForestArray (graph.go:46-62)
+    for (int i = 0; i < s->size; ++i) {
+        if (forest[i] < 0 || forest[i] >= s->size) return fail(KF_ERR_ARG, "forest out of range");
+        if (forest[i] != i) bg.edge(forest[i], i);
+    }
+    for (int i = 0; i < s->size; ++i) {  // the reference leaves cycles unchecked (FIXME
+        int hops = 0;                    // graph.go:60); here they are an error
+        for (int j = i; forest[j] != j; j = forest[j]) {
+            if (++hops > s->size) return fail(KF_ERR_ARG, "forest has a cycle");
+        }
+    }
+    if (s->aworker.joinable() && std::this_thread::get_id() == s->aworker.get_id()) {
+        return fail(KF_ERR_ARG, "blocking collective from a done callback");
+    }
+    const int rc = s->wait_all();
+    if (rc != KF_OK) return rc;
+    const std::vector<Strategy> one{simple(bg)};
+    return s->all_reduce(static_cast<const char *>(send), static_cast<char *>(recv), count, dt,
+                         op, name, stream, kAllReduce, &one);
 }
 
 int kf_session_reduce(kf_session_t *s, const void *send, void *recv, size_t count,

@@ -126,6 +126,22 @@ class Session:
         import torch
         return torch.cuda.current_stream(t.device).cuda_stream
 
+    def subset_all_reduce(self, send, recv, forest, name, op="sum"):
+        """Session.SubsetAllReduce (allreduce.go:14-24): each tree of `forest`
+        (forest[i] = father of i, a root is its own) all-reduces within itself."""
+        red = OP_NAMES[op] if isinstance(op, str) else OP(op)
+        count, dt, sp = self._meta(send)
+        rcount, rdt, rp = self._meta(recv)
+        if (rcount, rdt) != (count, dt):
+            raise ValueError("send/recv mismatch")
+        if len(forest) != self.size:
+            raise ValueError("forest needs one entry per peer")
+        f = (ctypes.c_int32 * self.size)(*forest)
+        _lib.check(self.lib.kf_session_subset_all_reduce(self._h, sp, rp, count, dt, int(red), f,
+                                                         name.encode(), self._stream(send)),
+                   "kf_session_subset_all_reduce")
+        return recv
+
     def reduce(self, send, recv, name, op="sum"):
         """Session.Reduce (session.go:159-162): the first strategy's reduce
         graph only; its root's recv holds the reduction."""

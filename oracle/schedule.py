@@ -297,6 +297,39 @@ def all_reduce(inputs, dt, op="sum", strategy="BINARY_TREE_STAR", hosts=None,
     return recv
 
 
+def from_forest_array(forest):
+    """graph.go:46-62 FromForestArray: forest[i] is i's father (i itself for a
+    root); returns (bcast graph, number of roots) or None if out of range."""
+    n = len(forest)
+    g, m = Graph(n), 0
+    for i, father in enumerate(forest):
+        if father < 0 or father >= n:
+            return None
+        if father == i:
+            m += 1
+        else:
+            g.add_edge(father, i)
+    return g, m
+
+
+def subset_all_reduce(inputs, dt, op, forest, name="NegotiatedGrad_0/AllReduce",
+                      hash_method="NAME", arrival=None):
+    """Session.SubsetAllReduce (allreduce.go:14-24): every tree of the forest
+    all-reduces within itself, chunked as AllReduce, one strategy
+    (simpleSingleGraphStrategy, strategy.go:105-107)."""
+    bg, _ = from_forest_array(forest)
+    sl = [_simple(bg)]
+    count = inputs[0].size
+    send = [np.array(x, copy=True) for x in inputs]
+    recv = [np.zeros_like(x) for x in inputs]
+    nchunks = ceil_div(count * inputs[0].itemsize, CHUNK_SIZE)
+    for b, e in (even_partition(0, count, nchunks) if nchunks else []):
+        rg, g = sl[0]
+        run_graphs([x[b:e] for x in send], [r[b:e] for r in recv], dt, op, [rg, g],
+                   arrival=arrival)
+    return recv
+
+
 def reduce(inputs, dt, op="sum", strategy="BINARY_TREE_STAR", hosts=None, arrival=None,
            initial=None):
     """Session.Reduce (session.go:159-162): runGraphs(w, strategies[0].reduceGraph)

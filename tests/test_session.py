@@ -518,3 +518,68 @@ def test_session_reduce_broadcast_device(strategy):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     _run_rb(4, "device", strategy)
+
+
+def _subset_body(rank, size, sock_dir, mode, errq):
+    """Session.SubsetAllReduce (allreduce.go:14-24) for several forests
+    against the schedule oracle: two trees, a chain, all lone nodes; bad
+    forests (cycle, out of range) are refused before any message moves."""
+    sys.path[:0] = [ROOT, HERE]
+    try:
+        from kungfu_amd._lib import KungFuAMDError
+        from kungfu_amd.session import Session
+        from oracle import schedule
+        n = (2 << 20) // 4 + 3
+        xs = [inputs(r, n, "c1") for r in range(size)]
+        forests = [[0, 0, 2, 2], [1, 1, 1, 2], [0, 1, 2, 3]]
+        if mode == "device":
+            import torch
+            dev = torch.device("cuda:0")
+            s = Session(rank, size, sock_dir, mode="device")
+            x = torch.from_numpy(xs[rank]).to(dev)
+        else:
+            s = Session(rank, size, sock_dir, mode="host", host_reduce_fn=oracle_reduce_fn())
+            x = xs[rank]
+        for bad in ([1, 0, 2, 3], [0, 0, 9, 2]):
+            try:
+                s.subset_all_reduce(x, x, bad, "bad")
+                raise AssertionError("bad forest accepted: %r" % bad)
+            except KungFuAMDError as e:
+                assert "KF_ERR_ARG" in str(e)
+        for j, forest in enumerate(forests):
+            want = schedule.subset_all_reduce(xs, "f32", "sum", forest, name="sub%d" % j)[rank]
+            y = (torch.zeros_like(x) if mode == "device" else np.zeros_like(x))
+            s.subset_all_reduce(x, y, forest, "sub%d" % j)
+            got = y.cpu().numpy() if mode == "device" else y
+            assert np.array_equal(got, want), (forest, rank)
+        s.close()
+    except Exception:
+        errq.put("rank %d: %s" % (rank, traceback.format_exc()))
+
+
+def _run_subset(mode):
+    ctx = mp.get_context("spawn")
+    errq = ctx.SimpleQueue()
+    with tempfile.TemporaryDirectory() as d:
+        ps = [ctx.Process(target=_subset_body, args=(r, 4, d, mode, errq)) for r in range(4)]
+        for p in ps:
+            p.start()
+        for p in ps:
+            p.join(timeout=300)
+    errs = []
+    while not errq.empty():
+        errs.append(errq.get())
+    assert not errs, "\n".join(errs)
+    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+
+
+def test_session_subset_all_reduce_host():
+    _run_subset("host")
+
+
+@pytest.mark.gpu
+def test_session_subset_all_reduce_device():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _run_subset("device")
