@@ -228,6 +228,61 @@ __device__ __forceinline__ typename Elt<T>::S finish(typename Elt<T>::Acc a)
 }
 
 // ---------------------------------------------------------------------------
+// Vector-path lanes. A lane is one element of the 16-B vector, except for the
+// 8-bit integers, whose lanes are 32-bit words of 4 packed bytes: split into
+// bytes, the compiler re-types the 16-B load as <16 x i8> and drops its nt
+// bit (seen in the gfx950 ISA), and the byte-wise adds cost ~3x the VALU of a
+// packed word. Results are the same bytes as Elt<T> element by element.
+// ---------------------------------------------------------------------------
+template <typename T, typename = void> struct Lane {
+    using W   = typename Elt<T>::S;
+    using Acc = typename Elt<T>::Acc;
+    __device__ static Acc load(W w) { return Elt<T>::load(w); }
+    template <int OP> __device__ static Acc combine(Acc a, W b)
+    {
+        return Elt<T>::template combine<OP>(a, b);
+    }
+    template <int OP, int EPI> __device__ static W emit(const Acc &a, const Div &np)
+    {
+        if constexpr (EPI == EPI_DIV) {
+            return Elt<T>::div(a, np);
+        } else {
+            return finish<T, OP>(a);
+        }
+    }
+};
+
+template <typename T>
+struct Lane<T, typename std::enable_if<std::is_integral<T>::value && sizeof(T) == 1>::type> {
+    using W   = uint32_t;
+    using Acc = uint32_t;
+    __device__ static Acc load(W w) { return w; }
+    template <int OP> __device__ static Acc combine(Acc a, W b)
+    {
+        if constexpr (OP == OP_SUM) {
+            // per-byte add mod 2^8: low 7 bits add without crossing a byte,
+            // the top bit of each byte is the xor of the inputs' and the carry
+            return ((a & 0x7f7f7f7fu) + (b & 0x7f7f7f7fu)) ^ ((a ^ b) & 0x80808080u);
+        } else {
+            uint32_t r = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const T x = static_cast<T>(a >> (8 * i));
+                const T y = static_cast<T>(b >> (8 * i));
+                const T z = Elt<T>::template combine<OP>(x, y);
+                r |= static_cast<uint32_t>(static_cast<uint8_t>(z)) << (8 * i);
+            }
+            return r;
+        }
+    }
+    template <int OP, int EPI> __device__ static W emit(const Acc &a, const Div &)
+    {
+        static_assert(EPI == EPI_NONE, "8-bit integers have no /np epilogue");
+        return a;
+    }
+};
+
+// ---------------------------------------------------------------------------
 // Kernel arguments.
 // ---------------------------------------------------------------------------
 constexpr int kMaxInputs = 16;
@@ -308,13 +363,16 @@ __global__ void __launch_bounds__(BLOCK)
                   size_t nvec, Div np)
 {
     using S         = typename Elt<T>::S;
-    using Acc       = typename Elt<T>::Acc;
-    constexpr int V = Vec<S>::N;
+    using L         = Lane<T>;
+    using W         = typename L::W;
+    using Acc       = typename L::Acc;
+    constexpr int V = Vec<W>::N;                 // lanes per 16-B vector
+    constexpr int E = static_cast<int>(16 / sizeof(S));  // elements per vector
     const int kk    = KC > 0 ? KC : k;
 
     // scalar edges: head elements, then the tail after the vector body
     const size_t tid   = static_cast<size_t>(blockIdx.x) * BLOCK + threadIdx.x;
-    const size_t vend  = head + nvec * V;
+    const size_t vend  = head + nvec * E;
     const size_t nedge = head + (n - vend);
     if (tid < nedge) {
         const size_t i = tid < head ? tid : vend + (tid - head);
@@ -326,13 +384,7 @@ __global__ void __launch_bounds__(BLOCK)
     };
     char *obase = reinterpret_cast<char *>(out) + head * sizeof(S);
 
-    auto emit = [&](const Acc &a) -> S {
-        if constexpr (EPI == EPI_DIV) {
-            return Elt<T>::div(a, np);
-        } else {
-            return finish<T, OP>(a);
-        }
-    };
+    auto emit = [&](const Acc &a) -> W { return L::template emit<OP, EPI>(a, np); };
 
     const size_t tile   = static_cast<size_t>(BLOCK) * UNROLL;
     const size_t ntiles = (nvec + tile - 1) / tile;
@@ -342,86 +394,86 @@ __global__ void __launch_bounds__(BLOCK)
             Acc acc[UNROLL][V];
             if constexpr (KC > 0) {
                 // compile-time k: all KC x UNROLL loads issued before any use
-                Vec<S> v[KC][UNROLL];
+                Vec<W> v[KC][UNROLL];
 #pragma unroll
                 for (int j = 0; j < KC; ++j) {
                     const char *sj = src(j);
 #pragma unroll
-                    for (int u = 0; u < UNROLL; ++u) v[j][u] = ld_vec<S, LOADNT>(sj, v0 + u * BLOCK);
+                    for (int u = 0; u < UNROLL; ++u) v[j][u] = ld_vec<W, LOADNT>(sj, v0 + u * BLOCK);
                 }
 #pragma unroll
                 for (int u = 0; u < UNROLL; ++u) {
 #pragma unroll
                     for (int e = 0; e < V; ++e) {
-                        acc[u][e] = Elt<T>::load(v[0][u].e[e]);
+                        acc[u][e] = L::load(v[0][u].e[e]);
 #pragma unroll
                         for (int j = 1; j < KC; ++j) {
-                            acc[u][e] = Elt<T>::template combine<OP>(acc[u][e], v[j][u].e[e]);
+                            acc[u][e] = L::template combine<OP>(acc[u][e], v[j][u].e[e]);
                         }
                     }
                 }
             } else {
                 // runtime k: inputs 0 and 1 up front, then one input at a time
-                Vec<S> a[UNROLL];
-                Vec<S> b[UNROLL];
+                Vec<W> a[UNROLL];
+                Vec<W> b[UNROLL];
                 const char *s0 = src(0);
 #pragma unroll
-                for (int u = 0; u < UNROLL; ++u) a[u] = ld_vec<S, LOADNT>(s0, v0 + u * BLOCK);
+                for (int u = 0; u < UNROLL; ++u) a[u] = ld_vec<W, LOADNT>(s0, v0 + u * BLOCK);
                 if (kk > 1) {
                     const char *s1 = src(1);
 #pragma unroll
-                    for (int u = 0; u < UNROLL; ++u) b[u] = ld_vec<S, LOADNT>(s1, v0 + u * BLOCK);
+                    for (int u = 0; u < UNROLL; ++u) b[u] = ld_vec<W, LOADNT>(s1, v0 + u * BLOCK);
                 }
 #pragma unroll
                 for (int u = 0; u < UNROLL; ++u) {
 #pragma unroll
                     for (int e = 0; e < V; ++e) {
-                        acc[u][e] = Elt<T>::load(a[u].e[e]);
+                        acc[u][e] = L::load(a[u].e[e]);
                         if (kk > 1) {
-                            acc[u][e] = Elt<T>::template combine<OP>(acc[u][e], b[u].e[e]);
+                            acc[u][e] = L::template combine<OP>(acc[u][e], b[u].e[e]);
                         }
                     }
                 }
                 for (int j = 2; j < kk; ++j) {
                     const char *sj = src(j);
 #pragma unroll
-                    for (int u = 0; u < UNROLL; ++u) b[u] = ld_vec<S, LOADNT>(sj, v0 + u * BLOCK);
+                    for (int u = 0; u < UNROLL; ++u) b[u] = ld_vec<W, LOADNT>(sj, v0 + u * BLOCK);
 #pragma unroll
                     for (int u = 0; u < UNROLL; ++u) {
 #pragma unroll
                         for (int e = 0; e < V; ++e) {
-                            acc[u][e] = Elt<T>::template combine<OP>(acc[u][e], b[u].e[e]);
+                            acc[u][e] = L::template combine<OP>(acc[u][e], b[u].e[e]);
                         }
                     }
                 }
             }
 #pragma unroll
             for (int u = 0; u < UNROLL; ++u) {
-                Vec<S> r;
+                Vec<W> r;
 #pragma unroll
                 for (int e = 0; e < V; ++e) r.e[e] = emit(acc[u][e]);
-                st_vec<S, STPLAIN>(obase, v0 + u * BLOCK, r);
+                st_vec<W, STPLAIN>(obase, v0 + u * BLOCK, r);
             }
         } else {
             // ragged last tile
             for (int u = 0; u < UNROLL; ++u) {
                 const size_t vi = v0 + u * BLOCK;
                 if (vi >= nvec) break;
-                Vec<S> a = ld_vec<S, LOADNT>(src(0), vi);
+                Vec<W> a = ld_vec<W, LOADNT>(src(0), vi);
                 Acc acc[V];
 #pragma unroll
-                for (int e = 0; e < V; ++e) acc[e] = Elt<T>::load(a.e[e]);
+                for (int e = 0; e < V; ++e) acc[e] = L::load(a.e[e]);
                 for (int j = 1; j < kk; ++j) {
-                    Vec<S> b = ld_vec<S, LOADNT>(src(j), vi);
+                    Vec<W> b = ld_vec<W, LOADNT>(src(j), vi);
 #pragma unroll
                     for (int e = 0; e < V; ++e) {
-                        acc[e] = Elt<T>::template combine<OP>(acc[e], b.e[e]);
+                        acc[e] = L::template combine<OP>(acc[e], b.e[e]);
                     }
                 }
-                Vec<S> r;
+                Vec<W> r;
 #pragma unroll
                 for (int e = 0; e < V; ++e) r.e[e] = emit(acc[e]);
-                st_vec<S, STPLAIN>(obase, vi, r);
+                st_vec<W, STPLAIN>(obase, vi, r);
             }
         }
     }
@@ -442,11 +494,14 @@ __global__ void __launch_bounds__(BLOCK)
                          size_t nvec, Div np)
 {
     using S         = typename Elt<T>::S;
-    using Acc       = typename Elt<T>::Acc;
-    constexpr int V = Vec<S>::N;
+    using L         = Lane<T>;
+    using W         = typename L::W;
+    using Acc       = typename L::Acc;
+    constexpr int V = Vec<W>::N;
+    constexpr int E = static_cast<int>(16 / sizeof(S));
     constexpr int G = 8;
     const size_t tid   = static_cast<size_t>(blockIdx.x) * BLOCK + threadIdx.x;
-    const size_t vend  = head + nvec * V;
+    const size_t vend  = head + nvec * E;
     const size_t nedge = head + (n - vend);
     if (tid < nedge) {
         const size_t i = tid < head ? tid : vend + (tid - head);
@@ -456,11 +511,11 @@ __global__ void __launch_bounds__(BLOCK)
     for (size_t vi = tid; vi < nvec; vi += static_cast<size_t>(gridDim.x) * BLOCK) {
         Acc acc[V];
         for (int j0 = 0; j0 < k; j0 += G) {
-            Vec<S> v[G];
+            Vec<W> v[G];
 #pragma unroll
             for (int j = 0; j < G; ++j) {
                 if (j0 + j < k) {
-                    v[j] = ld_vec<S, 1>(reinterpret_cast<const char *>(in.p[j0 + j]) +
+                    v[j] = ld_vec<W, 1>(reinterpret_cast<const char *>(in.p[j0 + j]) +
                                             head * sizeof(S), vi);
                 }
             }
@@ -469,22 +524,18 @@ __global__ void __launch_bounds__(BLOCK)
                 if (j0 + j < k) {
 #pragma unroll
                     for (int e = 0; e < V; ++e) {
-                        acc[e] = (j0 + j == 0) ? Elt<T>::load(v[j].e[e])
-                                               : Elt<T>::template combine<OP>(acc[e], v[j].e[e]);
+                        acc[e] = (j0 + j == 0) ? L::load(v[j].e[e])
+                                               : L::template combine<OP>(acc[e], v[j].e[e]);
                     }
                 }
             }
         }
-        Vec<S> r;
+        Vec<W> r;
 #pragma unroll
         for (int e = 0; e < V; ++e) {
-            if constexpr (EPI == EPI_DIV) {
-                r.e[e] = Elt<T>::div(acc[e], np);
-            } else {
-                r.e[e] = finish<T, OP>(acc[e]);
-            }
+            r.e[e] = L::template emit<OP, EPI>(acc[e], np);
         }
-        st_vec<S>(obase, vi, r);
+        st_vec<W>(obase, vi, r);
     }
 }
 

@@ -17,7 +17,9 @@ import torch
 
 PEAK = 8000.0
 CODES = {"f32": (0x20408, torch.float32), "bf16": (0x20209, torch.bfloat16),
-         "f16": (0x20208, torch.float16), "i32": (0x10408, torch.int32)}
+         "f16": (0x20208, torch.float16), "i32": (0x10408, torch.int32),
+         "i8": (0x10108, torch.int8), "u8": (0x00108, torch.uint8)}
+OPS = {"sum": 0, "min": 1, "max": 2, "prod": 3}
 
 
 def main():
@@ -27,6 +29,7 @@ def main():
     ap.add_argument("--dtype", default="f32")
     ap.add_argument("--mib", type=int, default=256)
     ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--op", default="sum", choices=sorted(OPS))
     a = ap.parse_args()
     libs = []
     for p in a.libs:
@@ -36,6 +39,8 @@ def main():
                                        ctypes.c_void_p]
         libs.append(l)
     code, tdt = CODES[a.dtype]
+    op = OPS[a.op]
+    lo, hi = (0, 256) if tdt == torch.uint8 else (-128, 128) if tdt == torch.int8 else (-1000, 1000)
     dev = torch.device("cuda:0")
     s = torch.cuda.current_stream()
     esz = torch.tensor([], dtype=tdt).element_size()
@@ -44,7 +49,7 @@ def main():
         sets = []
         for _ in range(3):
             ins = [torch.randn(n, device=dev).to(tdt) if tdt.is_floating_point
-                   else torch.randint(-1000, 1000, (n,), device=dev, dtype=tdt)
+                   else torch.randint(lo, hi, (n,), device=dev, dtype=tdt)
                    for _ in range(k)]
             out = torch.empty_like(ins[0])
             arr = (ctypes.c_void_p * k)(*[t.data_ptr() for t in ins])
@@ -52,7 +57,7 @@ def main():
         results = [[] for _ in libs]
         outs = []
         for li, l in enumerate(libs):  # same answer from every build
-            l.kf_bucket_reduce(sets[0][0], k, sets[0][1].data_ptr(), n, code, 0, s.cuda_stream)
+            l.kf_bucket_reduce(sets[0][0], k, sets[0][1].data_ptr(), n, code, op, s.cuda_stream)
             torch.cuda.synchronize()
             outs.append(sets[0][1].clone())
         same = all(torch.equal(outs[0], o) for o in outs[1:])
@@ -62,18 +67,18 @@ def main():
             for li, l in enumerate(libs):
                 for i in range(3):
                     arr, out, _ = sets[i % 3]
-                    l.kf_bucket_reduce(arr, k, out.data_ptr(), n, code, 0, s.cuda_stream)
+                    l.kf_bucket_reduce(arr, k, out.data_ptr(), n, code, op, s.cuda_stream)
                 e0.record(s)
                 for i in range(20):
                     arr, out, _ = sets[i % 3]
-                    l.kf_bucket_reduce(arr, k, out.data_ptr(), n, code, 0, s.cuda_stream)
+                    l.kf_bucket_reduce(arr, k, out.data_ptr(), n, code, op, s.cuda_stream)
                 e1.record(s)
                 torch.cuda.synchronize()
                 results[li].append(e0.elapsed_time(e1) * 1e3 / 20)
         algo = (k + 1) * n * esz
         for li, p in enumerate(a.libs):
             us = statistics.median(results[li])
-            print(json.dumps({"lib": os.path.basename(p), "k": k, "dtype": a.dtype,
+            print(json.dumps({"lib": os.path.basename(p), "k": k, "dtype": a.dtype, "op": a.op,
                               "us": round(us, 2), "GBps": round(algo / us / 1e3, 1),
                               "frac": round(algo / us / 1e3 / PEAK, 4), "same_result": same}))
         sys.stdout.flush()
