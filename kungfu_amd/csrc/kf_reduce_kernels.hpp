@@ -65,16 +65,16 @@ __device__ __forceinline__ float bf16_to_f32(uint16_t h)
     return __uint_as_float(static_cast<uint32_t>(h) << 16);
 }
 
-// RNE narrow; a NaN keeps its sign and upper payload and is made quiet. The
-// same bit recipe as the oracle, so bf16 results compare bit for bit.
+// RNE narrow; a NaN keeps its sign and upper payload and is made quiet. This
+// is gfx950's v_cvt_pk_bf16_f32 (clang's float -> __bf16), which equals the
+// oracle's bit recipe ((u + 0x7fff + lsb) >> 16; NaN: (u >> 16) | 0x0040) on
+// all 2^32 fp32 patterns (tools/explore/bf16_cvt_check.hip, 0 mismatches,
+// profiles/r01/bf16_cvt_check.json). The recipe written out in integer ops
+// compiled to a divergent branch per element (613 VALU, ~60 exec-mask
+// branches in the k = 2 kernel) and ran at 0.79 of the roofline vs 0.81.
 __device__ __forceinline__ uint16_t f32_to_bf16(float f)
 {
-    uint32_t u = __float_as_uint(f);
-    if ((u & 0x7fffffffu) > 0x7f800000u) {
-        return static_cast<uint16_t>((u >> 16) | 0x0040u);
-    }
-    u += 0x7fffu + ((u >> 16) & 1u);
-    return static_cast<uint16_t>(u >> 16);
+    return __builtin_bit_cast(uint16_t, static_cast<__bf16>(f));
 }
 
 // ---------------------------------------------------------------------------
