@@ -230,6 +230,41 @@ def test_peers_fold_bit_exact(lib, orc, dev, k):
                 assert golden_io.same_bits_or_nan(got, want), (dt, "avg", head)
 
 
+@pytest.mark.parametrize("dt", ["u8", "i8"])
+def test_8bit_lanes_k_fold_and_peers(lib, orc, dev, dt):
+    # The vector path carries 8-bit data as 32-bit words of 4 packed bytes
+    # (Lane<T>: SWAR add, per-byte MIN/MAX/PROD). Runtime-k fold and the
+    # peers fold, every op, heads 0..3 (byte offsets that leave the word
+    # lanes at every alignment) and ragged tails, against the oracle chain.
+    from kungfu_amd import _lib
+    from oracle.oracle import DT, NP, OPS
+    info = np.iinfo(NP[dt])
+    rng = np.random.default_rng(zlib.crc32(dt.encode()))
+    s = torch.cuda.current_stream().cuda_stream
+    for k in (3, 8):
+        n = 65536 * 4 + 11
+        xs = [rng.integers(info.min, info.max, size=n + 3, dtype=NP[dt], endpoint=True)
+              for _ in range(k)]
+        ts = [to_dev(x, dev) for x in xs]
+        out = torch.zeros_like(ts[0])
+        for head in (0, 1, 2, 3):
+            ptrs = _lib.ptr_array([t.data_ptr() + head for t in ts])
+            m = n - head
+            for op in ("sum", "min", "max", "prod"):
+                want = orc.reduce_k([x[head:head + m].copy() for x in xs], dt, op)
+                for fn in ("kf_bucket_reduce", "kf_bucket_reduce_peers"):
+                    out.zero_()
+                    if fn == "kf_bucket_reduce":
+                        rc = lib.kf_bucket_reduce(ptrs, k, out.data_ptr() + head, m, DT[dt],
+                                                  OPS[op], s)
+                    else:
+                        rc = lib.kf_bucket_reduce_peers(ptrs, k, out.data_ptr() + head, m,
+                                                        DT[dt], OPS[op], 0, s)
+                    assert rc == 0, lib.kf_last_error()
+                    torch.cuda.synchronize()
+                    got = from_dev(out, xs[0])[head:head + m]
+                    assert np.array_equal(got, want), (k, head, op, fn)
+
 def test_schedule_all_reduce_matches_device_fold(lib, orc, dev):
     # Whole reference schedule (RING, np=4, 4 MiB bucket = 4 chunks with
     # hash-chosen roots): per chunk, the device fold in that chunk's ring order
