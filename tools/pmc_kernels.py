@@ -39,6 +39,8 @@ VARIANTS = [
     ("div_ f32 (S-SGD shard epilogue)", 1, 1),
     ("sma_blend f32", 2, 1),
     ("reduce SUM k=2 bf16", 2, 1),
+    ("reduce SUM k=2 i8 (packed 32-bit lanes)", 2, 1),
+    ("reduce MAX k=8 i8 (packed 32-bit lanes)", 8, 1),
 ]
 
 
@@ -54,7 +56,9 @@ def run():
         m = BYTES // torch.empty((), dtype=dtype).element_size()
         sets = []
         for _ in range(3):
-            ins = [torch.randn(m, device=dev).to(dtype) for _ in range(k)]
+            ins = [torch.randn(m, device=dev).to(dtype) if dtype.is_floating_point
+                   else torch.randint(-128, 128, (m,), device=dev, dtype=dtype)
+                   for _ in range(k)]
             sets.append((ins, torch.empty_like(ins[0])))
         return sets
 
@@ -74,6 +78,10 @@ def run():
     plan.append((lambda ins, out: lib.kf_bucket_reduce(
         _lib.ptr_array([t.data_ptr() for t in ins]), 2, out.data_ptr(), out.numel(), 0x20209, 0,
         s), sets))
+    for k, op in ((2, 0), (8, 2)):
+        plan.append((lambda ins, out, k=k, op=op: lib.kf_bucket_reduce(
+            _lib.ptr_array([t.data_ptr() for t in ins]), k, out.data_ptr(), out.numel(),
+            0x10108, op, s), bufs(k, torch.int8)))
     assert len(plan) == len(VARIANTS)
     torch.cuda.synchronize()
     for fn, sets in plan:
