@@ -1,0 +1,96 @@
+"""gfx950 ISA of the shipped streaming kernels, read from the built library
+(no GPU needed): every 16-B global load and store of a product instantiation
+carries the non-temporal bit, and no kernel branches per element.
+
+Both properties were lost once without any test failing: split into bytes,
+the 8-bit kernels' loads were re-typed by the compiler and dropped `nt`, and
+the bf16 narrow compiled to a divergent branch per element (DESIGN.md §3
+notes 1 and 2; 0.72 and 0.79 of the roofline against 0.81 after the fix).
+"""
+import os
+import re
+import shutil
+import subprocess
+from collections import defaultdict
+
+import pytest
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+LIB = os.path.join(ROOT, "kungfu_amd", "libkungfu_amd.so")
+OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+
+# reduce_kernel<T, OP, EPI, KC, BLOCK, UNROLL, LOADNT, STPLAIN>: the product
+# instantiations are LOADNT = 1, STPLAIN = 0; the other policy combinations,
+# and unroll 1/2/8 of the fp32 SUM k = 2 kernel, exist only for
+# tools/tune_reduce.py (kf_set_geometry). (At unroll 1 the compiler merges the
+# full-tile and ragged-tile stores into one and drops its nt bit.)
+PRODUCT_REDUCE = re.compile(r"^_ZN2kf13reduce_kernelI.*ELi256ELi\d+ELi1ELi0EEEv")
+TUNING_ONLY = re.compile(r"^_ZN2kf13reduce_kernelIfLi0ELi0ELi2ELi256ELi[128]E")
+STREAMING = ("_ZN2kf20reduce_spread_kernelI", "_ZN2kf10sma_kernelI")
+# the scalar head/tail and the ragged last tile are the only divergent code
+MAX_EXEC_BRANCHES = 6
+
+
+@pytest.fixture(scope="module")
+def kernels(tmp_path_factory):
+    if not os.path.exists(OBJDUMP):
+        pytest.skip("llvm-objdump not found")
+    if not os.path.exists(LIB):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "kungfu_amd", "csrc")],
+                       check=True)
+    d = tmp_path_factory.mktemp("isa")
+    lib = d / "lib.so"
+    shutil.copy(LIB, lib)
+    # writes the bundled code objects next to its input: hence the copy
+    subprocess.run([OBJDUMP, "--offloading", str(lib)], check=True, capture_output=True)
+    objs = sorted(p for p in d.iterdir() if p.name.endswith("gfx950"))
+    assert objs, "no gfx950 code object in the library"
+    body = defaultdict(list)
+    for o in objs:
+        asm = subprocess.run([OBJDUMP, "-d", str(o)], check=True, capture_output=True,
+                             text=True).stdout
+        name = None
+        for line in asm.splitlines():
+            m = re.match(r"^[0-9a-f]+ <(.+)>:$", line)
+            if m:
+                name = m.group(1)
+            elif name and line.strip():
+                body[name].append(line.split("//")[0].strip())
+            else:
+                name = None
+    return body
+
+
+def product_kernels(kernels):
+    return {k: v for k, v in kernels.items()
+            if (PRODUCT_REDUCE.match(k) and not TUNING_ONLY.match(k)) or k.startswith(STREAMING)}
+
+
+def test_product_kernels_found(kernels):
+    ks = product_kernels(kernels)
+    # 10 dtypes x ops x k forms, the peers fold and the SMA blend
+    assert sum(1 for k in ks if k.startswith("_ZN2kf13reduce_kernel")) >= 100
+    assert any(k.startswith("_ZN2kf13reduce_kernelIaLi0E") for k in ks)  # i8 SUM
+    assert any(k.startswith("_ZN2kf13reduce_kernelINS_6bf16_t") for k in ks)
+    assert any(k.startswith(STREAMING[0]) for k in ks)
+    assert any(k.startswith(STREAMING[1]) for k in ks)
+
+
+def test_streaming_loads_and_stores_are_nontemporal(kernels):
+    bad = []
+    for name, lines in product_kernels(kernels).items():
+        for ins in lines:
+            if ins.startswith(("global_load_dwordx4", "global_store_dwordx4")):
+                if not re.search(r"\bnt\b", ins):
+                    bad.append((name, ins))
+                    break
+    assert not bad, bad[:5]
+
+
+def test_no_per_element_branches(kernels):
+    bad = []
+    for name, lines in product_kernels(kernels).items():
+        n = sum(1 for ins in lines if ins.startswith("s_and_saveexec"))
+        if n > MAX_EXEC_BRANCHES:
+            bad.append((name, n))
+    assert not bad, bad[:5]
