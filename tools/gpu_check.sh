@@ -2,7 +2,7 @@
 # One guarded GPU session: parity tests, smoke, bench, rocprofv3 kernel trace,
 # PMC traffic passes. Each GPU step has its own time limit; a crash/timeout
 # (anything but a plain test failure) stops everything after it.
-#   usage: bash tools/gpu_check.sh [tag] [extra steps: tune|big|rates]
+#   usage: bash tools/gpu_check.sh [tag] [extra steps: tune|big|rates|rates_prof]
 set -u
 TAG=${1:-r01}
 shift || true
@@ -39,6 +39,8 @@ for extra in "$@"; do
   case $extra in
     tune) step tune 600 python tools/tune_reduce.py || exit $? ;;
     rates) step kernel_rates 600 python tools/kernel_rates.py || exit $? ;;
+    rates_prof) step kernel_rates_prof 600 rocprofv3 --kernel-trace --stats -T -d "$OUT/prof_rates" \
+              -o rates --output-format csv -- python3 tools/kernel_rates.py || exit $? ;;
     big)  step tune_big 600 python tools/tune_reduce.py --elems 268435456 --rounds 3 \
               --unroll 1,4 --grid 4096,1048576 --loadnt 0,1 --stplain 0 || exit $? ;;
   esac
