@@ -77,7 +77,8 @@ def parse():
                     help="rehearsal only: put every rank on this GPU")
     ap.add_argument("--no-extra", action="store_true",
                     help="N>1: skip the C4/C5/P2P sub-benchmarks")
-    ap.add_argument("--extras", default="c4,c5,c3_ar,c3_p2p,c3_p2p_push,c3_p2p_hostbar,"
+    ap.add_argument("--extras", default="c3_per_bucket,c4,c5,c3_ar,c3_p2p,c3_p2p_push,"
+                                        "c3_p2p_hostbar,"
                                         "c4_p2p,c5_p2p",
                     help="N>1: which sub-benchmarks to run (comma list)")
     ap.add_argument("--extras-timeout", type=float, default=240.0,
@@ -427,6 +428,7 @@ def main():
         del allx, want
         if not _agree(ok, dev):
             raise SystemExit("C3 all-reduce parity check failed (N=2 bit-exact / N>2 bound)")
+        _progress(rank, "C3 parity ok; timing %d steps" % args.steps)
         gb.views[0].copy_(x)
         for _ in range(args.warmup):
             ex.all_reduce_(pieces, average=True)
@@ -444,9 +446,7 @@ def main():
         step_s = t.item() / args.steps
         value = world * s_bytes / step_s / 2**30
         busbw = 2 * (world - 1) / world * s_bytes / step_s / 1e9
-        # the same 64 buckets issued one RS/AG pair each (no fusion), beside
-        per_s = _timed(lambda: ex.all_reduce_(pieces, average=True, coalesce=False),
-                       min(args.steps, 20), 2, dev, world)
+        _progress(rank, "C3 %.3f ms per step" % (step_s * 1e3))
         out["collective"] = {
             "busbw_GBps": round(busbw, 2),
             "algbw_GiBps_per_gpu": round(s_bytes / step_s / 2**30, 3),
@@ -455,8 +455,6 @@ def main():
             "buckets": args.buckets,
             "fused": "contiguous ready buckets run as one RS -> /np -> AG "
                      "(the reference's nccl_fusion, sync_sgd.py:87-92)",
-            "per_bucket_ms_per_step": round(per_s * 1e3, 4),
-            "per_bucket_busbw_GBps": round(2 * (world - 1) / world * s_bytes / per_s / 1e9, 2),
         }
         workload = ("C3: S-SGD all-reduce of %d fp32 buckets (%d MiB) per rank, "
                     "fused: RCCL reduce-scatter -> HIP /np -> RCCL all-gather"
@@ -466,7 +464,9 @@ def main():
         dist.all_reduce(kt, op=dist.ReduceOp.MAX)
         kernel_s = kt.item()
         # the other multi-GPU configs of BASELINE.json, reported beside `value`
-        extra = (("c4", lambda: bench_c4(world, rank, dev, min(args.steps, 50), 5)),
+        extra = (("c3_per_bucket", lambda: bench_c3_per_bucket(world, dev, min(args.steps, 20),
+                                                               ex, pieces, s_bytes)),
+                 ("c4", lambda: bench_c4(world, rank, dev, min(args.steps, 50), 5)),
                  ("c5", lambda: bench_c5(world, rank, dev, min(args.steps, 50), 5)),
                  ("c3_ar", lambda: bench_c3_ar(world, rank, dev, min(args.steps, 50), 5, n, x)),
                  # last: the experimental peer-to-peer paths
@@ -639,6 +639,20 @@ def _exchange(kind):
         return PeerExchange(timeout_s=5.0)
     from kungfu_amd.collective import Exchange
     return Exchange()
+
+
+def bench_c3_per_bucket(world, dev, steps, ex, pieces, s_bytes):
+    """C3's buckets issued one RS -> /np -> AG each (no fusion), beside the
+    fused primary. A sub-benchmark (under the --extras-timeout watchdog): with
+    gloo and 4 ranks sharing one GPU, these 64 outstanding async collectives
+    were seen to stall (profiles/r01/README.md), and nothing may stall before
+    the primary line is safe."""
+    per_s = _timed(lambda: ex.all_reduce_(pieces, average=True, coalesce=False),
+                   steps, 2, dev, world)
+    return {"workload": "C3's %d buckets, one RS -> HIP /np -> AG each (no fusion)"
+                        % len(pieces),
+            "ms_per_step": round(per_s * 1e3, 4),
+            "busbw_GBps": round(2 * (world - 1) / world * s_bytes / per_s / 1e9, 2)}
 
 
 def bench_c4(world, rank, dev, steps, warmup, exchange="rccl"):
