@@ -288,6 +288,29 @@ def test_coalesced_equals_per_bucket(world):
     run_world("body_coalesced_equals_per_bucket", world)
 
 
+def body_per_bucket_many_outstanding(rank, world, use_gpu):
+    # bench.py's c3_per_bucket shape: 64 buckets, all 64 reduce-scatters in
+    # flight before the first wait, then 64 all-gathers in flight
+    from kungfu_amd.collective import Exchange, GradBuckets
+    ex = Exchange(epilogue=_epilogue(use_gpu))
+    n = 64 * 4096 * world
+    a = GradBuckets([n], torch.float32, torch.device("cpu"), world, n_buckets=64)
+    b = GradBuckets([n], torch.float32, torch.device("cpu"), world, n_buckets=64)
+    x = torch.from_numpy(_inputs(rank, n))
+    a.views[0].copy_(x)
+    b.views[0].copy_(x)
+    assert len(a.buckets) == 64
+    for _ in range(3):
+        ex.all_reduce_(a.buckets, average=True, coalesce=False)
+        ex.all_reduce_(b.buckets, average=True, coalesce=True)
+    assert torch.allclose(a.views[0], b.views[0], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("world", [4])
+def test_per_bucket_many_outstanding(world):
+    run_world("body_per_bucket_many_outstanding", world)
+
+
 def body_torch_ops(rank, world, use_gpu):
     # kungfu.torch.ops surface (srcs/python/kungfu/torch/ops/collective.py)
     from kungfu_amd.torch import ops
