@@ -108,6 +108,7 @@ enum KF_Status {
     KF_ERR_IO          = 6, /* socket read/write failed               */
     KF_ERR_PROTO       = 7, /* rchannel framing/length/token mismatch  */
     KF_ERR_TIMEOUT     = 8, /* a device-side peer barrier gave up      */
+    KF_ERR_RCCL        = 9, /* librccl missing or an RCCL call failed  */
 };
 
 /* Largest k accepted by kf_bucket_reduce*. */
@@ -132,6 +133,18 @@ int kf_bucket_reduce_avg(const void *const *inputs, int k, void *out, size_t n,
 /* In-place scale of an already-summed shard: x[i] = x[i] / np (the step
  * between RCCL reduce-scatter and all-gather). float types only. */
 int kf_bucket_div(void *x, size_t n, KungFu_Datatype dt, int np, void *stream);
+
+/* Many independent buckets in one launch per 16 of them: bucket b is
+ *   outs[b][i] = fold(inputs[b*k + 0][i], ..., inputs[b*k + k-1][i]), i < counts[b]
+ * with the same arithmetic as kf_bucket_reduce (np == 0) or
+ * kf_bucket_reduce_avg (np > 0: SUM then / np, float types). A bucket whose
+ * pointers do not share one 16-B residue, and MIN / MAX / PROD, get a launch
+ * each; k == 1 with np == 0 is a copy per bucket. For the per-bucket steps of
+ * an exchange (every shard's /np, every bucket's fold of the received shards),
+ * where one launch per 4 MiB bucket costs more than the bucket's HBM time. */
+int kf_bucket_reduce_batch(const void *const *inputs, int k, void *const *outs,
+                           const size_t *counts, int nb, KungFu_Datatype dt, KungFu_Op op,
+                           int np, void *stream);
 
 /* SMA epilogue (sma_sgd.py:60-65):
  *   v[i] = fl(fl(c1 * v[i]) + fl(c2 * fl(sum[i] / np)))
@@ -372,6 +385,96 @@ int kf_signal_free(void *ptr, int host);
 int kf_peer_barrier(void *const *sigs, int world, int rank, uint64_t epoch,
                     uint32_t timeout_us, void *status, void *stream);
 const char *kf_p2p_last_error(void);
+
+/* ---- multi-GPU exchange over RCCL (kungfu_amd/csrc/kf_exchange.hip) ------
+ *
+ * The reference's GPU collective, srcs/cpp/src/nccl/gpu_collective.cpp:
+ * a communicator per process built from a unique id that rank 0 creates and
+ * KungFu broadcasts (new_global, gpu_collective.cpp:190-200), then
+ * ncclAllReduce per tensor with a stream sync after each call (:151-165).
+ * Here the all-reduce of a bucket is split so the sum runs where the
+ * north_star puts it:
+ *   KF_ALGO_REDUCE_SCATTER  ncclReduceScatter -> HIP /np on the shard
+ *                           (kf_bucket_div) -> in-place ncclAllGather;
+ *   KF_ALGO_ALL_TO_ALL      ncclAllToAll of the shards -> HIP fold of the
+ *                           world received shards IN RANK ORDER (/np fused)
+ *                           -> in-place ncclAllGather. The sum is the HIP
+ *                           k-input kernel, so the bits are the oracle's
+ *                           reduce over ranks 0..world-1 for every dtype —
+ *                           bf16 with fp32 accumulation and one rounding,
+ *                           fp16 rounded per hop — equal to the P2P path;
+ *                           same xGMI bytes as the reduce-scatter.
+ *   KF_ALGO_AUTO            reduce-scatter for integers and f32/f64 SUM
+ *                           (RCCL's own order; integers exact), all-to-all
+ *                           for f16/bf16 and float MIN/MAX (the build's
+ *                           defined semantics) and for u16/i16.
+ * A count that does not split into world shards sends its last count % world
+ * elements through an all-gather and the same rank-order fold. Everything
+ * is queued on the caller's stream (no host sync, like RCCL); calls on one
+ * exchange must be issued in the same order on every rank, and if they use
+ * different streams the exchange orders its workspace between them.
+ */
+#define KF_UNIQUE_ID_BYTES 128
+enum KF_ExchangeAlgo {
+    KF_ALGO_AUTO           = 0,
+    KF_ALGO_REDUCE_SCATTER = 1,
+    KF_ALGO_ALL_TO_ALL     = 2,
+};
+#pragma GCC visibility pop
+typedef struct kf_exchange kf_exchange_t; /* opaque */
+#pragma GCC visibility push(default)
+
+/* ncclGetUniqueId (rank 0 calls it, gpu_collective.cpp:196). */
+int kf_exchange_unique_id(void *id);
+/* Broadcast rank 0's id[KF_UNIQUE_ID_BYTES] to every peer of a session, in
+ * place (Peer::Broadcast of the id, gpu_collective.cpp:197-198). */
+int kf_exchange_share_id(kf_session_t *s, void *id);
+/* ncclCommInitRank on HIP device `device` (the caller's current device is
+ * restored). NULL on failure (kf_exchange_last_error). */
+kf_exchange_t *kf_exchange_create(const void *id, int rank, int world, int device);
+/* gpu_collective::new_global: id from rank 0, shared over the session, then
+ * kf_exchange_create(id, rank, size, device). */
+kf_exchange_t *kf_exchange_create_session(kf_session_t *s, int rank, int world, int device);
+/* recv = all-reduce(send) (op; average != 0: SUM then / world, float types).
+ * send == recv is in place. */
+int kf_exchange_all_reduce(kf_exchange_t *ex, const void *send, void *recv, size_t count,
+                           KungFu_Datatype dt, KungFu_Op op, int average, int algo,
+                           void *stream);
+/* nb buckets in one call, each reduced as by kf_exchange_all_reduce: one
+ * grouped RCCL launch per phase and one batched HIP launch
+ * (kf_bucket_reduce_batch) for all shard epilogues / folds. */
+int kf_exchange_all_reduce_batch(kf_exchange_t *ex, const void *const *sends, void *const *recvs,
+                                 const size_t *counts, int nb, KungFu_Datatype dt, KungFu_Op op,
+                                 int average, int algo, void *stream);
+/* SMA (sma_sgd.py:60-65) for nb variable buckets: sums[b] = all-reduce-sum of
+ * vs[b], then vs[b] = (1 - alpha) vs[b] + alpha sums[b] / world
+ * (kf_sma_blend). sums[b] are caller workspaces of counts[b] elements. */
+int kf_exchange_sma_batch(kf_exchange_t *ex, void *const *vs, void *const *sums,
+                          const size_t *counts, int nb, KungFu_Datatype dt, double alpha,
+                          int algo, void *stream);
+/* Ordered issue of concurrently produced all-reduces, the reference's
+ * NCCLScheduler / LinearExecutor (srcs/cpp/src/nccl/scheduler.cpp:8-130):
+ * begin_step fixes this step's names in an order every rank shares;
+ * kf_exchange_start may be called for them in any order from any thread, and
+ * the exchange's thread issues them strictly in that order (a name waits for
+ * every name before it). With auto_order, the second step adopts rank 0's
+ * arrival order of the first (broadcast over the communicator, as
+ * NCCLScheduler::Reset does with Peer::Broadcast). done(status, arg) runs
+ * when that all-reduce has completed on the device. */
+int kf_exchange_begin_step(kf_exchange_t *ex, const char *const *names, int n, int auto_order);
+int kf_exchange_start(kf_exchange_t *ex, const char *name, const void *send, void *recv,
+                      size_t count, KungFu_Datatype dt, KungFu_Op op, int average, int algo,
+                      void *stream, kf_done_fn done, void *arg);
+/* Wait until every started all-reduce of the step has completed; the first
+ * failure, else KF_OK. *order (if not NULL, n entries) receives the issue
+ * order used. */
+int kf_exchange_wait_all(kf_exchange_t *ex, int32_t *order);
+/* KF_OK, or KF_ERR_RCCL after an asynchronous RCCL failure
+ * (ncclCommGetAsyncError). */
+int kf_exchange_check(kf_exchange_t *ex);
+int kf_exchange_info(kf_exchange_t *ex, int *rank, int *world, int *device);
+void kf_exchange_destroy(kf_exchange_t *ex);
+const char *kf_exchange_last_error(void);
 
 #pragma GCC visibility pop
 

@@ -62,6 +62,21 @@ EXPORTED = (
     "kf_signal_free",
     "kf_peer_barrier",
     "kf_p2p_last_error",
+    "kf_bucket_reduce_batch",
+    "kf_exchange_unique_id",
+    "kf_exchange_share_id",
+    "kf_exchange_create",
+    "kf_exchange_create_session",
+    "kf_exchange_all_reduce",
+    "kf_exchange_all_reduce_batch",
+    "kf_exchange_sma_batch",
+    "kf_exchange_begin_step",
+    "kf_exchange_start",
+    "kf_exchange_wait_all",
+    "kf_exchange_check",
+    "kf_exchange_info",
+    "kf_exchange_destroy",
+    "kf_exchange_last_error",
 )
 
 STATUS = {
@@ -74,6 +89,7 @@ STATUS = {
     6: "KF_ERR_IO",
     7: "KF_ERR_PROTO",
     8: "KF_ERR_TIMEOUT",
+    9: "KF_ERR_RCCL",
 }
 
 MAX_INPUTS = 16
@@ -228,6 +244,42 @@ def load():
     lib.kf_peer_barrier.restype = c_int
     lib.kf_p2p_last_error.argtypes = []
     lib.kf_p2p_last_error.restype = ctypes.c_char_p
+    P = ctypes.POINTER
+    lib.kf_bucket_reduce_batch.argtypes = [P(c_void_p), c_int, P(c_void_p), P(c_size_t), c_int,
+                                           c_int, c_int, c_int, c_void_p]
+    lib.kf_bucket_reduce_batch.restype = c_int
+    lib.kf_exchange_unique_id.argtypes = [c_void_p]
+    lib.kf_exchange_unique_id.restype = c_int
+    lib.kf_exchange_share_id.argtypes = [c_void_p, c_void_p]
+    lib.kf_exchange_share_id.restype = c_int
+    lib.kf_exchange_create.argtypes = [c_void_p, c_int, c_int, c_int]
+    lib.kf_exchange_create.restype = c_void_p
+    lib.kf_exchange_create_session.argtypes = [c_void_p, c_int, c_int, c_int]
+    lib.kf_exchange_create_session.restype = c_void_p
+    lib.kf_exchange_all_reduce.argtypes = [c_void_p, c_void_p, c_void_p, c_size_t, c_int, c_int,
+                                           c_int, c_int, c_void_p]
+    lib.kf_exchange_all_reduce.restype = c_int
+    lib.kf_exchange_all_reduce_batch.argtypes = [c_void_p, P(c_void_p), P(c_void_p), P(c_size_t),
+                                                 c_int, c_int, c_int, c_int, c_int, c_void_p]
+    lib.kf_exchange_all_reduce_batch.restype = c_int
+    lib.kf_exchange_sma_batch.argtypes = [c_void_p, P(c_void_p), P(c_void_p), P(c_size_t), c_int,
+                                          c_int, ctypes.c_double, c_int, c_void_p]
+    lib.kf_exchange_sma_batch.restype = c_int
+    lib.kf_exchange_begin_step.argtypes = [c_void_p, P(ctypes.c_char_p), c_int, c_int]
+    lib.kf_exchange_begin_step.restype = c_int
+    lib.kf_exchange_start.argtypes = [c_void_p, ctypes.c_char_p, c_void_p, c_void_p, c_size_t,
+                                      c_int, c_int, c_int, c_int, c_void_p, DONE_FN, c_void_p]
+    lib.kf_exchange_start.restype = c_int
+    lib.kf_exchange_wait_all.argtypes = [c_void_p, P(ctypes.c_int32)]
+    lib.kf_exchange_wait_all.restype = c_int
+    lib.kf_exchange_check.argtypes = [c_void_p]
+    lib.kf_exchange_check.restype = c_int
+    lib.kf_exchange_info.argtypes = [c_void_p, P(c_int), P(c_int), P(c_int)]
+    lib.kf_exchange_info.restype = c_int
+    lib.kf_exchange_destroy.argtypes = [c_void_p]
+    lib.kf_exchange_destroy.restype = None
+    lib.kf_exchange_last_error.argtypes = []
+    lib.kf_exchange_last_error.restype = ctypes.c_char_p
     _lib = lib
     return lib
 
@@ -235,8 +287,9 @@ def load():
 def check(rc, what):
     if rc != 0:
         lib = load()
-        detail = (lib.kf_session_last_error().decode() or lib.kf_last_error().decode()
-                  or lib.kf_ingest_last_error().decode() or lib.kf_p2p_last_error().decode())
+        detail = (lib.kf_exchange_last_error().decode() or lib.kf_session_last_error().decode()
+                  or lib.kf_last_error().decode() or lib.kf_ingest_last_error().decode()
+                  or lib.kf_p2p_last_error().decode())
         raise KungFuAMDError("%s failed: %s (%s)" % (what, STATUS.get(rc, rc), detail))
 
 

@@ -16,6 +16,14 @@ over xGMI, one process per GPU. Buckets are issued back to back so the
 epilogue of bucket i overlaps the reduce-scatter of bucket i+1 (all RS on the
 RCCL stream first, each AG queued behind its own epilogue).
 
+For f16/bf16 (and float MIN/MAX) step 1 is instead an all-to-all of the
+shards followed by the HIP k-input fold of the `world` received shards in rank
+order (algo "a2a"): RCCL's reduce-scatter would add in its own order and, for
+bf16, round to bf16 at every hop, while the build defines bf16 as fp32
+accumulation with one rounding (the oracle's semantics and the P2P path's).
+Same xGMI bytes as the reduce-scatter; the bits no longer depend on the
+transport (kungfu_amd/csrc/kf_exchange.hip does the same natively).
+
 The epilogue runs through ``kungfu_amd.ops`` (HIP kernels). It is injectable
 only so the orchestration can be exercised over gloo on CPU in tests; the
 product default is the HIP path and it raises on CPU tensors.
@@ -43,6 +51,12 @@ class HipEpilogue:
 
     def div_(self, x, np_):
         return ops.bucket_div_(x, np_)
+
+    def fold_(self, inputs, out, op, np_):
+        """out = left fold of inputs (rank order); np_ > 0: SUM then / np_."""
+        if np_:
+            return ops.bucket_reduce_avg(inputs, np_, out=out)
+        return ops.bucket_reduce(inputs, out=out, op=op)
 
     def sma_blend_(self, v, summed, np_, alpha):
         return ops.sma_blend_(v, summed, np_, alpha)
@@ -78,6 +92,21 @@ def coalesce_runs(buckets):
     return runs
 
 
+def resolve_algo(algo, dtype, op, world):
+    """"rs" (RCCL reduce-scatter) or "a2a" (all-to-all + HIP rank-order fold)
+    for one bucket dtype; "auto" keeps RCCL's reduce-scatter where its order
+    cannot change the defined result's meaning (integers; f32/f64 SUM, the
+    north_star's path) and folds on the GPU where the build defines the
+    arithmetic (f16/bf16, float MIN/MAX; kf_exchange.hip resolve_algo)."""
+    if algo in ("rs", "a2a"):
+        return algo
+    if algo != "auto":
+        raise ValueError("algo must be 'auto', 'rs' or 'a2a'")
+    own = dtype in (torch.float16, torch.bfloat16) or (
+        dtype.is_floating_point and op in (OP.MIN, OP.MAX))
+    return "a2a" if own and world <= 16 else "rs"
+
+
 def padded_count(count, world, itemsize):
     """Smallest length >= count that splits into `world` aligned shards."""
     unit = world * max(1, ALIGN_BYTES // itemsize)
@@ -87,11 +116,13 @@ def padded_count(count, world, itemsize):
 class Exchange:
     """One process group, its shard workspaces and the epilogue."""
 
-    def __init__(self, group=None, epilogue=None):
+    def __init__(self, group=None, epilogue=None, algo="auto"):
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.epilogue = epilogue if epilogue is not None else HipEpilogue()
+        self.algo = algo
+        resolve_algo(algo, torch.float32, OP.SUM, self.world)  # validates
         self._ws = {}
 
     def _workspace(self, key, n, like):
@@ -145,17 +176,29 @@ class Exchange:
         works = []
         for i, b in enumerate(buckets):
             shard = self._workspace((key, "rs", i), b.numel() // self.world, b)
-            works.append(dist.reduce_scatter_tensor(shard, b, op=_RED_OPS[red],
-                                                    group=self.group, async_op=True))
+            works.append(self._scatter(b, shard, red, (key, "a2a", i)))
             shards.append(shard)
         gathers = []
-        for b, shard, w in zip(buckets, shards, works):
+        for b, shard, (w, recv) in zip(buckets, shards, works):
             w.wait()
-            if average:
+            if recv is not None:  # the rank-order fold of the received shards
+                self.epilogue.fold_(list(recv.chunk(self.world)), shard, red,
+                                    self.world if average else 0)
+            elif average:
                 self.epilogue.div_(shard, self.world)
             gathers.append(dist.all_gather_into_tensor(b, shard, group=self.group,
                                                        async_op=True))
         return _Handle(gathers)
+
+    def _scatter(self, b, shard, red, key):
+        """Step 1 for one bucket: (work, None) for RCCL's reduce-scatter into
+        `shard`, or (work, recv) for the all-to-all whose `recv` holds the
+        `world` shards (rank order) still to be folded."""
+        if resolve_algo(self.algo, b.dtype, red, self.world) == "rs":
+            return (dist.reduce_scatter_tensor(shard, b, op=_RED_OPS[red], group=self.group,
+                                               async_op=True), None)
+        recv = self._workspace(key, b.numel(), b)
+        return dist.all_to_all_single(recv, b, group=self.group, async_op=True), recv
 
     def sma_(self, buckets, alpha):
         """SMA over flat variable buckets (sma_sgd.py:60-65): each rank's v
@@ -178,11 +221,12 @@ class Exchange:
         rs = []
         for i, b in enumerate(buckets):
             shard = self._workspace(("rs", i), b.numel() // self.world, b)
-            rs.append((shard, dist.reduce_scatter_tensor(
-                shard, b, op=dist.ReduceOp.SUM, group=self.group, async_op=True)))
+            rs.append((shard, self._scatter(b, shard, OP.SUM, ("a2a", i))))
         ags = []
-        for i, (b, (shard, w)) in enumerate(zip(buckets, rs)):
+        for i, (b, (shard, (w, recv))) in enumerate(zip(buckets, rs)):
             w.wait()
+            if recv is not None:
+                self.epilogue.fold_(list(recv.chunk(self.world)), shard, OP.SUM, 0)
             s = self._workspace(("sum", i), b.numel(), b)
             ags.append((s, dist.all_gather_into_tensor(s, shard, group=self.group,
                                                        async_op=True)))

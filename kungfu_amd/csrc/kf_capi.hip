@@ -289,6 +289,108 @@ int check_args(const void *const *inputs, int k, const void *out, size_t n)
     return KF_OK;
 }
 
+// ---------------------------------------------------------------------------
+// batch: nb buckets, one launch per kBatchSeg of them (kf_bucket_reduce_batch)
+// ---------------------------------------------------------------------------
+template <typename T, int OP, int EPI, int KC>
+int launch_batch_kc(const void *const *in, int k, void *const *outs, const size_t *counts,
+                    int nb, const Div &np, int npi, hipStream_t s)
+{
+    using S           = typename Elt<T>::S;
+    constexpr int V   = Vec<S>::N;
+    constexpr int U   = 4;
+    const size_t tile = static_cast<size_t>(kBlock) * U;
+    BatchArgs a;
+    a.nseg          = 0;
+    size_t blocks   = 0;
+    auto flush      = [&]() -> int {
+        if (a.nseg == 0) return KF_OK;
+        a.blk0[a.nseg] = static_cast<unsigned>(blocks);
+        reduce_batch_kernel<T, OP, EPI, KC, kBlock, U>
+            <<<static_cast<unsigned>(blocks), kBlock, 0, s>>>(a, k, np);
+        a.nseg = 0;
+        blocks = 0;
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return hip_fail(e, "reduce batch kernel launch");
+        return KF_OK;
+    };
+    for (int b = 0; b < nb; ++b) {
+        const size_t n = counts[b];
+        if (n == 0) continue;
+        const void *const *ptrs = in + static_cast<size_t>(b) * k;
+        const Plan p            = make_plan(ptrs, k, outs[b], n, sizeof(S));
+        if (!p.vec_ok) {  // residues differ: this bucket gets a launch of its own
+            int rc = launch_typed<T, OP, EPI>(ptrs, k, outs[b], n, npi, s, 0);
+            if (rc != KF_OK) return rc;
+            continue;
+        }
+        const size_t nedge = p.head + (n - p.head - p.nvec * V);
+        size_t nblk        = (p.nvec + tile - 1) / tile;
+        const size_t eblk  = (nedge + kBlock - 1) / kBlock;
+        if (nblk > static_cast<size_t>(geometry().grid_cap)) nblk = geometry().grid_cap;
+        if (nblk < eblk) nblk = eblk;
+        if (nblk < 1) nblk = 1;
+        if (blocks + nblk > 0xffffffffu) {
+            int rc = flush();
+            if (rc != KF_OK) return rc;
+        }
+        const int j = a.nseg;
+        for (int i = 0; i < kMaxInputs; ++i) a.in[j].p[i] = i < k ? ptrs[i] : nullptr;
+        a.out[j]  = outs[b];
+        a.n[j]    = n;
+        a.head[j] = p.head;
+        a.nvec[j] = p.nvec;
+        a.blk0[j] = static_cast<unsigned>(blocks);
+        blocks += nblk;
+        ++a.nseg;
+        if (a.nseg == kBatchSeg) {
+            int rc = flush();
+            if (rc != KF_OK) return rc;
+        }
+    }
+    return flush();
+}
+
+template <typename T, int OP, int EPI>
+int launch_batch(const void *const *in, int k, void *const *outs, const size_t *counts, int nb,
+                 int npi, hipStream_t s)
+{
+    const Div np = make_div(npi);
+    if (k == 1) return launch_batch_kc<T, OP, EPI, 1>(in, k, outs, counts, nb, np, npi, s);
+    if (k == 2) return launch_batch_kc<T, OP, EPI, 2>(in, k, outs, counts, nb, np, npi, s);
+    return launch_batch_kc<T, OP, EPI, 0>(in, k, outs, counts, nb, np, npi, s);
+}
+
+int dispatch_batch(const void *const *in, int k, void *const *outs, const size_t *counts, int nb,
+                   KungFu_Datatype dt, int np, hipStream_t s)
+{
+    // SUM only (plain for every dtype, / np for the float types)
+    if (np > 0) {
+        switch (dt) {
+        case KungFu_FLOAT16: return launch_batch<f16_t, OP_SUM, EPI_DIV>(in, k, outs, counts, nb, np, s);
+        case KungFu_FLOAT: return launch_batch<float, OP_SUM, EPI_DIV>(in, k, outs, counts, nb, np, s);
+        case KungFu_DOUBLE: return launch_batch<double, OP_SUM, EPI_DIV>(in, k, outs, counts, nb, np, s);
+        case KungFu_BFLOAT16: return launch_batch<bf16_t, OP_SUM, EPI_DIV>(in, k, outs, counts, nb, np, s);
+        default: return KF_ERR_DTYPE;
+        }
+    }
+    switch (dt) {
+    case KungFu_UINT8: return launch_batch<uint8_t, OP_SUM, EPI_NONE>(in, k, outs, counts, nb, 1, s);
+    case KungFu_UINT16: return launch_batch<uint16_t, OP_SUM, EPI_NONE>(in, k, outs, counts, nb, 1, s);
+    case KungFu_UINT32: return launch_batch<uint32_t, OP_SUM, EPI_NONE>(in, k, outs, counts, nb, 1, s);
+    case KungFu_UINT64: return launch_batch<uint64_t, OP_SUM, EPI_NONE>(in, k, outs, counts, nb, 1, s);
+    case KungFu_INT8: return launch_batch<int8_t, OP_SUM, EPI_NONE>(in, k, outs, counts, nb, 1, s);
+    case KungFu_INT16: return launch_batch<int16_t, OP_SUM, EPI_NONE>(in, k, outs, counts, nb, 1, s);
+    case KungFu_INT32: return launch_batch<int32_t, OP_SUM, EPI_NONE>(in, k, outs, counts, nb, 1, s);
+    case KungFu_INT64: return launch_batch<int64_t, OP_SUM, EPI_NONE>(in, k, outs, counts, nb, 1, s);
+    case KungFu_FLOAT16: return launch_batch<f16_t, OP_SUM, EPI_NONE>(in, k, outs, counts, nb, 1, s);
+    case KungFu_FLOAT: return launch_batch<float, OP_SUM, EPI_NONE>(in, k, outs, counts, nb, 1, s);
+    case KungFu_DOUBLE: return launch_batch<double, OP_SUM, EPI_NONE>(in, k, outs, counts, nb, 1, s);
+    case KungFu_BFLOAT16: return launch_batch<bf16_t, OP_SUM, EPI_NONE>(in, k, outs, counts, nb, 1, s);
+    default: return KF_ERR_DTYPE;
+    }
+}
+
 template <typename T, typename C>
 int launch_sma(void *v, const void *sum, size_t n, int np, C c1, C c2,
                hipStream_t s)
@@ -567,6 +669,44 @@ int kf_bucket_reduce_peers(const void *const *inputs, int k, void *out, size_t n
         return KF_OK;
     }
     return dispatch_none(inputs, k, out, n, dt, op, s, 0, LM_SPREAD);
+}
+
+int kf_bucket_reduce_batch(const void *const *inputs, int k, void *const *outs,
+                           const size_t *counts, int nb, KungFu_Datatype dt, KungFu_Op op,
+                           int np, void *stream)
+{
+    if (nb < 0 || k < 1 || k > KF_MAX_INPUTS || np < 0) return KF_ERR_ARG;
+    if (nb == 0) return KF_OK;
+    if (!inputs || !outs || !counts) return KF_ERR_ARG;
+    const int sz = type_size(dt);
+    if (sz == 0 || dt == KungFu_BOOL) return KF_ERR_DTYPE;
+    if (op < KungFu_SUM || op > KungFu_PROD) return KF_ERR_OP;
+    if ((dt == KungFu_FLOAT16 || np > 0) && op != KungFu_SUM) return KF_ERR_OP;
+    if (np > 0 && !is_float(dt)) return KF_ERR_DTYPE;
+    for (int b = 0; b < nb; ++b) {
+        if (counts[b] == 0) continue;
+        int rc = check_args(inputs + static_cast<size_t>(b) * k, k, outs[b], counts[b]);
+        if (rc != KF_OK) return rc;
+    }
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (k == 1 && np == 0) {  // a copy per bucket, as kf_bucket_reduce
+        for (int b = 0; b < nb; ++b) {
+            if (counts[b] && outs[b] != inputs[b]) {
+                KF_HIP(hipMemcpyAsync(outs[b], inputs[b], counts[b] * sz, hipMemcpyDeviceToDevice, s));
+            }
+        }
+        return KF_OK;
+    }
+    if (op != KungFu_SUM) {  // MIN / MAX / PROD: one launch per bucket
+        for (int b = 0; b < nb; ++b) {
+            if (counts[b] == 0) continue;
+            int rc = dispatch_none(inputs + static_cast<size_t>(b) * k, k, outs[b], counts[b], dt,
+                                   op, s);
+            if (rc != KF_OK) return rc;
+        }
+        return KF_OK;
+    }
+    return dispatch_batch(inputs, k, outs, counts, nb, dt, np, s);
 }
 
 int kf_set_geometry(int unroll, int grid_cap, int loadnt, int stplain)

@@ -1,0 +1,785 @@
+// kf_exchange.hip — the multi-GPU bucket exchange over RCCL behind the C ABI
+// (include/kungfu_amd.h, "multi-GPU exchange").
+//
+// Reference: srcs/cpp/src/nccl/gpu_collective.cpp. There, one communicator per
+// process is built from an ncclUniqueId that rank 0 creates and KungFu
+// broadcasts (new_global, :190-200), and every tensor goes through
+// ncclAllReduce followed by a stream sync (:151-165); the TF ops order the
+// calls across ranks with NCCLScheduler (srcs/cpp/src/nccl/scheduler.cpp).
+//
+// Here a bucket's all-reduce is split so that the element-wise sum is the
+// build's HIP kernel where the semantics call for it (north_star: RCCL
+// reduce-scatter + all-gather over xGMI):
+//   reduce-scatter algo: ncclReduceScatter -> kf_bucket_div on the shard ->
+//                        in-place ncclAllGather;
+//   all-to-all algo:     ncclAllToAll of the shards -> HIP k-input fold of
+//                        the received shards in rank order (/np fused) ->
+//                        in-place ncclAllGather. Same xGMI bytes as the
+//                        reduce-scatter ((w-1)/w of the bucket out and in per
+//                        rank), one extra HBM pass over the received shards,
+//                        and the result is the oracle's rank-order fold for
+//                        every dtype (bf16: fp32 accumulation, one rounding).
+// Many buckets go in ONE call: every phase is one ncclGroupStart/End (RCCL
+// fuses the group into one launch) and all shard epilogues are one batched
+// HIP launch (kf_bucket_reduce_batch), so 64 x 4 MiB buckets cost 3 launches.
+//
+// librccl is opened at run time (dlopen "librccl.so.1"): the B1 drop-in does
+// not need it, and in a process where torch already loaded its RCCL (same
+// soname) both use that one library.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <map>
+#include <mutex>
+#include <numeric>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "kungfu_amd.h"
+
+// kf_session.hip (library-internal)
+int kf_session_device_mode_internal(const kf_session_t *s);
+
+namespace
+{
+thread_local std::string t_ex_error;
+
+int fail(int rc, const std::string &msg)
+{
+    t_ex_error = msg;
+    return rc;
+}
+
+int hip_fail(hipError_t e, const char *what)
+{
+    return fail(KF_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define KF_HIP(call)                                                           \
+    do {                                                                       \
+        hipError_t e_ = (call);                                                \
+        if (e_ != hipSuccess) return hip_fail(e_, #call);                      \
+    } while (0)
+
+// ---------------------------------------------------------------------------
+// librccl, resolved at run time
+// ---------------------------------------------------------------------------
+struct Rccl {
+    bool ok = false;
+    std::string why;
+    decltype(&::ncclGetUniqueId) GetUniqueId             = nullptr;
+    decltype(&::ncclCommInitRank) CommInitRank           = nullptr;
+    decltype(&::ncclCommDestroy) CommDestroy             = nullptr;
+    decltype(&::ncclCommAbort) CommAbort                 = nullptr;
+    decltype(&::ncclCommGetAsyncError) CommGetAsyncError = nullptr;
+    decltype(&::ncclReduceScatter) ReduceScatter         = nullptr;
+    decltype(&::ncclAllGather) AllGather                 = nullptr;
+    decltype(&::ncclAllToAll) AllToAll                   = nullptr;
+    decltype(&::ncclBroadcast) Broadcast                 = nullptr;
+    decltype(&::ncclGroupStart) GroupStart               = nullptr;
+    decltype(&::ncclGroupEnd) GroupEnd                   = nullptr;
+    decltype(&::ncclGetErrorString) GetErrorString       = nullptr;
+};
+
+const Rccl &rccl()
+{
+    static const Rccl r = [] {
+        Rccl x;
+        void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) {
+            const char *e = dlerror();
+            x.why         = std::string("dlopen librccl.so.1: ") + (e ? e : "?");
+            return x;
+        }
+#define KF_LOAD(field, sym)                                                    \
+    x.field = reinterpret_cast<decltype(x.field)>(dlsym(h, #sym));             \
+    if (!x.field) {                                                            \
+        x.why = "librccl.so.1 lacks " #sym;                                    \
+        return x;                                                              \
+    }
+        KF_LOAD(GetUniqueId, ncclGetUniqueId)
+        KF_LOAD(CommInitRank, ncclCommInitRank)
+        KF_LOAD(CommDestroy, ncclCommDestroy)
+        KF_LOAD(CommAbort, ncclCommAbort)
+        KF_LOAD(CommGetAsyncError, ncclCommGetAsyncError)
+        KF_LOAD(ReduceScatter, ncclReduceScatter)
+        KF_LOAD(AllGather, ncclAllGather)
+        KF_LOAD(AllToAll, ncclAllToAll)
+        KF_LOAD(Broadcast, ncclBroadcast)
+        KF_LOAD(GroupStart, ncclGroupStart)
+        KF_LOAD(GroupEnd, ncclGroupEnd)
+        KF_LOAD(GetErrorString, ncclGetErrorString)
+#undef KF_LOAD
+        x.ok = true;
+        return x;
+    }();
+    return r;
+}
+
+int nccl_fail(ncclResult_t r, const char *what)
+{
+    return fail(KF_ERR_RCCL, std::string(what) + ": " + rccl().GetErrorString(r));
+}
+
+#define KF_NCCL(call)                                                          \
+    do {                                                                       \
+        ncclResult_t r_ = (call);                                              \
+        if (r_ != ncclSuccess) return nccl_fail(r_, #call);                    \
+    } while (0)
+
+int need_rccl()
+{
+    if (!rccl().ok) return fail(KF_ERR_RCCL, rccl().why);
+    return KF_OK;
+}
+
+// The caller's device is restored after every entry point.
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int d)
+    {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != d) (void)hipSetDevice(d);
+    }
+    ~DeviceGuard()
+    {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+int tsize(KungFu_Datatype dt)
+{
+    switch (dt) {
+    case KungFu_UINT8: case KungFu_INT8: return 1;
+    case KungFu_UINT16: case KungFu_INT16: case KungFu_FLOAT16: case KungFu_BFLOAT16: return 2;
+    case KungFu_UINT32: case KungFu_INT32: case KungFu_FLOAT: return 4;
+    case KungFu_UINT64: case KungFu_INT64: case KungFu_DOUBLE: return 8;
+    default: return 0;
+    }
+}
+
+bool is_float(KungFu_Datatype dt)
+{
+    return dt == KungFu_FLOAT16 || dt == KungFu_BFLOAT16 || dt == KungFu_FLOAT ||
+           dt == KungFu_DOUBLE;
+}
+
+// dtypes RCCL can reduce (gpu_collective.cpp:60-73 maps int32/f16/f32)
+bool nccl_type(KungFu_Datatype dt, ncclDataType_t *t)
+{
+    switch (dt) {
+    case KungFu_UINT8: *t = ncclUint8; return true;
+    case KungFu_INT8: *t = ncclInt8; return true;
+    case KungFu_UINT32: *t = ncclUint32; return true;
+    case KungFu_INT32: *t = ncclInt32; return true;
+    case KungFu_UINT64: *t = ncclUint64; return true;
+    case KungFu_INT64: *t = ncclInt64; return true;
+    case KungFu_FLOAT16: *t = ncclFloat16; return true;
+    case KungFu_FLOAT: *t = ncclFloat32; return true;
+    case KungFu_DOUBLE: *t = ncclFloat64; return true;
+    case KungFu_BFLOAT16: *t = ncclBfloat16; return true;
+    default: return false;  // u16 / i16: no RCCL reduction type
+    }
+}
+
+ncclRedOp_t nccl_op(KungFu_Op op)
+{
+    switch (op) {
+    case KungFu_MIN: return ncclMin;
+    case KungFu_MAX: return ncclMax;
+    case KungFu_PROD: return ncclProd;
+    default: return ncclSum;
+    }
+}
+
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// the exchange
+// ---------------------------------------------------------------------------
+struct Task {
+    const void *send = nullptr;
+    void *recv       = nullptr;
+    size_t count     = 0;
+    KungFu_Datatype dt;
+    KungFu_Op op;
+    int average = 0, algo = 0;
+    hipStream_t stream = nullptr;
+    kf_done_fn done    = nullptr;
+    void *arg          = nullptr;
+    bool started       = false;
+};
+
+struct Done {
+    hipEvent_t ev;
+    kf_done_fn done;
+    void *arg;
+    int status;
+};
+
+struct kf_exchange {
+    ncclComm_t comm = nullptr;
+    int rank = 0, world = 1, device = 0;
+    std::mutex mu;  // one collective sequence at a time
+
+    // workspace (received shards, tails), ordered between streams by ws_ev
+    void *ws            = nullptr;
+    size_t ws_cap       = 0;
+    hipEvent_t ws_ev    = nullptr;
+    hipStream_t ws_last = nullptr;
+    bool ws_used        = false;
+    hipStream_t own     = nullptr;  // internal (order broadcast)
+
+    // NCCLScheduler / LinearExecutor
+    std::mutex smu;
+    std::condition_variable scv;
+    std::map<std::string, int> idx;
+    std::vector<int32_t> order, arrive, first_arrive;
+    std::vector<Task> tasks;
+    size_t issued = 0, completed = 0, ntasks = 0;
+    int steps      = 0;
+    int sstatus    = KF_OK;
+    bool stop      = false;
+    std::deque<Done> cq;
+    std::thread issuer, completer;
+
+    int ensure_ws(size_t bytes, hipStream_t s);
+    void release_ws(hipStream_t s);
+    int batch(const void *const *sends, void *const *recvs, const size_t *counts, int nb,
+              KungFu_Datatype dt, KungFu_Op op, int average, int algo, hipStream_t s);
+    void issue_loop();
+    void complete_loop();
+    ~kf_exchange();
+};
+
+int kf_exchange::ensure_ws(size_t bytes, hipStream_t s)
+{
+    if (ws_used && ws_last != s) KF_HIP(hipStreamWaitEvent(s, ws_ev, 0));
+    if (bytes > ws_cap) {
+        if (ws) {
+            if (ws_used) KF_HIP(hipEventSynchronize(ws_ev));
+            KF_HIP(hipFree(ws));
+            ws     = nullptr;
+            ws_cap = 0;
+        }
+        const size_t cap = align_up(bytes, size_t(2) << 20);
+        KF_HIP(hipMalloc(&ws, cap));
+        ws_cap = cap;
+    }
+    return KF_OK;
+}
+
+void kf_exchange::release_ws(hipStream_t s)
+{
+    if (hipEventRecord(ws_ev, s) == hipSuccess) {
+        ws_last = s;
+        ws_used = true;
+    }
+}
+
+// Resolve KF_ALGO_AUTO; KF_ERR_* for a combination that cannot run.
+static int resolve_algo(int algo, KungFu_Datatype dt, KungFu_Op op, int world, int *out)
+{
+    ncclDataType_t t;
+    const bool rs_ok = nccl_type(dt, &t);
+    if (algo == KF_ALGO_REDUCE_SCATTER) {
+        if (!rs_ok) return fail(KF_ERR_DTYPE, "no RCCL reduction type for this dtype");
+        *out = algo;
+        return KF_OK;
+    }
+    if (algo == KF_ALGO_ALL_TO_ALL) {
+        if (world > KF_MAX_INPUTS) {
+            return fail(KF_ERR_ARG, "all-to-all fold supports at most 16 ranks");
+        }
+        *out = algo;
+        return KF_OK;
+    }
+    if (algo != KF_ALGO_AUTO) return fail(KF_ERR_ARG, "unknown algo");
+    const bool own_semantics = dt == KungFu_FLOAT16 || dt == KungFu_BFLOAT16 ||
+                               (is_float(dt) && (op == KungFu_MIN || op == KungFu_MAX));
+    if (world <= KF_MAX_INPUTS && (own_semantics || !rs_ok)) {
+        *out = KF_ALGO_ALL_TO_ALL;
+    } else if (rs_ok) {
+        *out = KF_ALGO_REDUCE_SCATTER;
+    } else {
+        return fail(KF_ERR_DTYPE, "dtype needs the all-to-all fold (at most 16 ranks)");
+    }
+    return KF_OK;
+}
+
+int kf_exchange::batch(const void *const *sends, void *const *recvs, const size_t *counts,
+                       int nb, KungFu_Datatype dt, KungFu_Op op, int average, int algo,
+                       hipStream_t s)
+{
+    const Rccl &R = rccl();
+    const int sz  = tsize(dt);
+    const int W = world, r = rank;
+    if (W == 1) {  // a single peer: the sum is the bucket, x / 1 == x
+        for (int b = 0; b < nb; ++b) {
+            if (counts[b] && sends[b] != recvs[b]) {
+                KF_HIP(hipMemcpyAsync(recvs[b], sends[b], counts[b] * sz, hipMemcpyDeviceToDevice, s));
+            }
+        }
+        return KF_OK;
+    }
+    int a  = 0;
+    int rc = resolve_algo(algo, dt, op, W, &a);
+    if (rc != KF_OK) return rc;
+    ncclDataType_t nt = ncclUint8;
+    nccl_type(dt, &nt);
+
+    // workspace: received shards (all-to-all) and gathered tails
+    std::vector<size_t> wsoff(nb, 0), toff(nb, 0);
+    size_t need = 0;
+    for (int b = 0; b < nb; ++b) {
+        const size_t q = counts[b] / W, t = counts[b] % W;
+        if (a == KF_ALGO_ALL_TO_ALL && q) {
+            wsoff[b] = need;
+            need += align_up(q * W * sz, 256);
+        }
+        if (t) {
+            toff[b] = need;
+            need += align_up(t * W * sz, 256);
+        }
+    }
+    if (need) {
+        rc = ensure_ws(need, s);
+        if (rc != KF_OK) return rc;
+    }
+    char *wsp = static_cast<char *>(ws);
+
+    auto group_end = [&](int status) -> int {
+        ncclResult_t e = R.GroupEnd();
+        if (status != KF_OK) return status;
+        if (e != ncclSuccess) return nccl_fail(e, "ncclGroupEnd");
+        return KF_OK;
+    };
+
+    // phase 1: every bucket's reduce-scatter (or all-to-all) and tail gather
+    KF_NCCL(R.GroupStart());
+    rc = KF_OK;
+    for (int b = 0; b < nb && rc == KF_OK; ++b) {
+        const size_t q = counts[b] / W, t = counts[b] % W;
+        const char *snd = static_cast<const char *>(sends[b]);
+        char *rcv       = static_cast<char *>(recvs[b]);
+        ncclResult_t e  = ncclSuccess;
+        if (q && a == KF_ALGO_REDUCE_SCATTER) {
+            e = R.ReduceScatter(snd, rcv + r * q * sz, q, nt, nccl_op(op), comm, s);
+        } else if (q) {
+            e = R.AllToAll(snd, wsp + wsoff[b], q * sz, ncclUint8, comm, s);
+        }
+        if (e == ncclSuccess && t) {
+            e = R.AllGather(snd + q * W * sz, wsp + toff[b], t * sz, ncclUint8, comm, s);
+        }
+        if (e != ncclSuccess) rc = nccl_fail(e, "phase-1 collective");
+    }
+    rc = group_end(rc);
+    if (rc != KF_OK) return rc;
+
+    // phase 2: the element-wise work, batched over the buckets
+    std::vector<const void *> ins;
+    std::vector<void *> outs;
+    std::vector<size_t> cnts;
+    if (a == KF_ALGO_REDUCE_SCATTER && average) {
+        for (int b = 0; b < nb; ++b) {
+            const size_t q = counts[b] / W;
+            if (!q) continue;
+            char *sh = static_cast<char *>(recvs[b]) + r * q * sz;
+            ins.push_back(sh);
+            outs.push_back(sh);
+            cnts.push_back(q);
+        }
+        if (!outs.empty()) {
+            rc = kf_bucket_reduce_batch(ins.data(), 1, outs.data(), cnts.data(),
+                                        static_cast<int>(outs.size()), dt, KungFu_SUM, W, s);
+            if (rc != KF_OK) return fail(rc, "shard /np epilogue");
+        }
+        ins.clear();
+        outs.clear();
+        cnts.clear();
+    }
+    for (int b = 0; b < nb; ++b) {  // rank-order folds: shards and tails
+        const size_t q = counts[b] / W, t = counts[b] % W;
+        char *rcv      = static_cast<char *>(recvs[b]);
+        if (q && a == KF_ALGO_ALL_TO_ALL) {
+            for (int j = 0; j < W; ++j) ins.push_back(wsp + wsoff[b] + j * q * sz);
+            outs.push_back(rcv + r * q * sz);
+            cnts.push_back(q);
+        }
+        if (t) {
+            for (int j = 0; j < W; ++j) ins.push_back(wsp + toff[b] + j * t * sz);
+            outs.push_back(rcv + q * W * sz);
+            cnts.push_back(t);
+        }
+    }
+    if (!outs.empty()) {
+        rc = kf_bucket_reduce_batch(ins.data(), W, outs.data(), cnts.data(),
+                                    static_cast<int>(outs.size()), dt, op, average ? W : 0, s);
+        if (rc != KF_OK) return fail(rc, "rank-order fold of the received shards");
+    }
+
+    // phase 3: in-place all-gather of every reduced shard
+    KF_NCCL(R.GroupStart());
+    rc = KF_OK;
+    for (int b = 0; b < nb && rc == KF_OK; ++b) {
+        const size_t q = counts[b] / W;
+        if (!q) continue;
+        char *rcv      = static_cast<char *>(recvs[b]);
+        ncclResult_t e = R.AllGather(rcv + r * q * sz, rcv, q * sz, ncclUint8, comm, s);
+        if (e != ncclSuccess) rc = nccl_fail(e, "ncclAllGather");
+    }
+    rc = group_end(rc);
+    if (rc != KF_OK) return rc;
+    if (need) release_ws(s);
+    return KF_OK;
+}
+
+// Issue thread: the tasks of the step, strictly in `order`
+// (LinearExecutor, scheduler.cpp:40-58).
+void kf_exchange::issue_loop()
+{
+    (void)hipSetDevice(device);
+    std::unique_lock<std::mutex> lk(smu);
+    for (;;) {
+        scv.wait(lk, [&] {
+            return stop || (issued < ntasks && tasks[order[issued]].started);
+        });
+        if (stop) return;
+        Task t = tasks[order[issued]];
+        lk.unlock();
+        int rc;
+        {
+            std::lock_guard<std::mutex> g(mu);
+            const void *sp = t.send;
+            void *rp       = t.recv;
+            rc = batch(&sp, &rp, &t.count, 1, t.dt, t.op, t.average, t.algo, t.stream);
+        }
+        hipEvent_t ev = nullptr;
+        if (rc == KF_OK && hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess) {
+            if (hipEventRecord(ev, t.stream) != hipSuccess) {
+                (void)hipEventDestroy(ev);
+                ev = nullptr;
+                rc = fail(KF_ERR_HIP, "hipEventRecord");
+            }
+        } else if (rc == KF_OK) {
+            rc = fail(KF_ERR_HIP, "hipEventCreate");
+        }
+        lk.lock();
+        cq.push_back(Done{ev, t.done, t.arg, rc});
+        ++issued;
+        scv.notify_all();
+    }
+}
+
+// Completion thread: done(status, arg) once each issued all-reduce finished.
+void kf_exchange::complete_loop()
+{
+    (void)hipSetDevice(device);
+    std::unique_lock<std::mutex> lk(smu);
+    for (;;) {
+        scv.wait(lk, [&] { return stop || !cq.empty(); });
+        if (cq.empty() && stop) return;
+        Done d = cq.front();
+        cq.pop_front();
+        lk.unlock();
+        int rc = d.status;
+        if (d.ev) {
+            if (hipEventSynchronize(d.ev) != hipSuccess) rc = KF_ERR_HIP;
+            (void)hipEventDestroy(d.ev);
+        }
+        if (rc == KF_OK) {
+            ncclResult_t ae = ncclSuccess;
+            if (rccl().CommGetAsyncError(comm, &ae) != ncclSuccess || ae != ncclSuccess) {
+                rc = KF_ERR_RCCL;
+            }
+        }
+        if (d.done) d.done(rc, d.arg);
+        lk.lock();
+        if (rc != KF_OK && sstatus == KF_OK) sstatus = rc;
+        ++completed;
+        scv.notify_all();
+    }
+}
+
+kf_exchange::~kf_exchange()
+{
+    {
+        std::lock_guard<std::mutex> lk(smu);
+        stop = true;
+    }
+    scv.notify_all();
+    if (issuer.joinable()) issuer.join();
+    if (completer.joinable()) completer.join();
+    DeviceGuard g(device);
+    if (comm) (void)rccl().CommDestroy(comm);
+    if (ws) (void)hipFree(ws);
+    if (ws_ev) (void)hipEventDestroy(ws_ev);
+    if (own) (void)hipStreamDestroy(own);
+}
+
+extern "C" {
+
+int kf_exchange_unique_id(void *id)
+{
+    if (!id) return KF_ERR_ARG;
+    int rc = need_rccl();
+    if (rc != KF_OK) return rc;
+    static_assert(sizeof(ncclUniqueId) == KF_UNIQUE_ID_BYTES, "id size");
+    ncclUniqueId u;
+    KF_NCCL(rccl().GetUniqueId(&u));
+    std::memcpy(id, &u, sizeof(u));
+    return KF_OK;
+}
+
+int kf_exchange_share_id(kf_session_t *s, void *id)
+{
+    if (!s || !id) return KF_ERR_ARG;
+    const int dm = kf_session_device_mode_internal(s);
+    if (dm == 0) {
+        return kf_session_broadcast(s, id, id, KF_UNIQUE_ID_BYTES, KungFu_UINT8, "nccl id", nullptr);
+    }
+    void *d = nullptr;
+    KF_HIP(hipMalloc(&d, KF_UNIQUE_ID_BYTES));
+    int rc = KF_OK;
+    hipError_t e = hipMemcpy(d, id, KF_UNIQUE_ID_BYTES, hipMemcpyHostToDevice);
+    if (e != hipSuccess) rc = hip_fail(e, "hipMemcpy(id)");
+    if (rc == KF_OK) {
+        rc = kf_session_broadcast(s, d, d, KF_UNIQUE_ID_BYTES, KungFu_UINT8, "nccl id", nullptr);
+    }
+    if (rc == KF_OK) {
+        e = hipMemcpy(id, d, KF_UNIQUE_ID_BYTES, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) rc = hip_fail(e, "hipMemcpy(id)");
+    }
+    (void)hipFree(d);
+    return rc;
+}
+
+kf_exchange_t *kf_exchange_create(const void *id, int rank, int world, int device)
+{
+    if (!id || world < 1 || rank < 0 || rank >= world || device < 0) {
+        fail(KF_ERR_ARG, "kf_exchange_create: bad arguments");
+        return nullptr;
+    }
+    if (need_rccl() != KF_OK) return nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device >= ndev) {
+        fail(KF_ERR_NO_DEVICE, "kf_exchange_create: no HIP device " + std::to_string(device));
+        return nullptr;
+    }
+    DeviceGuard g(device);
+    auto *ex   = new kf_exchange;
+    ex->rank   = rank;
+    ex->world  = world;
+    ex->device = device;
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof(u));
+    ncclResult_t e = rccl().CommInitRank(&ex->comm, world, u, rank);
+    if (e != ncclSuccess) {
+        nccl_fail(e, "ncclCommInitRank");
+        ex->comm = nullptr;
+        delete ex;
+        return nullptr;
+    }
+    if (hipEventCreateWithFlags(&ex->ws_ev, hipEventDisableTiming) != hipSuccess ||
+        hipStreamCreateWithFlags(&ex->own, hipStreamNonBlocking) != hipSuccess) {
+        fail(KF_ERR_HIP, "kf_exchange_create: event/stream");
+        delete ex;
+        return nullptr;
+    }
+    return ex;
+}
+
+kf_exchange_t *kf_exchange_create_session(kf_session_t *s, int rank, int world, int device)
+{
+    unsigned char id[KF_UNIQUE_ID_BYTES] = {0};
+    if (rank == 0 && kf_exchange_unique_id(id) != KF_OK) {
+        // the peers still wait for an id: send the zeros, they fail in init
+        std::string why = t_ex_error;
+        (void)kf_exchange_share_id(s, id);
+        fail(KF_ERR_RCCL, why);
+        return nullptr;
+    }
+    int rc = kf_exchange_share_id(s, id);
+    if (rc != KF_OK) {
+        fail(rc, "kf_exchange_share_id failed");
+        return nullptr;
+    }
+    return kf_exchange_create(id, rank, world, device);
+}
+
+static int check_bucket_args(kf_exchange_t *ex, const void *const *sends, void *const *recvs,
+                             const size_t *counts, int nb, KungFu_Datatype dt, KungFu_Op op,
+                             int average)
+{
+    if (!ex || nb < 0 || (nb > 0 && (!sends || !recvs || !counts))) {
+        return fail(KF_ERR_ARG, "bad arguments");
+    }
+    if (tsize(dt) == 0) return fail(KF_ERR_DTYPE, "unsupported dtype");
+    if (static_cast<unsigned>(op) > KungFu_PROD) return fail(KF_ERR_OP, "unsupported op");
+    if (dt == KungFu_FLOAT16 && op != KungFu_SUM) return fail(KF_ERR_OP, "fp16 supports SUM only");
+    if (average && (op != KungFu_SUM || !is_float(dt))) {
+        return fail(KF_ERR_OP, "average needs SUM on a float dtype");
+    }
+    for (int b = 0; b < nb; ++b) {
+        if (counts[b] && (!sends[b] || !recvs[b])) return fail(KF_ERR_ARG, "null bucket");
+    }
+    return KF_OK;
+}
+
+int kf_exchange_all_reduce_batch(kf_exchange_t *ex, const void *const *sends, void *const *recvs,
+                                 const size_t *counts, int nb, KungFu_Datatype dt, KungFu_Op op,
+                                 int average, int algo, void *stream)
+{
+    int rc = check_bucket_args(ex, sends, recvs, counts, nb, dt, op, average);
+    if (rc != KF_OK || nb == 0) return rc;
+    DeviceGuard g(ex->device);
+    std::lock_guard<std::mutex> lk(ex->mu);
+    return ex->batch(sends, recvs, counts, nb, dt, op, average, algo,
+                     static_cast<hipStream_t>(stream));
+}
+
+int kf_exchange_all_reduce(kf_exchange_t *ex, const void *send, void *recv, size_t count,
+                           KungFu_Datatype dt, KungFu_Op op, int average, int algo, void *stream)
+{
+    return kf_exchange_all_reduce_batch(ex, &send, &recv, &count, 1, dt, op, average, algo, stream);
+}
+
+int kf_exchange_sma_batch(kf_exchange_t *ex, void *const *vs, void *const *sums,
+                          const size_t *counts, int nb, KungFu_Datatype dt, double alpha,
+                          int algo, void *stream)
+{
+    int rc = check_bucket_args(ex, vs, sums, counts, nb, dt, KungFu_SUM, 0);
+    if (rc != KF_OK || nb == 0) return rc;
+    if (!is_float(dt)) return fail(KF_ERR_DTYPE, "SMA needs a float dtype");
+    DeviceGuard g(ex->device);
+    std::lock_guard<std::mutex> lk(ex->mu);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    std::vector<const void *> snd(vs, vs + nb);
+    rc = ex->batch(snd.data(), sums, counts, nb, dt, KungFu_SUM, 0, algo, s);
+    if (rc != KF_OK) return rc;
+    for (int b = 0; b < nb; ++b) {
+        rc = kf_sma_blend(vs[b], sums[b], counts[b], dt, ex->world, alpha, stream);
+        if (rc != KF_OK) return fail(rc, "kf_sma_blend");
+    }
+    return KF_OK;
+}
+
+int kf_exchange_begin_step(kf_exchange_t *ex, const char *const *names, int n, int auto_order)
+{
+    if (!ex || n < 0 || (n > 0 && !names)) return fail(KF_ERR_ARG, "bad arguments");
+    std::unique_lock<std::mutex> lk(ex->smu);
+    ex->scv.wait(lk, [&] { return ex->completed == ex->ntasks; });  // previous step done
+    std::map<std::string, int> idx;
+    for (int i = 0; i < n; ++i) {
+        if (!names[i] || !idx.emplace(names[i], i).second) {
+            return fail(KF_ERR_ARG, "names must be distinct and non-null");
+        }
+    }
+    if (ex->steps == 1 && auto_order && ex->first_arrive.size() == static_cast<size_t>(n)) {
+        // NCCLScheduler::Reset (scheduler.cpp:96-118): the second step takes
+        // rank 0's arrival order of the first
+        lk.unlock();
+        DeviceGuard g(ex->device);
+        std::vector<int32_t> ord = ex->first_arrive;
+        int rc      = KF_OK;
+        int32_t *d  = nullptr;
+        const size_t bytes = sizeof(int32_t) * n;
+        hipError_t e = hipMalloc(&d, bytes);
+        if (e == hipSuccess) e = hipMemcpyAsync(d, ord.data(), bytes, hipMemcpyHostToDevice, ex->own);
+        if (e != hipSuccess) rc = hip_fail(e, "order broadcast buffer");
+        if (rc == KF_OK) {
+            std::lock_guard<std::mutex> g2(ex->mu);
+            ncclResult_t r = rccl().Broadcast(d, d, n, ncclInt32, 0, ex->comm, ex->own);
+            if (r != ncclSuccess) rc = nccl_fail(r, "ncclBroadcast(order)");
+        }
+        if (rc == KF_OK) {
+            e = hipMemcpyAsync(ord.data(), d, bytes, hipMemcpyDeviceToHost, ex->own);
+            if (e == hipSuccess) e = hipStreamSynchronize(ex->own);
+            if (e != hipSuccess) rc = hip_fail(e, "order broadcast");
+        }
+        if (d) (void)hipFree(d);
+        if (rc != KF_OK) return rc;
+        lk.lock();
+        ex->order = ord;
+    } else if (ex->order.size() != static_cast<size_t>(n)) {
+        ex->order.resize(n);
+        std::iota(ex->order.begin(), ex->order.end(), 0);
+    }
+    ex->idx = std::move(idx);
+    ex->tasks.assign(n, Task{});
+    ex->arrive.clear();
+    ex->issued = ex->completed = 0;
+    ex->ntasks  = n;
+    ex->sstatus = KF_OK;
+    ex->steps++;
+    if (!ex->issuer.joinable()) {
+        ex->issuer    = std::thread([ex] { ex->issue_loop(); });
+        ex->completer = std::thread([ex] { ex->complete_loop(); });
+    }
+    return KF_OK;
+}
+
+int kf_exchange_start(kf_exchange_t *ex, const char *name, const void *send, void *recv,
+                      size_t count, KungFu_Datatype dt, KungFu_Op op, int average, int algo,
+                      void *stream, kf_done_fn done, void *arg)
+{
+    if (!ex || !name) return fail(KF_ERR_ARG, "bad arguments");
+    size_t c  = count;
+    int rc    = check_bucket_args(ex, &send, &recv, &c, 1, dt, op, average);
+    if (rc != KF_OK) return rc;
+    std::lock_guard<std::mutex> lk(ex->smu);
+    auto it = ex->idx.find(name);
+    if (it == ex->idx.end()) return fail(KF_ERR_ARG, std::string("name not in this step: ") + name);
+    Task &t = ex->tasks[it->second];
+    if (t.started) return fail(KF_ERR_ARG, std::string("started twice: ") + name);
+    t = Task{send, recv, count, dt, op, average, algo, static_cast<hipStream_t>(stream), done, arg,
+             true};
+    ex->arrive.push_back(it->second);
+    if (ex->steps == 1) ex->first_arrive = ex->arrive;
+    ex->scv.notify_all();
+    return KF_OK;
+}
+
+int kf_exchange_wait_all(kf_exchange_t *ex, int32_t *order)
+{
+    if (!ex) return KF_ERR_ARG;
+    if (std::this_thread::get_id() == ex->completer.get_id()) {
+        return fail(KF_ERR_ARG, "kf_exchange_wait_all from a done callback");
+    }
+    std::unique_lock<std::mutex> lk(ex->smu);
+    ex->scv.wait(lk, [&] { return ex->completed == ex->ntasks; });
+    if (order) std::copy(ex->order.begin(), ex->order.end(), order);
+    return ex->sstatus;
+}
+
+int kf_exchange_check(kf_exchange_t *ex)
+{
+    if (!ex) return KF_ERR_ARG;
+    ncclResult_t ae = ncclSuccess;
+    KF_NCCL(rccl().CommGetAsyncError(ex->comm, &ae));
+    if (ae != ncclSuccess) return nccl_fail(ae, "RCCL asynchronous error");
+    return KF_OK;
+}
+
+int kf_exchange_info(kf_exchange_t *ex, int *rank, int *world, int *device)
+{
+    if (!ex) return KF_ERR_ARG;
+    if (rank) *rank = ex->rank;
+    if (world) *world = ex->world;
+    if (device) *device = ex->device;
+    return KF_OK;
+}
+
+void kf_exchange_destroy(kf_exchange_t *ex) { delete ex; }
+
+const char *kf_exchange_last_error(void) { return t_ex_error.c_str(); }
+
+}  // extern "C"

@@ -356,11 +356,14 @@ fold_scalar(const InPtrs &in, int k, size_t i, const Div &np)
 // input count (2 for the hot path) or 0 = runtime k (pointers are then read
 // from the kernel-argument block with scalar loads, never a local array).
 // ---------------------------------------------------------------------------
+// The body of one block, `blk` of `nblk` working on one bucket: reduce_kernel
+// runs it with (blockIdx.x, gridDim.x); the batch kernel below with the block's
+// index inside its bucket's share of the grid.
 template <typename T, int OP, int EPI, int KC, int BLOCK, int UNROLL, int LOADNT,
           int STPLAIN = 0>
-__global__ void __launch_bounds__(BLOCK)
-    reduce_kernel(InPtrs in, int k, void *out, size_t n, size_t head,
-                  size_t nvec, Div np)
+__device__ __forceinline__ void reduce_body(const InPtrs &in, int k, void *out, size_t n,
+                                            size_t head, size_t nvec, const Div &np,
+                                            size_t blk, size_t nblk)
 {
     using S         = typename Elt<T>::S;
     using L         = Lane<T>;
@@ -371,7 +374,7 @@ __global__ void __launch_bounds__(BLOCK)
     const int kk    = KC > 0 ? KC : k;
 
     // scalar edges: head elements, then the tail after the vector body
-    const size_t tid   = static_cast<size_t>(blockIdx.x) * BLOCK + threadIdx.x;
+    const size_t tid   = blk * BLOCK + threadIdx.x;
     const size_t vend  = head + nvec * E;
     const size_t nedge = head + (n - vend);
     if (tid < nedge) {
@@ -388,7 +391,7 @@ __global__ void __launch_bounds__(BLOCK)
 
     const size_t tile   = static_cast<size_t>(BLOCK) * UNROLL;
     const size_t ntiles = (nvec + tile - 1) / tile;
-    for (size_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    for (size_t t = blk; t < ntiles; t += nblk) {
         const size_t v0 = t * tile + threadIdx.x;
         if (v0 + (UNROLL - 1) * BLOCK < nvec) {
             Acc acc[UNROLL][V];
@@ -477,6 +480,47 @@ __global__ void __launch_bounds__(BLOCK)
             }
         }
     }
+}
+
+template <typename T, int OP, int EPI, int KC, int BLOCK, int UNROLL, int LOADNT,
+          int STPLAIN = 0>
+__global__ void __launch_bounds__(BLOCK)
+    reduce_kernel(InPtrs in, int k, void *out, size_t n, size_t head,
+                  size_t nvec, Div np)
+{
+    reduce_body<T, OP, EPI, KC, BLOCK, UNROLL, LOADNT, STPLAIN>(in, k, out, n, head, nvec, np,
+                                                               blockIdx.x, gridDim.x);
+}
+
+// ---------------------------------------------------------------------------
+// Batch: many independent buckets (same dtype, op, k and epilogue) in ONE
+// launch. A 4 MiB bucket is 4.5 us of launch for 1.6 us of HBM time
+// (profiles/r01/size_sweep.jsonl: 0.35 of the roofline); the per-bucket steps
+// of an exchange (the /np of every shard, the fold of every bucket's received
+// shards) come in dozens per step. Bucket s owns blocks [blk0[s], blk0[s+1])
+// of the grid, one block per tile as in reduce_kernel, so the launch streams
+// all buckets with the same per-block schedule. The arguments live in the
+// kernarg segment (scalar loads; the bucket index is wave-uniform).
+// ---------------------------------------------------------------------------
+constexpr int kBatchSeg = 16;
+
+struct BatchArgs {
+    InPtrs in[kBatchSeg];
+    void *out[kBatchSeg];
+    size_t n[kBatchSeg], head[kBatchSeg], nvec[kBatchSeg];
+    unsigned blk0[kBatchSeg + 1];
+    int nseg;
+};
+
+template <typename T, int OP, int EPI, int KC, int BLOCK, int UNROLL>
+__global__ void __launch_bounds__(BLOCK) reduce_batch_kernel(BatchArgs a, int k, Div np)
+{
+    const unsigned b = blockIdx.x;
+    int s            = 0;
+    while (s + 1 < a.nseg && b >= a.blk0[s + 1]) ++s;
+    const size_t nblk = a.blk0[s + 1] - a.blk0[s];
+    reduce_body<T, OP, EPI, KC, BLOCK, UNROLL, 1, 0>(a.in[s], k, a.out[s], a.n[s], a.head[s],
+                                                    a.nvec[s], np, b - a.blk0[s], nblk);
 }
 
 // Fold for inputs that sit behind DIFFERENT links (the P2P shard fold reads

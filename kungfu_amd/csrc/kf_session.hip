@@ -1343,3 +1343,7 @@ void kf_session_destroy(kf_session_t *s) { delete s; }
 const char *kf_session_last_error(void) { return t_sess_error.c_str(); }
 
 }  // extern "C"
+
+// library-internal (hidden): whether a session moves device or host buffers
+// (kf_exchange.hip broadcasts the RCCL id through it)
+int kf_session_device_mode_internal(const kf_session_t *s) { return s ? s->device_mode : -1; }

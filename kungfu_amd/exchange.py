@@ -1,0 +1,212 @@
+"""Multi-GPU bucket exchange through the native C-ABI (kf_exchange_*,
+kungfu_amd/csrc/kf_exchange.hip): RCCL over xGMI for the data movement, the
+build's HIP kernels for the element-wise sum.
+
+The reference's GPU path is native too: gpu_collective_nccl
+(srcs/cpp/src/nccl/gpu_collective.cpp:91-188) owns an NCCL communicator whose
+id rank 0 creates and KungFu broadcasts (:190-200). ``NativeExchange`` does the
+same with torch.distributed carrying the 128-byte id, then hands every step's
+buckets to ONE native call:
+
+  algo="rs"   ncclReduceScatter -> HIP /np on the shard -> ncclAllGather
+  algo="a2a"  ncclAllToAll -> HIP rank-order fold (/np fused) -> ncclAllGather
+  algo="auto" rs for integers and f32/f64 SUM, a2a for f16/bf16 and float
+              MIN/MAX (the build's defined semantics: bf16 accumulates in fp32
+              and rounds once, bit-identical to the P2P exchange and the oracle)
+
+Each phase of a call is one grouped RCCL launch and all shard epilogues one
+batched HIP launch, so a step of 64 buckets costs 3 launches whatever the
+bucket size. Same interface as collective.Exchange (all_reduce_, start_, sma_,
+world), so the optimizers take it as ``exchange=NativeExchange()``.
+"""
+import ctypes
+
+import torch
+import torch.distributed as dist
+
+from . import _lib
+from .base import OP, OP_NAMES
+from .ops import kungfu_dtype
+
+ALGOS = {"auto": 0, "rs": 1, "a2a": 2}
+
+
+def _arr(t, vals):
+    return (t * len(vals))(*vals)
+
+
+class NativeExchange:
+    def __init__(self, group=None, algo="auto", device=None):
+        if algo not in ALGOS:
+            raise ValueError("algo must be one of %s" % sorted(ALGOS))
+        self.algo = algo
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.lib = _lib.load()
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        self.device = torch.device(device)
+        uid = (ctypes.c_char * 128)()
+        if self.rank == 0:
+            _lib.check(self.lib.kf_exchange_unique_id(uid), "kf_exchange_unique_id")
+        if self.world > 1:
+            # gpu_collective.cpp:196-198: rank 0's id, broadcast to the group
+            obj = [bytes(uid) if self.rank == 0 else None]
+            src = dist.get_global_rank(group, 0) if group is not None else 0
+            dist.broadcast_object_list(obj, src=src, group=group)
+            ctypes.memmove(uid, obj[0], 128)
+        h = self.lib.kf_exchange_create(uid, self.rank, self.world, self.device.index)
+        if not h:
+            raise _lib.KungFuAMDError("kf_exchange_create: " +
+                                      self.lib.kf_exchange_last_error().decode())
+        self._h = h
+        self._side = None
+        self._sums = {}
+
+    # -- the optimizers' interface (collective.Exchange) --------------------
+    def _check(self, buckets):
+        for b in buckets:
+            if not b.is_cuda or b.dim() != 1 or not b.is_contiguous():
+                raise ValueError("buckets must be flat contiguous GPU tensors")
+            if b.dtype != buckets[0].dtype:
+                raise ValueError("one dtype per call")
+
+    def _issue(self, buckets, op, average, stream):
+        red = OP_NAMES[op] if isinstance(op, str) else OP(op)
+        if average and red != OP.SUM:
+            raise ValueError("average requires op='sum'")
+        ptrs = [b.data_ptr() for b in buckets]
+        rc = self.lib.kf_exchange_all_reduce_batch(
+            self._h, _lib.ptr_array(ptrs), _lib.ptr_array(ptrs),
+            _arr(ctypes.c_size_t, [b.numel() for b in buckets]), len(buckets),
+            int(kungfu_dtype(buckets[0])), int(red), 1 if average else 0, ALGOS[self.algo],
+            stream.cuda_stream)
+        _lib.check(rc, "kf_exchange_all_reduce_batch")
+
+    def _runs(self, buckets, coalesce):
+        from .collective import coalesce_runs
+        return coalesce_runs(buckets) if coalesce else list(buckets)
+
+    def all_reduce_(self, buckets, op="sum", average=False, coalesce=True):
+        """In place, queued on the current stream (no host sync)."""
+        buckets = list(buckets)
+        if not buckets:
+            return buckets
+        self._check(buckets)
+        self._issue(self._runs(buckets, coalesce), op, average,
+                    torch.cuda.current_stream(self.device))
+        return buckets
+
+    def start_(self, buckets, op="sum", average=False, coalesce=True, key=None):
+        """Queue the all-reduce on the exchange's own stream, after the work
+        already queued on the current one (the gradients), so it overlaps the
+        rest of backward; handle.wait() orders the current stream after it."""
+        buckets = list(buckets)
+        self._check(buckets)
+        if self._side is None:
+            self._side = torch.cuda.Stream(self.device)
+        cur = torch.cuda.current_stream(self.device)
+        self._side.wait_stream(cur)
+        self._issue(self._runs(buckets, coalesce), op, average, self._side)
+        ev = torch.cuda.Event()
+        ev.record(self._side)
+        for b in buckets:
+            b.record_stream(self._side)
+        return _Handle(ev, self.device)
+
+    def sma_(self, buckets, alpha):
+        """SMA (sma_sgd.py:60-65) over flat variable buckets, in place."""
+        buckets = list(buckets)
+        if not buckets:
+            return buckets
+        self._check(buckets)
+        key = tuple((b.data_ptr(), b.numel()) for b in buckets)
+        sums = self._sums.get(key)
+        if sums is None:
+            sums = [torch.empty_like(b) for b in buckets]
+            self._sums[key] = sums
+        vp = [b.data_ptr() for b in buckets]
+        sp = [s.data_ptr() for s in sums]
+        rc = self.lib.kf_exchange_sma_batch(
+            self._h, _lib.ptr_array(vp), _lib.ptr_array(sp),
+            _arr(ctypes.c_size_t, [b.numel() for b in buckets]), len(buckets),
+            int(kungfu_dtype(buckets[0])), float(alpha), ALGOS[self.algo],
+            torch.cuda.current_stream(self.device).cuda_stream)
+        _lib.check(rc, "kf_exchange_sma_batch")
+        return buckets
+
+    def check(self):
+        """Raise if RCCL reported an asynchronous error."""
+        _lib.check(self.lib.kf_exchange_check(self._h), "kf_exchange_check")
+
+    def finish(self):
+        """Nothing to settle: RCCL and the HIP epilogues are stream-ordered."""
+
+    def close(self):
+        if getattr(self, "_h", None):
+            torch.cuda.synchronize(self.device)
+            self.lib.kf_exchange_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class _Handle:
+    def __init__(self, ev, device):
+        self.ev = ev
+        self.device = device
+
+    def wait(self):
+        torch.cuda.current_stream(self.device).wait_event(self.ev)
+
+
+class Scheduler:
+    """Ordered issue of all-reduces that become ready in any order — the
+    reference's NCCLScheduler (srcs/cpp/src/nccl/scheduler.cpp:8-130) on
+    kf_exchange_begin_step / kf_exchange_start. ``begin_step(names)`` fixes
+    the step's names (same list on every rank); ``start(name, buf)`` may come
+    in any order; the native thread issues them in the agreed order (with
+    ``auto_order``, rank 0's arrival order of the first step from the second
+    step on)."""
+
+    def __init__(self, exchange, auto_order=True):
+        self.ex = exchange
+        self.auto_order = bool(auto_order)
+        self._keep = []
+
+    def begin_step(self, names):
+        arr = (ctypes.c_char_p * len(names))(*[n.encode() for n in names])
+        self.names = list(names)
+        _lib.check(self.ex.lib.kf_exchange_begin_step(self.ex._h, arr, len(names),
+                                                      1 if self.auto_order else 0),
+                   "kf_exchange_begin_step")
+        self._keep = []
+
+    def start(self, name, buf, op="sum", average=False, stream=None, callback=None):
+        red = OP_NAMES[op] if isinstance(op, str) else OP(op)
+        s = stream if stream is not None else torch.cuda.current_stream(buf.device)
+
+        def done(status, _arg):
+            if callback is not None:
+                callback(name, status)
+
+        cfn = _lib.DONE_FN(done)
+        self._keep.append((cfn, buf))
+        rc = self.ex.lib.kf_exchange_start(self.ex._h, name.encode(), buf.data_ptr(),
+                                           buf.data_ptr(), buf.numel(), int(kungfu_dtype(buf)),
+                                           int(red), 1 if average else 0,
+                                           ALGOS[self.ex.algo], s.cuda_stream, cfn, None)
+        _lib.check(rc, "kf_exchange_start")
+
+    def wait_all(self):
+        """Block until the step's all-reduces completed; returns the issue
+        order (names)."""
+        order = (ctypes.c_int32 * len(self.names))()
+        rc = self.ex.lib.kf_exchange_wait_all(self.ex._h, order)
+        _lib.check(rc, "kf_exchange_wait_all")
+        return [self.names[i] for i in order]

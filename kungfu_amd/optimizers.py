@@ -34,6 +34,15 @@ def _wrap(optimizer, mixin):
     return obj
 
 
+def _finish(exchange):
+    """An exchange whose queued work can fail without the host seeing it
+    (the P2P device barriers) settles and raises here, before the update
+    consumes the reduced values."""
+    fin = getattr(exchange, "finish", None)
+    if fin is not None:
+        fin()
+
+
 class _Bucketed:
     def _kf_setup(self, named_parameters, exchange, bucket_bytes):
         if named_parameters is None:
@@ -142,6 +151,7 @@ class _SyncSGD(_Bucketed):
 
     def step(self, closure=None):
         self.sync_gradients()
+        _finish(self._kf_ex)
         return super().step(closure)
 
 
@@ -189,6 +199,7 @@ class _SMA(_Bucketed):
 
     def step(self, closure=None):
         self.sync_variables()
+        _finish(self._kf_ex)
         return super().step(closure)
 
 

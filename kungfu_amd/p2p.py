@@ -160,6 +160,14 @@ class P2PExchange:
                                       "arrived)" % (_lib.STATUS.get(st, st),
                                                     self.timeout_us / 1e6))
 
+    def finish(self):
+        """Wait for the queued exchange and raise if one of its barriers gave
+        up. A timed-out barrier lets the fold and gather behind it run on peer
+        buffers nobody synchronised, so a result must not be used before this
+        returns (the optimizers call it before their update)."""
+        torch.cuda.current_stream().synchronize()
+        self.check()
+
     def _barrier(self):
         if self.barrier == "host":
             torch.cuda.synchronize()
@@ -310,6 +318,10 @@ class PeerExchange:
             self.epilogue.sma_blend_(b, s, self.world, alpha)
         return list(buckets)
 
+    def finish(self):
+        for ex in self._ex.values():
+            ex.finish()
+
     def close(self):
         for ex in self._ex.values():
             ex.close()
@@ -326,10 +338,15 @@ def _same_host(group=None):
 
 
 class AutoExchange:
-    """Exchange that picks, per bucket list, the faster of RCCL
-    (collective.Exchange: RS -> HIP epilogue -> AG) and the xGMI P2P exchange
-    (PeerExchange) by timing both on the real buckets the first time it sees
-    them — the way RCCL itself tunes its algorithm per size, lifted one level.
+    """Exchange that picks, per bucket list, the fastest of candidates that
+    give the SAME bits, by timing them on the real buckets the first time it
+    sees them — the way RCCL itself tunes its algorithm per size, lifted one
+    level. The candidates are RCCL's all-to-all + HIP rank-order fold
+    (collective.Exchange(algo="a2a")) and the xGMI P2P exchange (PeerExchange),
+    which both fold the ranks in order 0..n-1 with the same kernel; RCCL's
+    reduce-scatter joins them only where its own order cannot change a bit
+    (integer dtypes; two ranks summing f32/f64). So the result never depends
+    on which transport won on a given box.
 
     The trial runs `trials` exchanges with each candidate on the buckets, then
     restores their contents from a snapshot, so the first call returns the
@@ -346,7 +363,8 @@ class AutoExchange:
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.trials = int(trials)
         self.epilogue = epilogue if epilogue is not None else HipEpilogue()
-        self.rccl = Exchange(group, epilogue=self.epilogue)
+        self.rccl = Exchange(group, epilogue=self.epilogue, algo="a2a")
+        self.rccl_rs = Exchange(group, epilogue=self.epilogue, algo="rs")
         self.mode = mode
         self._p2p = None
         self._host_ok = None
@@ -369,13 +387,23 @@ class AutoExchange:
         dist.all_gather_object(flags, bool(flag), group=self.group)
         return all(flags)
 
-    def _pick(self, buckets, step):
+    def _rs_exact(self, buckets, op):
+        """RCCL's reduce-scatter gives the rank-order bits: integer sums and
+        selects in any order, or a single addition of two f32/f64 values."""
+        if all(not b.dtype.is_floating_point for b in buckets):
+            return True
+        return (self.world == 2 and op == "sum" and
+                all(b.dtype in (torch.float32, torch.float64) for b in buckets))
+
+    def _pick(self, buckets, step, op="sum"):
         import time
         key = tuple((b.data_ptr(), b.numel(), b.dtype) for b in buckets)
         ex = self._choice.get(key)
         if ex is not None:
             return ex
         cands = [("rccl", self.rccl)]
+        if self._rs_exact(buckets, op):
+            cands.append(("rccl_rs", self.rccl_rs))
         p2p = self._p2p_candidate(buckets)
         if p2p is not None:
             cands.append(("p2p", p2p))
@@ -387,7 +415,12 @@ class AutoExchange:
                 try:
                     step(cand)  # warm-up; maps the buckets for P2P
                     torch.cuda.synchronize()
-                except Exception:
+                    if hasattr(cand, "finish"):
+                        cand.finish()
+                except Exception as e:  # say why; the other candidates still run
+                    import sys
+                    print("kungfu_amd AutoExchange: candidate %s failed on rank %d: %r"
+                          % (name, self.rank, e), file=sys.stderr)
                     ok = False
                 if not self._agree_all(ok):
                     times.append(float("inf"))
@@ -398,6 +431,8 @@ class AutoExchange:
                     step(cand)
                 torch.cuda.synchronize()
                 times.append(time.perf_counter() - t0)
+                if hasattr(cand, "finish"):
+                    cand.finish()
             every = [None] * self.world
             dist.all_gather_object(every, times, group=self.group)
             worst = [max(t[i] for t in every) for i in range(len(cands))]
@@ -415,9 +450,13 @@ class AutoExchange:
         buckets = list(buckets)
         if self.world == 1:
             return self.rccl.all_reduce_(buckets, op=op, average=average)
-        ex = self._pick(buckets, lambda e: e.all_reduce_(buckets, op=op, average=average))
+        ex = self._pick(buckets, lambda e: e.all_reduce_(buckets, op=op, average=average), op)
         ex.all_reduce_(buckets, op=op, average=average)
         return buckets
+
+    def finish(self):
+        if self._p2p is not None:
+            self._p2p.finish()
 
     def sma_(self, buckets, alpha):
         buckets = list(buckets)

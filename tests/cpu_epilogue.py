@@ -8,7 +8,8 @@ import torch
 from oracle import oracle
 
 _DT = {torch.float32: "f32", torch.float64: "f64", torch.float16: "f16",
-       torch.bfloat16: "bf16"}
+       torch.bfloat16: "bf16", torch.int32: "i32", torch.int64: "i64", torch.uint8: "u8",
+       torch.int8: "i8", torch.int16: "i16"}
 
 
 def _np(t):
@@ -22,6 +23,15 @@ class CpuEpilogue:
         a = _np(x)
         a[...] = oracle.reduce_avg([np.ascontiguousarray(a)], _DT[x.dtype], np_)
         return x
+
+    def fold_(self, inputs, out, op, np_):
+        arrs = [np.ascontiguousarray(_np(t)) for t in inputs]
+        if np_:
+            res = oracle.reduce_avg(arrs, _DT[out.dtype], np_)
+        else:
+            res = oracle.reduce_k(arrs, _DT[out.dtype], int(op))
+        _np(out)[...] = res
+        return out
 
     def sma_blend_(self, v, summed, np_, alpha):
         a = _np(v)
@@ -44,6 +54,12 @@ class GpuShardEpilogue:
         self.hip.div_(g, np_)
         x.copy_(g.cpu())
         return x
+
+    def fold_(self, inputs, out, op, np_):
+        g = out.to(self.device)
+        self.hip.fold_([t.to(self.device) for t in inputs], g, op, np_)
+        out.copy_(g.cpu())
+        return out
 
     def sma_blend_(self, v, summed, np_, alpha):
         g = v.to(self.device)

@@ -448,7 +448,9 @@ def body_auto_exchange_cpu(rank, world, use_gpu):
             p -= 0.1 * (s / world)
     for p, q in zip(m.parameters(), ref.parameters()):
         assert torch.allclose(p, q, rtol=0, atol=1e-6)
-    assert set(ex.picked.values()) == {"rccl"}
+    # RCCL's paths only (no P2P for host buckets); reduce-scatter only where
+    # its order cannot change a bit (two ranks)
+    assert set(ex.picked.values()) <= ({"rccl", "rccl_rs"} if world == 2 else {"rccl"})
 
 
 @pytest.mark.parametrize("world", [2, 3])
@@ -468,3 +470,60 @@ def test_more_ranks_all_reduce(world):
 def test_eight_ranks_resnet50_and_sgd():
     run_world("body_resnet50_buckets", 8)
     run_world("body_sync_sgd", 8)
+
+
+def body_a2a_rank_order(rank, world, use_gpu):
+    # algo "a2a": all-to-all of the shards, then the rank-order fold — the
+    # oracle's reduce over ranks 0..world-1 bit for bit at EVERY world size
+    # (bf16: fp32 accumulation, one rounding; f16: per-hop rounding; f32: the
+    # rank-order sum), both for S-SGD (sum, / np) and SMA
+    from kungfu_amd.collective import Exchange, GradBuckets
+    from oracle import oracle
+    import cpu_epilogue
+    ex = Exchange(epilogue=_epilogue(use_gpu), algo="a2a")
+    auto = Exchange(epilogue=_epilogue(use_gpu))  # auto: bf16/f16 -> a2a
+    sizes = [1000, 33333, 7]
+    for dtype, name in ((torch.bfloat16, "bf16"), (torch.float16, "f16"),
+                        (torch.float32, "f32")):
+        xs = [[torch.from_numpy(_inputs(100 * r + i, n)).to(dtype) for i, n in enumerate(sizes)]
+              for r in range(world)]
+        for e in ((ex, auto) if dtype != torch.float32 else (ex,)):
+            gb = GradBuckets(sizes, dtype, torch.device("cpu"), world, n_buckets=2)
+            for v, x in zip(gb.views, xs[rank]):
+                v.copy_(x)
+            e.all_reduce_(gb.buckets, average=True, coalesce=False)
+            for i, v in enumerate(gb.views):
+                want = oracle.reduce_avg([cpu_epilogue._np(xs[r][i]).copy() for r in range(world)],
+                                         name, world)
+                assert np.array_equal(cpu_epilogue._np(v), want), (name, i)
+        # SMA: v <- (1-a) v + a sum/np, sum folded in rank order
+        alpha = 0.1
+        gb = GradBuckets(sizes, dtype, torch.device("cpu"), world, bucket_bytes=40000)
+        for v, x in zip(gb.views, xs[rank]):
+            v.copy_(x)
+        before = [cpu_epilogue._np(b).copy() for b in gb.buckets]
+        allb = []
+        for r in range(world):
+            g2 = GradBuckets(sizes, dtype, torch.device("cpu"), world, bucket_bytes=40000)
+            for v, x in zip(g2.views, xs[r]):
+                v.copy_(x)
+            allb.append([cpu_epilogue._np(b).copy() for b in g2.buckets])
+        ex.sma_(gb.buckets, alpha)
+        for j, b in enumerate(gb.buckets):
+            s = oracle.reduce_k([allb[r][j] for r in range(world)], name, "sum")
+            want = oracle.sma_blend(before[j], s, name, world, alpha)
+            assert np.array_equal(cpu_epilogue._np(b), want), (name, "sma", j)
+    # integers: the fold and RCCL's order agree
+    n = 5000
+    ints = [np.random.default_rng(7 + r).integers(-2**31, 2**31 - 1, n, dtype=np.int32)
+            for r in range(world)]
+    from kungfu_amd.collective import padded_count
+    bi = torch.zeros(padded_count(n, world, 4), dtype=torch.int32)
+    bi[:n] = torch.from_numpy(ints[rank])
+    ex.all_reduce_([bi], op="max")
+    assert np.array_equal(bi[:n].numpy(), np.max(np.array(ints), axis=0))
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_a2a_rank_order_bit_exact(world):
+    run_world("body_a2a_rank_order", world)

@@ -26,7 +26,8 @@ OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
 # full-tile and ragged-tile stores into one and drops its nt bit.)
 PRODUCT_REDUCE = re.compile(r"^_ZN2kf13reduce_kernelI.*ELi256ELi\d+ELi1ELi0EEEv")
 TUNING_ONLY = re.compile(r"^_ZN2kf13reduce_kernelIfLi0ELi0ELi2ELi256ELi[128]E")
-STREAMING = ("_ZN2kf20reduce_spread_kernelI", "_ZN2kf10sma_kernelI")
+STREAMING = ("_ZN2kf20reduce_spread_kernelI", "_ZN2kf10sma_kernelI",
+             "_ZN2kf19reduce_batch_kernelI")
 # the scalar head/tail and the ragged last tile are the only divergent code
 MAX_EXEC_BRANCHES = 6
 
@@ -74,6 +75,8 @@ def test_product_kernels_found(kernels):
     assert any(k.startswith("_ZN2kf13reduce_kernelINS_6bf16_t") for k in ks)
     assert any(k.startswith(STREAMING[0]) for k in ks)
     assert any(k.startswith(STREAMING[1]) for k in ks)
+    # the multi-bucket launch: 12 dtypes plain (k = 1, 2, runtime) + 4 floats / np
+    assert sum(1 for k in ks if k.startswith(STREAMING[2])) >= 40
 
 
 def test_streaming_loads_and_stores_are_nontemporal(kernels):
