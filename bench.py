@@ -77,13 +77,18 @@ def parse():
                     help="rehearsal only: put every rank on this GPU")
     ap.add_argument("--no-extra", action="store_true",
                     help="N>1: skip the C4/C5/P2P sub-benchmarks")
-    ap.add_argument("--extras", default="c3_per_bucket,c4,c5,c3_ar,c3_p2p,c3_p2p_push,"
-                                        "c3_p2p_hostbar,"
+    ap.add_argument("--extras", default="c4,c5,c3_a2a,c3_torch_fused,c3_per_bucket,c4_torch,"
+                                        "c5_torch,c3_ar,c3_p2p,c3_p2p_push,c3_p2p_hostbar,"
                                         "c4_p2p,c5_p2p",
                     help="N>1: which sub-benchmarks to run (comma list)")
     ap.add_argument("--extras-timeout", type=float, default=240.0,
                     help="N>1: seconds for all sub-benchmarks together; past it the "
                          "line is printed with what finished and the ranks exit")
+    ap.add_argument("--native-timeout", type=float, default=120.0,
+                    help="N>1: seconds for the native exchange's communicator to come up "
+                         "before the torch.distributed path is used instead")
+    ap.add_argument("--no-c1", action="store_true",
+                    help="N=1: skip the C1 (np=2 localhost) sub-object")
     ap.add_argument("--config", default="default", choices=["default", "c1"],
                     help="c1: BASELINE configs[0], np=2 localhost all-reduce of "
                          "one 4 MiB fp32 bucket over the rchannel wire format")
@@ -290,9 +295,19 @@ def c1_child(args):
     else:
         xs, ys = x, np.zeros_like(x)
         fn = None
+        cpu_kind = None
         if args.c1_mode == "cpu":
+            # the reference's own std_transform_2 (oracle/_ref) when built,
+            # else the oracle's restatement of it
             from oracle import oracle
-            fn = ctypes.cast(oracle.lib().oracle_transform2, ctypes.c_void_p)
+            ref = oracle.ref_transform2_addr()
+            if ref is not None:
+                oracle.lib().oracle_set_fold_fn(ctypes.c_void_p(ref))
+                fn = ctypes.cast(oracle.lib().oracle_fold_via_fn, ctypes.c_void_p)
+                cpu_kind = "reference"
+            else:
+                fn = ctypes.cast(oracle.lib().oracle_transform2, ctypes.c_void_p)
+                cpu_kind = "port"
         sess = Session(r, npeers, args.c1_dir, mode="host", host_reduce_fn=fn)
         result = lambda: ys  # noqa: E731
     name = "NegotiatedGrad_0/AllReduce"
@@ -310,32 +325,60 @@ def c1_child(args):
         ts.sort()
         med = ts[len(ts) // 2]
         nbytes = C1_ELEMS * 4
-        print(json.dumps({"mode": args.c1_mode, "correct": ok,
-                          "latency_ms_median": round(med * 1e3, 4),
-                          "latency_ms_min": round(ts[0] * 1e3, 4),
-                          "rate_GiBps": round(4 * (npeers - 1) * nbytes / med / 2**30, 3)}),
-              flush=True)
+        rec = {"mode": args.c1_mode, "correct": ok,
+               "latency_ms_median": round(med * 1e3, 4),
+               "latency_ms_min": round(ts[0] * 1e3, 4),
+               "rate_GiBps": round(4 * (npeers - 1) * nbytes / med / 2**30, 3)}
+        if args.c1_mode == "cpu":
+            rec["kind"] = cpu_kind
+        print(json.dumps(rec), flush=True)
 
 
-def c1_parent(args):
-    """Launch the np peers per mode (subprocesses, one unix socket each)."""
+def c1_run(npeers, modes, steps, warmup, timeout=600):
+    """Launch the np peers per mode (subprocesses, one unix socket each);
+    {mode: rank 0's record}."""
     import subprocess
     import tempfile
     res = {}
-    modes = ("device", "device_chain", "dropin", "cpu") if args.c1_np > 2 else \
-        ("device", "dropin", "cpu")
     for mode in modes:
         with tempfile.TemporaryDirectory() as d:
             cmd = [sys.executable, os.path.abspath(__file__), "--c1-child",
-                   "--c1-mode", mode, "--c1-dir", d, "--steps", str(args.steps),
-                   "--warmup", str(args.warmup), "--c1-np", str(args.c1_np)]
+                   "--c1-mode", mode, "--c1-dir", d, "--steps", str(steps),
+                   "--warmup", str(warmup), "--c1-np", str(npeers)]
             procs = [subprocess.Popen(cmd + ["--c1-rank", str(r)], stdout=subprocess.PIPE,
-                                      text=True, cwd=ROOT) for r in range(args.c1_np)]
-            outs = [p.communicate(timeout=600)[0] for p in procs]
+                                      text=True, cwd=ROOT) for r in range(npeers)]
+            try:
+                outs = [p.communicate(timeout=timeout)[0] for p in procs]
+            except subprocess.TimeoutExpired:
+                for p in procs:
+                    p.kill()
+                res[mode] = {"error": "not finished within %d s" % timeout}
+                continue
             if any(p.returncode for p in procs):
                 res[mode] = {"error": "peer exit codes %s" % [p.returncode for p in procs]}
                 continue
             res[mode] = json.loads(outs[0].strip().splitlines()[-1])
+    return res
+
+
+def c1_summary(steps=100, warmup=10):
+    """BASELINE configs[0] beside the N = 1 line: np = 2 peers on this host,
+    one 4 MiB fp32 bucket, median latency and 4(np-1)*bytes/t
+    (kungfu-bench-allreduce.go:73-80); the device session against the
+    reference's own CPU fold (oracle/_ref) in the same session engine."""
+    res = c1_run(2, ("device", "cpu"), steps, warmup, timeout=180)
+    out = {"workload": "C1: np=2 localhost, one 4 MiB fp32 bucket, 4 x 1 MiB chunks, STAR "
+                       "at rank 0, rchannel framing over unix sockets",
+           "np": 2, "steps": steps, "unit": "GiB/s (4(np-1)*bytes/t, median)"}
+    out.update(res)
+    out["correct"] = all(r.get("correct") is True for r in res.values())
+    return out
+
+
+def c1_parent(args):
+    modes = ("device", "device_chain", "dropin", "cpu") if args.c1_np > 2 else \
+        ("device", "dropin", "cpu")
+    res = c1_run(args.c1_np, modes, args.steps, args.warmup)
     line = {
         "metric": "C1 all-reduce rate 4(np-1)*bytes/t (kungfu-bench-allreduce.go:73-80)",
         "unit": "GiB/s",
@@ -405,18 +448,22 @@ def main():
         workload = "C2: device-resident z = x + y, one 256 MiB fp32 bucket"
         parallelism = "single GPU"
     else:
-        from kungfu_amd.collective import Exchange, GradBuckets
         _progress(rank, "C3 all-reduce, %d ranks" % world)
-        ex = Exchange()
-        # the 256 MiB gradient set as --buckets equal pipelined buckets
+        # the primary exchange: the native C-ABI path (kf_exchange_*: RCCL
+        # reduce-scatter -> HIP /np -> RCCL all-gather), every bucket its own
+        # shards, all 64 in one call (grouped RCCL launches, one batched HIP
+        # epilogue); the torch.distributed path if it cannot be set up
+        prim_ex, how, fallback = _primary_exchange(args, rank, world, dev)
+        from kungfu_amd.collective import GradBuckets
         gb = GradBuckets([n], torch.float32, dev, world, n_buckets=args.buckets)
         pieces = gb.buckets
         gb.views[0].copy_(x)
+        coalesce = fallback is not None  # the torch path fuses contiguous buckets
         # correctness of the timed path before timing it: every rank's x is
         # regenerated from its seed and reduced locally by the HIP k-input
-        # fold (rank order) -> must match the RCCL result (bit-exact at N=2)
+        # fold (rank order) -> must match (bit-exact at N=2, bound beyond)
         from kungfu_amd import ops
-        ex.all_reduce_(pieces, average=True)
+        prim_ex.all_reduce_(pieces, average=True, coalesce=coalesce)
         allx = [torch.randn(n, device=dev, generator=torch.Generator(device=dev).manual_seed(2 * r))
                 for r in range(world)]
         want = ops.bucket_reduce_avg(allx, world)
@@ -430,20 +477,8 @@ def main():
             raise SystemExit("C3 all-reduce parity check failed (N=2 bit-exact / N>2 bound)")
         _progress(rank, "C3 parity ok; timing %d steps" % args.steps)
         gb.views[0].copy_(x)
-        for _ in range(args.warmup):
-            ex.all_reduce_(pieces, average=True)
-        torch.cuda.synchronize()
-        dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            ex.all_reduce_(pieces, average=True)
-        torch.cuda.synchronize()
-        dist.barrier()
-        torch.cuda.synchronize()
-        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        step_s = t.item() / args.steps
+        step_s = _timed(lambda: prim_ex.all_reduce_(pieces, average=True, coalesce=coalesce),
+                        args.steps, args.warmup, dev, world)
         value = world * s_bytes / step_s / 2**30
         busbw = 2 * (world - 1) / world * s_bytes / step_s / 1e9
         _progress(rank, "C3 %.3f ms per step" % (step_s * 1e3))
@@ -453,56 +488,72 @@ def main():
             "xgmi_bound_GBps": round(153.0 * (world - 1), 1),
             "frac_of_xgmi": round(busbw / (153.0 * (world - 1)), 4),
             "buckets": args.buckets,
-            "fused": "contiguous ready buckets run as one RS -> /np -> AG "
-                     "(the reference's nccl_fusion, sync_sgd.py:87-92)",
+            "exchange": how,
         }
-        workload = ("C3: S-SGD all-reduce of %d fp32 buckets (%d MiB) per rank, "
-                    "fused: RCCL reduce-scatter -> HIP /np -> RCCL all-gather"
-                    % (len(pieces), s_bytes >> 20))
+        if fallback is not None:
+            out["collective"]["native_exchange_error"] = fallback
+        workload = ("C3: S-SGD all-reduce of %d fp32 buckets (%d MiB) per rank: %s"
+                    % (len(pieces), s_bytes >> 20, how))
         parallelism = "dp%d" % world
         kt = torch.tensor([kernel_s], dtype=torch.float64, device=dev)
         dist.all_reduce(kt, op=dist.ReduceOp.MAX)
         kernel_s = kt.item()
+        native = prim_ex if fallback is None else None
+        steps_x = min(args.steps, 50)
         # the other multi-GPU configs of BASELINE.json, reported beside `value`
-        extra = (("c3_per_bucket", lambda: bench_c3_per_bucket(world, dev, min(args.steps, 20),
-                                                               ex, pieces, s_bytes)),
-                 ("c4", lambda: bench_c4(world, rank, dev, min(args.steps, 50), 5)),
-                 ("c5", lambda: bench_c5(world, rank, dev, min(args.steps, 50), 5)),
-                 ("c3_ar", lambda: bench_c3_ar(world, rank, dev, min(args.steps, 50), 5, n, x)),
+        extra = (("c4", lambda: bench_c4(world, rank, dev, steps_x, 5, exchange="native")),
+                 ("c5", lambda: bench_c5(world, rank, dev, steps_x, 5, exchange="native")),
+                 ("c3_a2a", lambda: bench_c3_native(world, rank, dev, steps_x, 5, n, x,
+                                                    "a2a", args.buckets)),
+                 ("c3_torch_fused", lambda: bench_c3_torch(world, dev, min(args.steps, 20), n, x,
+                                                           args.buckets, True)),
+                 ("c3_per_bucket", lambda: bench_c3_torch(world, dev, min(args.steps, 20), n, x,
+                                                          args.buckets, False)),
+                 ("c4_torch", lambda: bench_c4(world, rank, dev, steps_x, 5, exchange="torch")),
+                 ("c5_torch", lambda: bench_c5(world, rank, dev, steps_x, 5, exchange="torch")),
+                 ("c3_ar", lambda: bench_c3_ar(world, rank, dev, steps_x, 5, n, x)),
                  # last: the experimental peer-to-peer paths
-                 ("c3_p2p", lambda: bench_c3_p2p(world, rank, dev, min(args.steps, 50), 5,
-                                                 n, x)),
-                 ("c3_p2p_push", lambda: bench_c3_p2p(world, rank, dev, min(args.steps, 50),
-                                                      5, n, x, mode="push")),
-                 ("c3_p2p_hostbar", lambda: bench_c3_p2p(world, rank, dev, min(args.steps, 50),
-                                                         5, n, x, barrier="host")),
-                 ("c4_p2p", lambda: bench_c4(world, rank, dev, min(args.steps, 50), 5,
-                                             exchange="p2p")),
-                 ("c5_p2p", lambda: bench_c5(world, rank, dev, min(args.steps, 50), 5,
-                                             exchange="p2p")))
+                 ("c3_p2p", lambda: bench_c3_p2p(world, rank, dev, steps_x, 5, n, x)),
+                 ("c3_p2p_push", lambda: bench_c3_p2p(world, rank, dev, steps_x, 5, n, x,
+                                                      mode="push")),
+                 ("c3_p2p_hostbar", lambda: bench_c3_p2p(world, rank, dev, steps_x, 5, n, x,
+                                                         barrier="host")),
+                 ("c4_p2p", lambda: bench_c4(world, rank, dev, steps_x, 5, exchange="p2p")),
+                 ("c5_p2p", lambda: bench_c5(world, rank, dev, steps_x, 5, exchange="p2p")))
         # The primary number is measured by now: a sub-benchmark that hangs
         # (a peer mapping refused in a way that blocks, a stuck collective)
-        # must not take it down. Past --extras-timeout every rank stops; rank 0
-        # first prints the line with what was measured so far.
+        # must not take it down. Past --extras-timeout every rank dumps its
+        # stacks and stops with a non-zero status; rank 0 first prints the
+        # line with what was measured so far.
         prim = dict(value=value, step_s=step_s, kernel_s=kernel_s, workload=workload,
                     parallelism=parallelism)
         dog = threading.Timer(args.extras_timeout, _extras_timeout,
                               (args, rank, world, sets, s_bytes, n, hot_s, prim, out))
         dog.daemon = True
         dog.start()
+        wanted = args.extras.split(",")
         for key, fn in extra:
             if args.no_extra:
                 break
-            if key not in args.extras.split(","):
+            if key not in wanted:
                 continue
             _progress(rank, "sub-benchmark %s" % key)
             out["_running"] = key
+            t0 = time.perf_counter()
             try:
-                out[key] = fn()
+                res, err = fn(), None
             except Exception as e:  # keep the primary line; say what failed
-                out[key] = {"error": repr(e)[:300]}
+                res, err = None, repr(e)[:300]
+            # every rank learns whether every rank got through, before any
+            # starts the next sub-benchmark's collectives
+            if not _agree(err is None, dev):
+                res = {"error": err or "failed on another rank"}
+            res["wall_s"] = round(time.perf_counter() - t0, 2)
+            out[key] = res
         out.pop("_running", None)
         dog.cancel()
+        if native is not None:
+            native.close()
 
     res = _result(args, world, sets, s_bytes, n, hot_s,
                   dict(value=value, step_s=step_s, kernel_s=kernel_s, workload=workload,
@@ -513,6 +564,12 @@ def main():
             res["host_staged"] = host_staged(lib, x, y)
         if not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(x, y, args.cpu_seconds)
+        if not args.no_c1:
+            _progress(rank, "C1 (np=2 localhost, device and reference-CPU folds)")
+            try:
+                res["c1"] = c1_summary()
+            except Exception as e:  # the C2 line stands on its own
+                res["c1"] = {"error": repr(e)[:300]}
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:
@@ -563,17 +620,24 @@ def _result(args, world, sets, s_bytes, n, hot_s, prim):
 
 
 def _extras_timeout(args, rank, world, sets, s_bytes, n, hot_s, prim, out):
-    """Watchdog of the N>1 sub-benchmarks (a thread): print the line with the
-    primary number and whatever finished, then end this rank at once."""
-    res = _result(args, world, sets, s_bytes, n, hot_s, prim)
+    """Watchdog of the N>1 sub-benchmarks (a thread): dump every thread's
+    stack (so the stall names itself), print the line with the primary number
+    and whatever finished, then end this rank with a non-zero status — a
+    stuck sub-benchmark is a failure, not a success."""
+    import faulthandler
     stuck = out.pop("_running", "?")
+    print("[bench] rank %d: sub-benchmark %s not finished within --extras-timeout %.0f s; "
+          "stacks:" % (rank, stuck, args.extras_timeout), file=sys.stderr, flush=True)
+    faulthandler.dump_traceback(file=sys.stderr, all_threads=True)
+    res = _result(args, world, sets, s_bytes, n, hot_s, prim)
     res.update(out)
     res[stuck] = {"error": "not finished within --extras-timeout %.0f s; stopped" %
                   args.extras_timeout}
     if rank == 0:
         print(json.dumps(res), flush=True)
+    sys.stdout.flush()
     sys.stderr.flush()
-    os._exit(0)
+    os._exit(3)
 
 
 def _progress(rank, what):
@@ -630,32 +694,153 @@ def _fill(gb, rank_seed, dev, dtype):
         v.copy_(torch.randn(v.numel(), device=dev, generator=g).to(dtype))
 
 
+_NATIVE = {}  # the primary's NativeExchange, reused by the sub-benchmarks
+
+
+def _primary_exchange(args, rank, world, dev):
+    """(exchange, description, why the native path is not used or None).
+    The native C-ABI exchange needs RCCL with one GPU per rank; its
+    communicator is created on a helper thread so that an init that never
+    returns costs --native-timeout seconds and the torch.distributed path,
+    not the whole line. The id is shared on this thread (a torch collective)."""
+    from kungfu_amd.collective import Exchange
+    how_torch = "torch.distributed RCCL RS -> HIP /np -> AG, contiguous buckets fused into one"
+    if args.dist_backend != "nccl" or args.device_index is not None:
+        return Exchange(), how_torch, "not tried: ranks share a GPU (rehearsal)"
+    from kungfu_amd.exchange import NativeExchange
+    box = {}
+    try:
+        uid = NativeExchange.shared_id()
+    except Exception as e:
+        uid, box["err"] = None, repr(e)[:300]
+    if uid is not None:
+        def make():
+            try:
+                box["ex"] = NativeExchange(algo="rs", device=dev, uid=uid)
+            except Exception as e:
+                box["err"] = repr(e)[:300]
+        th = threading.Thread(target=make, daemon=True)
+        th.start()
+        th.join(args.native_timeout)
+    ex = box.get("ex")
+    if _agree(ex is not None, dev):
+        _NATIVE["ex"] = ex
+        return ex, ("native C-ABI exchange (kf_exchange_all_reduce_batch): per bucket RCCL "
+                    "reduce-scatter -> HIP /np -> RCCL all-gather, the buckets of a step in "
+                    "one call (grouped RCCL launches, one batched HIP epilogue)"), None
+    if ex is not None:
+        ex.close()
+    return Exchange(), how_torch, box.get("err", "not ready within %.0f s or failed on "
+                                                 "another rank" % args.native_timeout)
+
+
 def _exchange(kind):
-    """rccl: RS -> HIP epilogue -> AG (collective.Exchange); p2p: the xGMI
-    peer-mapped pull exchange with device barriers (p2p.PeerExchange), whose
-    rank-order fold is bit-exact at every N."""
+    """native: the C-ABI exchange (RCCL + HIP epilogue / rank-order fold);
+    torch: collective.Exchange over torch.distributed; p2p: the xGMI
+    peer-mapped pull exchange with device barriers (p2p.PeerExchange). Every
+    one picks algo "auto": f32 sums go through RCCL's reduce-scatter, bf16
+    through the all-to-all + rank-order fold (bit-exact at every N)."""
     if kind == "p2p":
         from kungfu_amd.p2p import PeerExchange
         return PeerExchange(timeout_s=5.0)
+    if kind == "native":
+        ex = _NATIVE.get("ex")
+        if ex is None:
+            raise RuntimeError("native exchange unavailable (see collective.native_exchange_error)")
+        return _AlgoView(ex, "auto")
     from kungfu_amd.collective import Exchange
     return Exchange()
 
 
-def bench_c3_per_bucket(world, dev, steps, ex, pieces, s_bytes):
-    """C3's buckets issued one RS -> /np -> AG each (no fusion), beside the
-    fused primary. A sub-benchmark (under the --extras-timeout watchdog): with
-    gloo and 4 ranks sharing one GPU, these 64 outstanding async collectives
-    were seen to stall (profiles/r01/README.md), and nothing may stall before
-    the primary line is safe."""
-    per_s = _timed(lambda: ex.all_reduce_(pieces, average=True, coalesce=False),
-                   steps, 2, dev, world)
-    return {"workload": "C3's %d buckets, one RS -> HIP /np -> AG each (no fusion)"
-                        % len(pieces),
+class _AlgoView:
+    """The primary NativeExchange with another algo (one communicator)."""
+
+    def __init__(self, ex, algo):
+        self.ex, self.algo, self.world = ex, algo, ex.world
+
+    def _run(self, fn, *a, **kw):
+        saved, self.ex.algo = self.ex.algo, self.algo
+        try:
+            return fn(*a, **kw)
+        finally:
+            self.ex.algo = saved
+
+    def all_reduce_(self, *a, **kw):
+        return self._run(self.ex.all_reduce_, *a, **kw)
+
+    def sma_(self, *a, **kw):
+        return self._run(self.ex.sma_, *a, **kw)
+
+
+def bench_c3_native(world, rank, dev, steps, warmup, n, x, algo, nb):
+    """C3 through the native exchange with another algo: "a2a" = RCCL
+    all-to-all of every bucket's shards -> HIP rank-order fold (/np fused) ->
+    RCCL all-gather, bit-exact against the local rank-order fold at every N."""
+    from kungfu_amd import ops
+    from kungfu_amd.collective import GradBuckets
+    ex = _exchange("native")
+    ex.algo = algo
+    gb = GradBuckets([n], torch.float32, dev, world, n_buckets=nb)
+    gb.views[0].copy_(x)
+    ex.all_reduce_(gb.buckets, average=True, coalesce=False)
+    allx = [torch.randn(n, device=dev, generator=torch.Generator(device=dev).manual_seed(2 * r))
+            for r in range(world)]
+    ok = bool(torch.equal(gb.views[0], ops.bucket_reduce_avg(allx, world)))
+    del allx
+    if not _agree(ok, dev):
+        return {"error": "native %s exchange not bit-exact against the rank-order fold" % algo}
+    step_s = _timed(lambda: ex.all_reduce_(gb.buckets, average=True, coalesce=False),
+                    steps, warmup, dev, world)
+    s_bytes = n * 4
+    busbw = 2 * (world - 1) / world * s_bytes / step_s / 1e9
+    return {"workload": "C3's %d buckets via the native exchange, algo %s (RCCL all-to-all -> "
+                        "HIP rank-order fold + /np -> RCCL all-gather)" % (nb, algo),
+            "ms_per_step": round(step_s * 1e3, 4),
+            "GiBps_per_gpu": round(s_bytes / step_s / 2**30, 3),
+            "busbw_GBps": round(busbw, 2),
+            "frac_of_xgmi": round(busbw / (153.0 * (world - 1)), 4),
+            "parity": "bit-exact vs the rank-order fold (every N)"}
+
+
+def bench_c3_torch(world, dev, steps, n, x, nb, fused):
+    """C3 through torch.distributed (collective.Exchange, RCCL RS -> HIP /np
+    -> AG): the 64 buckets coalesced into one collective (fused), or one RS ->
+    /np -> AG per bucket, all reduce-scatters in flight first. Checked before
+    timing; a progress line per timed step, so a slow step shows as slow and a
+    stuck one is named by the watchdog's stack dump."""
+    from kungfu_amd import ops
+    from kungfu_amd.collective import Exchange, GradBuckets
+    ex = Exchange()
+    gb = GradBuckets([n], torch.float32, dev, world, n_buckets=nb)
+    gb.views[0].copy_(x)
+    ex.all_reduce_(gb.buckets, average=True, coalesce=fused)
+    allx = [torch.randn(n, device=dev, generator=torch.Generator(device=dev).manual_seed(2 * r))
+            for r in range(world)]
+    want = ops.bucket_reduce_avg(allx, world)
+    ok = (bool(torch.equal(gb.views[0], want)) if world == 2 else
+          _within(gb.views[0], want, sum(a.abs() for a in allx), world))
+    del allx, want
+    if not _agree(ok, dev):
+        return {"error": "torch exchange check failed (N=2 bit-exact / N>2 bound)"}
+    rank = dist.get_rank()
+
+    def step():
+        t0 = time.perf_counter()
+        ex.all_reduce_(gb.buckets, average=True, coalesce=fused)
+        if not fused:
+            torch.cuda.synchronize()
+            _progress(rank, "  c3 per-bucket step %.1f ms" % ((time.perf_counter() - t0) * 1e3))
+
+    per_s = _timed(step, steps, 2, dev, world)
+    s_bytes = n * 4
+    return {"workload": "C3's %d buckets via torch.distributed, %s" % (
+                nb, "coalesced into one RS -> /np -> AG" if fused else
+                "one RS -> HIP /np -> AG per bucket"),
             "ms_per_step": round(per_s * 1e3, 4),
             "busbw_GBps": round(2 * (world - 1) / world * s_bytes / per_s / 1e9, 2)}
 
 
-def bench_c4(world, rank, dev, steps, warmup, exchange="rccl"):
+def bench_c4(world, rank, dev, steps, warmup, exchange="native"):
     """C4: ResNet-50 gradient set (214 tensors, 25,583,592 fp32) fused into 16
     buckets (EvenPartition), S-SGD all-reduce."""
     from kungfu_amd import ops
@@ -672,7 +857,7 @@ def bench_c4(world, rank, dev, steps, warmup, exchange="rccl"):
     ex.all_reduce_(mine.buckets, average=True)
     ok = True
     for b, w, ab, sp in zip(mine.buckets, want, absums, mine.spans):
-        if world == 2 or exchange == "p2p":
+        if world == 2 or exchange == "p2p":  # rank order or two operands
             ok &= bool(torch.equal(b[:sp], w[:sp]))
         else:
             ok &= _within(b[:sp], w[:sp], ab[:sp], world)
@@ -685,8 +870,11 @@ def bench_c4(world, rank, dev, steps, warmup, exchange="rccl"):
     if exchange == "p2p":
         ex.close()
     busbw = 2 * (world - 1) / world * s_bytes / step_s / 1e9
-    how = ("RCCL RS -> HIP /np -> RCCL AG" if exchange == "rccl" else
-           "xGMI P2P pull: rank-order shard fold from peers' HBM + gather, device barriers")
+    how = {"native": "native C-ABI exchange: RCCL RS -> HIP /np -> RCCL AG, 16 buckets "
+                     "in one call",
+           "torch": "torch.distributed RCCL RS -> HIP /np -> RCCL AG",
+           "p2p": "xGMI P2P pull: rank-order shard fold from peers' HBM + gather, "
+                  "device barriers"}[exchange]
     return {"workload": "C4: ResNet-50 grads, 25,583,592 fp32 in %d buckets, S-SGD "
                         "(%s)" % (len(mine.buckets), how),
             "bytes": s_bytes, "ms_per_step": round(step_s * 1e3, 4),
@@ -788,7 +976,7 @@ def bench_c3_p2p(world, rank, dev, steps, warmup, n, x, mode="pull", barrier="de
                       "two fresh inputs: %s" % ("yes" if after else "NO")}
 
 
-def bench_c5(world, rank, dev, steps, warmup, alpha=0.1, exchange="rccl"):
+def bench_c5(world, rank, dev, steps, warmup, alpha=0.1, exchange="native"):
     """C5: BERT-base (first 201 tensors of the fake model, 109,483,778
     params) in bf16 with SynchronousAveragingOptimizer semantics (sum, /np,
     alpha-blend), buckets pipelined."""
@@ -798,8 +986,9 @@ def bench_c5(world, rank, dev, steps, warmup, alpha=0.1, exchange="rccl"):
     ex = _exchange(exchange)
     mine = GradBuckets(sizes, torch.bfloat16, dev, world, bucket_bytes=16 << 20)
     _fill(mine, 700 + rank, dev, torch.bfloat16)
-    # expected after one SMA step: local fp32 fold of every rank's variables
-    # (regenerated), then the blend; bf16 RCCL sums round per hop -> bounded
+    # expected after one SMA step: the local rank-order fold of every rank's
+    # variables (regenerated; fp32 accumulation, one bf16 rounding), then the
+    # blend — every exchange folds bf16 that way (a2a or P2P): bit-exact
     others = []
     for r in range(world):
         gb = GradBuckets(sizes, torch.bfloat16, dev, world, bucket_bytes=16 << 20)
@@ -811,31 +1000,28 @@ def bench_c5(world, rank, dev, steps, warmup, alpha=0.1, exchange="rccl"):
     for i, b in enumerate(mine.buckets):
         s = ops.bucket_reduce([gb.buckets[i] for gb in others])
         want = ops.sma_blend_(v0[i].clone(), s, world, alpha)
-        absum = sum(gb.buckets[i].float().abs() for gb in others)
-        bound = alpha * (world - 1) * 2.0 ** -8 * absum / world + 2 * 2.0 ** -8 * want.float().abs()
-        if exchange == "p2p":  # the same k-input bf16 fold (one rounding), rank order
-            ok &= bool(torch.equal(b, want))
-        else:
-            ok &= bool(((b.float() - want.float()).abs() <= 2 * bound + 1e-30).all())
+        ok &= bool(torch.equal(b, want))
     del others, v0
     if not _agree(ok, dev):
-        return {"error": "C5 check failed (outside the bf16 bound)"}
+        return {"error": "C5 not bit-exact against the rank-order bf16 fold + blend"}
     s_bytes = sum(sizes) * 2
     step_s = _timed(lambda: ex.sma_(mine.buckets, alpha), steps, warmup, dev, world)
     if exchange == "p2p":
         ex.close()
     busbw = 2 * (world - 1) / world * s_bytes / step_s / 1e9
-    how = ("RCCL RS -> RCCL AG -> HIP blend" if exchange == "rccl" else
-           "xGMI P2P pull sum, device barriers -> HIP blend")
+    how = {"native": "native C-ABI exchange: RCCL all-to-all -> HIP rank-order bf16 fold "
+                     "(fp32 accumulation) -> RCCL all-gather -> HIP blend, all buckets in one call",
+           "torch": "torch.distributed all-to-all -> HIP rank-order fold -> all-gather -> "
+                    "HIP blend, pipelined",
+           "p2p": "xGMI P2P pull sum, device barriers -> HIP blend"}[exchange]
     return {"workload": "C5: BERT-base 109,483,778 params bf16, SMA alpha=%.2f, %d "
                         "pipelined buckets (%s)" % (alpha, len(mine.buckets), how),
             "bytes": s_bytes, "ms_per_step": round(step_s * 1e3, 4),
             "GiBps_per_gpu": round(s_bytes / step_s / 2**30, 3),
             "busbw_GBps": round(busbw, 2),
             "frac_of_xgmi": round(busbw / (153.0 * (world - 1)), 4),
-            "parity": "bf16 unpinned (DESIGN.md); " + (
-                "bit-exact vs the local rank-order fold + blend" if exchange == "p2p"
-                else "checked within bound")}
+            "parity": "bf16 unpinned (DESIGN.md); bit-exact vs the local rank-order fold "
+                      "+ blend"}
 
 
 

@@ -36,7 +36,26 @@ def _arr(t, vals):
 
 
 class NativeExchange:
-    def __init__(self, group=None, algo="auto", device=None):
+    @staticmethod
+    def shared_id(group=None):
+        """Rank 0's unique id, broadcast to the group (gpu_collective.cpp:
+        196-198); every rank of the group calls it."""
+        world = dist.get_world_size(group) if dist.is_initialized() else 1
+        rank = dist.get_rank(group) if dist.is_initialized() else 0
+        lib = _lib.load()
+        uid = (ctypes.c_char * 128)()
+        if rank == 0:
+            _lib.check(lib.kf_exchange_unique_id(uid), "kf_exchange_unique_id")
+        if world > 1:
+            obj = [bytes(uid) if rank == 0 else None]
+            src = dist.get_global_rank(group, 0) if group is not None else 0
+            dist.broadcast_object_list(obj, src=src, group=group)
+            return obj[0]
+        return bytes(uid)
+
+    def __init__(self, group=None, algo="auto", device=None, uid=None):
+        """uid: the bytes of shared_id(group), when the caller shared it
+        already (e.g. to create the communicator on another thread)."""
         if algo not in ALGOS:
             raise ValueError("algo must be one of %s" % sorted(ALGOS))
         self.algo = algo
@@ -47,16 +66,10 @@ class NativeExchange:
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device())
         self.device = torch.device(device)
-        uid = (ctypes.c_char * 128)()
-        if self.rank == 0:
-            _lib.check(self.lib.kf_exchange_unique_id(uid), "kf_exchange_unique_id")
-        if self.world > 1:
-            # gpu_collective.cpp:196-198: rank 0's id, broadcast to the group
-            obj = [bytes(uid) if self.rank == 0 else None]
-            src = dist.get_global_rank(group, 0) if group is not None else 0
-            dist.broadcast_object_list(obj, src=src, group=group)
-            ctypes.memmove(uid, obj[0], 128)
-        h = self.lib.kf_exchange_create(uid, self.rank, self.world, self.device.index)
+        if uid is None:
+            uid = self.shared_id(group)
+        buf = (ctypes.c_char * 128).from_buffer_copy(uid)
+        h = self.lib.kf_exchange_create(buf, self.rank, self.world, self.device.index)
         if not h:
             raise _lib.KungFuAMDError("kf_exchange_create: " +
                                       self.lib.kf_exchange_last_error().decode())

@@ -419,3 +419,17 @@ double oracle_bench_fn(void *fn, const void *x, const void *y, void *z, int64_t 
     if (!fn) return -1.0;
     return bench((transform2_fn)fn, x, y, z, n, dt, op, reps, threads, chunk_bytes);
 }
+
+/* The session's host fold (kf_host_reduce_fn, include/kungfu_amd.h) around a
+ * std_transform_2-compatible function: bench.py's C1 CPU mode folds with the
+ * reference's own compiled std_transform_2 (oracle/_ref) through this. */
+static transform2_fn g_fold_fn;
+
+void oracle_set_fold_fn(void *fn) { g_fold_fn = (transform2_fn)fn; }
+
+int oracle_fold_via_fn(const void *x, const void *y, void *out, int64_t n, int dt, int op)
+{
+    if (!g_fold_fn || n > 2147483647) return 3;
+    g_fold_fn(x, y, out, (int)n, dt, op);
+    return 0;
+}
