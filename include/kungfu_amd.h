@@ -476,6 +476,20 @@ int kf_exchange_info(kf_exchange_t *ex, int *rank, int *world, int *device);
 void kf_exchange_destroy(kf_exchange_t *ex);
 const char *kf_exchange_last_error(void);
 
+/* Loopback transport, for testing the exchange on ONE device: a group of
+ * `world` ranks that are threads of one process (RCCL refuses two ranks on
+ * one GPU). Each rank's exchange runs the same code as over RCCL — shards,
+ * tails, workspace, batched folds, scheduler — with every collective a
+ * rendezvous of the ranks' threads that moves the bytes with hipMemcpy (the
+ * reduce-scatter folds in rank order on the host; no f16/bf16 reduce-scatter).
+ * Every rank's calls must come from its own thread. */
+#pragma GCC visibility pop
+typedef struct kf_loopback kf_loopback_t; /* opaque */
+#pragma GCC visibility push(default)
+kf_loopback_t *kf_loopback_create(int world);
+void kf_loopback_destroy(kf_loopback_t *g);
+kf_exchange_t *kf_exchange_create_loopback(kf_loopback_t *g, int rank, int device);
+
 #pragma GCC visibility pop
 
 #ifdef __cplusplus

@@ -77,6 +77,9 @@ EXPORTED = (
     "kf_exchange_info",
     "kf_exchange_destroy",
     "kf_exchange_last_error",
+    "kf_loopback_create",
+    "kf_loopback_destroy",
+    "kf_exchange_create_loopback",
 )
 
 STATUS = {
@@ -280,6 +283,12 @@ def load():
     lib.kf_exchange_destroy.restype = None
     lib.kf_exchange_last_error.argtypes = []
     lib.kf_exchange_last_error.restype = ctypes.c_char_p
+    lib.kf_loopback_create.argtypes = [c_int]
+    lib.kf_loopback_create.restype = c_void_p
+    lib.kf_loopback_destroy.argtypes = [c_void_p]
+    lib.kf_loopback_destroy.restype = None
+    lib.kf_exchange_create_loopback.argtypes = [c_void_p, c_int, c_int]
+    lib.kf_exchange_create_loopback.restype = c_void_p
     _lib = lib
     return lib
 

@@ -124,7 +124,8 @@ const Rccl &rccl()
 
 int nccl_fail(ncclResult_t r, const char *what)
 {
-    return fail(KF_ERR_RCCL, std::string(what) + ": " + rccl().GetErrorString(r));
+    const char *why = rccl().ok ? rccl().GetErrorString(r) : "RCCL error";
+    return fail(KF_ERR_RCCL, std::string(what) + ": " + why + " (" + std::to_string(int(r)) + ")");
 }
 
 #define KF_NCCL(call)                                                          \
@@ -200,6 +201,208 @@ ncclRedOp_t nccl_op(KungFu_Op op)
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// ---------------------------------------------------------------------------
+// Loopback transport (testing): the RCCL entry points the exchange uses,
+// re-implemented for `world` ranks that are threads of ONE process on ONE
+// device, so the sharding, tails, workspace and fold logic of every world
+// size runs on a single GPU (RCCL itself refuses two ranks on one device).
+// Every collective is a rendezvous: each rank synchronises its stream and
+// posts its buffers; the last to arrive moves the bytes (hipMemcpy, and for
+// the reduce-scatter a host fold in rank order) and releases the others.
+// ---------------------------------------------------------------------------
+struct LoopSlot {
+    int arrived = 0, left = 0;
+    bool done   = false;
+    std::vector<const void *> send;
+    std::vector<void *> recv;
+};
+
+struct LoopGroup {
+    int world;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::map<uint64_t, LoopSlot> slots;
+    explicit LoopGroup(int w) : world(w) {}
+};
+
+struct LoopComm {
+    LoopGroup *g;
+    int rank;
+    uint64_t seq = 0;
+};
+
+size_t nccl_size(ncclDataType_t t)
+{
+    switch (t) {
+    case ncclInt8: case ncclUint8: return 1;
+    case ncclFloat16: case ncclBfloat16: return 2;
+    case ncclInt32: case ncclUint32: case ncclFloat32: return 4;
+    case ncclInt64: case ncclUint64: case ncclFloat64: return 8;
+    default: return 0;
+    }
+}
+
+template <typename T>
+void host_fold(const std::vector<std::vector<char>> &in, size_t off, size_t n, ncclRedOp_t op,
+               char *out)
+{
+    for (size_t i = 0; i < n; ++i) {
+        T a = reinterpret_cast<const T *>(in[0].data() + off)[i];
+        for (size_t j = 1; j < in.size(); ++j) {
+            const T b = reinterpret_cast<const T *>(in[j].data() + off)[i];
+            if (op == ncclSum) a = static_cast<T>(a + b);
+            else if (op == ncclProd) a = static_cast<T>(a * b);
+            else if (op == ncclMin) a = (b < a) ? b : a;
+            else a = (a < b) ? b : a;
+        }
+        reinterpret_cast<T *>(out)[i] = a;
+    }
+}
+
+// rendezvous; `move` runs once, on the last rank to arrive, with every
+// rank's posted buffers
+template <typename F>
+ncclResult_t loop_collective(ncclComm_t comm, const void *send, void *recv, hipStream_t s, F move)
+{
+    auto *c = reinterpret_cast<LoopComm *>(comm);
+    if (hipStreamSynchronize(s) != hipSuccess) return ncclUnhandledCudaError;
+    LoopGroup *g = c->g;
+    std::unique_lock<std::mutex> lk(g->mu);
+    LoopSlot &sl = g->slots[c->seq];
+    const uint64_t seq = c->seq++;
+    if (sl.send.empty()) {
+        sl.send.assign(g->world, nullptr);
+        sl.recv.assign(g->world, nullptr);
+    }
+    sl.send[c->rank] = send;
+    sl.recv[c->rank] = recv;
+    ncclResult_t rc = ncclSuccess;
+    if (++sl.arrived == g->world) {
+        rc      = move(sl.send, sl.recv);
+        sl.done = true;
+        g->cv.notify_all();
+    } else {
+        g->cv.wait(lk, [&] { return sl.done; });
+    }
+    if (++sl.left == g->world) g->slots.erase(seq);
+    return rc;
+}
+
+ncclResult_t loop_reduce_scatter(const void *send, void *recv, size_t count, ncclDataType_t t,
+                                 ncclRedOp_t op, ncclComm_t comm, hipStream_t s)
+{
+    return loop_collective(comm, send, recv, s, [&](const std::vector<const void *> &sd,
+                                                     const std::vector<void *> &rv) {
+        const size_t sz = nccl_size(t), W = sd.size();
+        if (sz == 0 || t == ncclFloat16 || t == ncclBfloat16) return ncclInvalidArgument;
+        std::vector<std::vector<char>> in(W, std::vector<char>(count * W * sz));
+        for (size_t j = 0; j < W; ++j) {
+            if (hipMemcpy(in[j].data(), sd[j], count * W * sz, hipMemcpyDeviceToHost) != hipSuccess)
+                return ncclUnhandledCudaError;
+        }
+        std::vector<char> out(count * sz);
+        for (size_t r = 0; r < W; ++r) {
+            const size_t off = r * count * sz;
+            switch (t) {
+            case ncclInt8: host_fold<int8_t>(in, off, count, op, out.data()); break;
+            case ncclUint8: host_fold<uint8_t>(in, off, count, op, out.data()); break;
+            case ncclInt32: host_fold<int32_t>(in, off, count, op, out.data()); break;
+            case ncclUint32: host_fold<uint32_t>(in, off, count, op, out.data()); break;
+            case ncclInt64: host_fold<int64_t>(in, off, count, op, out.data()); break;
+            case ncclUint64: host_fold<uint64_t>(in, off, count, op, out.data()); break;
+            case ncclFloat32: host_fold<float>(in, off, count, op, out.data()); break;
+            default: host_fold<double>(in, off, count, op, out.data()); break;
+            }
+            if (hipMemcpy(rv[r], out.data(), count * sz, hipMemcpyHostToDevice) != hipSuccess)
+                return ncclUnhandledCudaError;
+        }
+        return ncclSuccess;
+    });
+}
+
+ncclResult_t loop_all_gather(const void *send, void *recv, size_t count, ncclDataType_t t,
+                             ncclComm_t comm, hipStream_t s)
+{
+    return loop_collective(comm, send, recv, s, [&](const std::vector<const void *> &sd,
+                                                     const std::vector<void *> &rv) {
+        const size_t b = count * nccl_size(t), W = sd.size();
+        for (size_t r = 0; r < W; ++r) {
+            for (size_t j = 0; j < W; ++j) {
+                char *dst = static_cast<char *>(rv[r]) + j * b;
+                if (dst == sd[j]) continue;  // in place
+                if (hipMemcpy(dst, sd[j], b, hipMemcpyDeviceToDevice) != hipSuccess)
+                    return ncclUnhandledCudaError;
+            }
+        }
+        return ncclSuccess;
+    });
+}
+
+ncclResult_t loop_all_to_all(const void *send, void *recv, size_t count, ncclDataType_t t,
+                             ncclComm_t comm, hipStream_t s)
+{
+    return loop_collective(comm, send, recv, s, [&](const std::vector<const void *> &sd,
+                                                     const std::vector<void *> &rv) {
+        const size_t b = count * nccl_size(t), W = sd.size();
+        for (size_t r = 0; r < W; ++r) {
+            for (size_t j = 0; j < W; ++j) {
+                if (hipMemcpy(static_cast<char *>(rv[r]) + j * b,
+                              static_cast<const char *>(sd[j]) + r * b, b,
+                              hipMemcpyDeviceToDevice) != hipSuccess)
+                    return ncclUnhandledCudaError;
+            }
+        }
+        return ncclSuccess;
+    });
+}
+
+ncclResult_t loop_broadcast(const void *send, void *recv, size_t count, ncclDataType_t t, int root,
+                            ncclComm_t comm, hipStream_t s)
+{
+    return loop_collective(comm, send, recv, s, [&](const std::vector<const void *> &sd,
+                                                     const std::vector<void *> &rv) {
+        const size_t b = count * nccl_size(t);
+        for (size_t r = 0; r < rv.size(); ++r) {
+            if (rv[r] == sd[root]) continue;
+            if (hipMemcpy(rv[r], sd[root], b, hipMemcpyDeviceToDevice) != hipSuccess)
+                return ncclUnhandledCudaError;
+        }
+        return ncclSuccess;
+    });
+}
+
+ncclResult_t loop_nop() { return ncclSuccess; }
+ncclResult_t loop_async_error(ncclComm_t, ncclResult_t *e)
+{
+    *e = ncclSuccess;
+    return ncclSuccess;
+}
+ncclResult_t loop_destroy(ncclComm_t comm)
+{
+    delete reinterpret_cast<LoopComm *>(comm);
+    return ncclSuccess;
+}
+const char *loop_error_string(ncclResult_t) { return "loopback transport error"; }
+
+const Rccl &loop_rccl()
+{
+    static const Rccl r = [] {
+        Rccl x;
+        x.CommDestroy       = loop_destroy;
+        x.CommGetAsyncError = loop_async_error;
+        x.ReduceScatter     = loop_reduce_scatter;
+        x.AllGather         = loop_all_gather;
+        x.AllToAll          = loop_all_to_all;
+        x.Broadcast         = loop_broadcast;
+        x.GroupStart        = loop_nop;
+        x.GroupEnd          = loop_nop;
+        x.GetErrorString    = loop_error_string;
+        x.ok                = true;
+        return x;
+    }();
+    return r;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -226,6 +429,7 @@ struct Done {
 };
 
 struct kf_exchange {
+    const Rccl *R   = nullptr;  // librccl, or the loopback transport
     ncclComm_t comm = nullptr;
     int rank = 0, world = 1, device = 0;
     std::mutex mu;  // one collective sequence at a time
@@ -319,7 +523,7 @@ int kf_exchange::batch(const void *const *sends, void *const *recvs, const size_
                        int nb, KungFu_Datatype dt, KungFu_Op op, int average, int algo,
                        hipStream_t s)
 {
-    const Rccl &R = rccl();
+    const Rccl &R = *this->R;
     const int sz  = tsize(dt);
     const int W = world, r = rank;
     if (W == 1) {  // a single peer: the sum is the bucket, x / 1 == x
@@ -497,7 +701,7 @@ void kf_exchange::complete_loop()
         }
         if (rc == KF_OK) {
             ncclResult_t ae = ncclSuccess;
-            if (rccl().CommGetAsyncError(comm, &ae) != ncclSuccess || ae != ncclSuccess) {
+            if (R->CommGetAsyncError(comm, &ae) != ncclSuccess || ae != ncclSuccess) {
                 rc = KF_ERR_RCCL;
             }
         }
@@ -519,7 +723,7 @@ kf_exchange::~kf_exchange()
     if (issuer.joinable()) issuer.join();
     if (completer.joinable()) completer.join();
     DeviceGuard g(device);
-    if (comm) (void)rccl().CommDestroy(comm);
+    if (comm) (void)R->CommDestroy(comm);
     if (ws) (void)hipFree(ws);
     if (ws_ev) (void)hipEventDestroy(ws_ev);
     if (own) (void)hipStreamDestroy(own);
@@ -576,6 +780,7 @@ kf_exchange_t *kf_exchange_create(const void *id, int rank, int world, int devic
     }
     DeviceGuard g(device);
     auto *ex   = new kf_exchange;
+    ex->R      = &rccl();
     ex->rank   = rank;
     ex->world  = world;
     ex->device = device;
@@ -697,7 +902,7 @@ int kf_exchange_begin_step(kf_exchange_t *ex, const char *const *names, int n, i
         if (e != hipSuccess) rc = hip_fail(e, "order broadcast buffer");
         if (rc == KF_OK) {
             std::lock_guard<std::mutex> g2(ex->mu);
-            ncclResult_t r = rccl().Broadcast(d, d, n, ncclInt32, 0, ex->comm, ex->own);
+            ncclResult_t r = ex->R->Broadcast(d, d, n, ncclInt32, 0, ex->comm, ex->own);
             if (r != ncclSuccess) rc = nccl_fail(r, "ncclBroadcast(order)");
         }
         if (rc == KF_OK) {
@@ -764,7 +969,7 @@ int kf_exchange_check(kf_exchange_t *ex)
 {
     if (!ex) return KF_ERR_ARG;
     ncclResult_t ae = ncclSuccess;
-    KF_NCCL(rccl().CommGetAsyncError(ex->comm, &ae));
+    KF_NCCL(ex->R->CommGetAsyncError(ex->comm, &ae));
     if (ae != ncclSuccess) return nccl_fail(ae, "RCCL asynchronous error");
     return KF_OK;
 }
@@ -779,6 +984,37 @@ int kf_exchange_info(kf_exchange_t *ex, int *rank, int *world, int *device)
 }
 
 void kf_exchange_destroy(kf_exchange_t *ex) { delete ex; }
+
+kf_loopback_t *kf_loopback_create(int world)
+{
+    if (world < 1) return nullptr;
+    return reinterpret_cast<kf_loopback_t *>(new LoopGroup(world));
+}
+
+void kf_loopback_destroy(kf_loopback_t *g) { delete reinterpret_cast<LoopGroup *>(g); }
+
+kf_exchange_t *kf_exchange_create_loopback(kf_loopback_t *g, int rank, int device)
+{
+    auto *lg = reinterpret_cast<LoopGroup *>(g);
+    if (!lg || rank < 0 || rank >= lg->world || device < 0) {
+        fail(KF_ERR_ARG, "kf_exchange_create_loopback: bad arguments");
+        return nullptr;
+    }
+    DeviceGuard dg(device);
+    auto *ex   = new kf_exchange;
+    ex->R      = &loop_rccl();
+    ex->rank   = rank;
+    ex->world  = lg->world;
+    ex->device = device;
+    ex->comm   = reinterpret_cast<ncclComm_t>(new LoopComm{lg, rank});
+    if (hipEventCreateWithFlags(&ex->ws_ev, hipEventDisableTiming) != hipSuccess ||
+        hipStreamCreateWithFlags(&ex->own, hipStreamNonBlocking) != hipSuccess) {
+        fail(KF_ERR_HIP, "kf_exchange_create_loopback: event/stream");
+        delete ex;
+        return nullptr;
+    }
+    return ex;
+}
 
 const char *kf_exchange_last_error(void) { return t_ex_error.c_str(); }
 

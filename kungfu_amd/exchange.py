@@ -77,6 +77,23 @@ class NativeExchange:
         self._side = None
         self._sums = {}
 
+    @classmethod
+    def loopback(cls, group, rank, algo="auto", device=None):
+        """Rank `rank` of a LoopbackGroup: the same exchange over the loopback
+        transport (ranks are threads of this process on one device; testing)."""
+        self = cls.__new__(cls)
+        if algo not in ALGOS:
+            raise ValueError("algo must be one of %s" % sorted(ALGOS))
+        self.algo, self.group, self.world, self.rank = algo, None, group.world, rank
+        self.lib = _lib.load()
+        self.device = torch.device(device if device is not None else "cuda:0")
+        h = self.lib.kf_exchange_create_loopback(group._h, rank, self.device.index)
+        if not h:
+            raise _lib.KungFuAMDError("kf_exchange_create_loopback: " +
+                                      self.lib.kf_exchange_last_error().decode())
+        self._h, self._side, self._sums = h, None, {}
+        return self
+
     # -- the optimizers' interface (collective.Exchange) --------------------
     def _check(self, buckets):
         for b in buckets:
@@ -167,6 +184,23 @@ class NativeExchange:
             self.close()
         except Exception:
             pass
+
+
+class LoopbackGroup:
+    """kf_loopback_create: `world` ranks as threads of one process on one GPU
+    (include/kungfu_amd.h, "Loopback transport")."""
+
+    def __init__(self, world):
+        self.world = world
+        self.lib = _lib.load()
+        self._h = self.lib.kf_loopback_create(world)
+        if not self._h:
+            raise _lib.KungFuAMDError("kf_loopback_create(%d)" % world)
+
+    def close(self):
+        if self._h:
+            self.lib.kf_loopback_destroy(self._h)
+            self._h = None
 
 
 class _Handle:

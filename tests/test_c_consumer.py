@@ -31,3 +31,30 @@ def test_c_consumer_on_gpu(binary):
     r = subprocess.run([binary], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "ok" in r.stdout
+
+
+@pytest.fixture(scope="module")
+def exchange_binary(tmp_path_factory):
+    """tests/c/test_exchange.cpp: a C++ host of kf_exchange_* through the C
+    ABI alone (the reference's C++ side, gpu_collective.cpp / scheduler.cpp)."""
+    out = str(tmp_path_factory.mktemp("cx") / "test_exchange")
+    lib = os.path.join(ROOT, "kungfu_amd")
+    subprocess.run(["g++", "-std=c++17", "-Wall", "-Wextra", "-Werror", "-D__HIP_PLATFORM_AMD__",
+                    "-I", os.path.join(ROOT, "include"), "-I", "/opt/rocm/include",
+                    os.path.join(ROOT, "tests", "c", "test_exchange.cpp"),
+                    "-L", lib, "-lkungfu_amd", "-Wl,-rpath," + lib,
+                    "-L", "/opt/rocm/lib", "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib",
+                    "-lpthread", "-o", out], check=True)
+    return out
+
+
+def test_cpp_exchange_host_builds(exchange_binary):
+    r = subprocess.run([exchange_binary], capture_output=True, text=True, timeout=300)
+    assert r.returncode in (0, 77), r.stdout + r.stderr
+
+
+@pytest.mark.gpu
+def test_cpp_exchange_host_on_gpu(exchange_binary):
+    r = subprocess.run([exchange_binary], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "exchange ok" in r.stdout

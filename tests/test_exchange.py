@@ -219,3 +219,142 @@ def test_world1_native_exchange():
         assert all(st == 0 for _, st in seen) and len(seen) == 18
         assert all(torch.all(b == i) for i, b in enumerate(bufs))
         ex.close()
+
+
+# ---- the exchange's multi-rank logic over the loopback transport ------------
+
+def _loop_ranks(world, body):
+    """Run body(rank, ex) on `world` threads, each with its own exchange of
+    one loopback group; re-raise the first failure."""
+    import threading
+    import torch
+    from kungfu_amd.exchange import LoopbackGroup, NativeExchange
+    g = LoopbackGroup(world)
+    errs = []
+
+    def run(r):
+        try:
+            torch.cuda.set_device(0)
+            ex = NativeExchange.loopback(g, r)
+            body(r, ex)
+            torch.cuda.synchronize()
+            ex.close()
+        except Exception:
+            errs.append("rank %d: %s" % (r, traceback.format_exc()))
+
+    ts = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=300)
+    g.close()
+    assert not errs, "\n".join(errs)
+    assert not any(t.is_alive() for t in ts), "a rank did not finish"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
+def test_exchange_multi_rank_loopback(world):
+    """The N > 1 code of kf_exchange (shards, tails of count % world, the
+    workspace, batched folds, in-place all-gather, SMA) at worlds 2-8 on one
+    GPU: the loopback transport moves the bytes where RCCL would, its
+    reduce-scatter folds in rank order, so every algo is bit-exact against the
+    oracle's rank-order fold."""
+    import torch
+    from oracle import oracle
+    dev = _gpu()
+    counts = [1, 7, world * 1000 + 3, 262147, world * 4096]
+
+    def body(rank, ex):
+        for algo in ("rs", "a2a", "auto"):
+            for name, avg in (("f32", True), ("bf16", True), ("f16", False), ("i32", False)):
+                if algo == "rs" and name in ("bf16", "f16"):
+                    continue  # the loopback has no half-precision reduce-scatter
+                seeds = [[1000 * r + 10 * b + len(algo) for b in range(len(counts))]
+                         for r in range(world)]
+                hs = [[_rand(name, n, seeds[r][b]) for b, n in enumerate(counts)]
+                      for r in range(world)]
+                bufs = [_to_dev(hs[rank][b], name, dev) for b in range(len(counts))]
+                ex.algo = algo
+                ex.all_reduce_(bufs, average=avg, coalesce=False)
+                torch.cuda.synchronize()
+                for b in range(len(counts)):
+                    ins = [hs[r][b] for r in range(world)]
+                    want = (oracle.reduce_avg(ins, name, world) if avg else
+                            oracle.reduce_k(ins, name, "sum"))
+                    assert np.array_equal(_to_np(bufs[b], name), want), (algo, name, b)
+        # MAX on i32 (RCCL's reduce-scatter under auto) and u16 SUM (no RCCL
+        # reduction type: the all-to-all fold)
+        ex.algo = "auto"
+        hs = [_rand("i32", 50001, 77 + r) for r in range(world)]
+        b = _to_dev(hs[rank], "i32", dev)
+        ex.all_reduce_([b], op="max")
+        torch.cuda.synchronize()
+        assert np.array_equal(_to_np(b, "i32"), np.max(np.array(hs), axis=0))
+        us = [np.random.default_rng(5 + r).integers(0, 65535, 9999).astype(np.uint16)
+              for r in range(world)]
+        ub = torch.from_numpy(us[rank].view(np.int16)).to(dev)
+        lib = ex.lib
+        from kungfu_amd import _lib
+        _lib.check(lib.kf_exchange_all_reduce(ex._h, ub.data_ptr(), ub.data_ptr(), ub.numel(),
+                                              0x00208, 0, 0, 0,
+                                              torch.cuda.current_stream().cuda_stream), "u16")
+        torch.cuda.synchronize()
+        assert np.array_equal(ub.cpu().numpy().view(np.uint16), oracle.reduce_k(us, "u16", "sum"))
+        # out of place: send untouched, recv = the average
+        xs = [_rand("f32", 30011, 900 + r) for r in range(world)]
+        x = _to_dev(xs[rank], "f32", dev)
+        y = torch.empty_like(x)
+        _lib.check(lib.kf_exchange_all_reduce(ex._h, x.data_ptr(), y.data_ptr(), x.numel(),
+                                              0x20408, 0, 1, 0,
+                                              torch.cuda.current_stream().cuda_stream), "oop")
+        torch.cuda.synchronize()
+        assert np.array_equal(_to_np(x, "f32"), xs[rank])
+        assert np.array_equal(_to_np(y, "f32"), oracle.reduce_avg(xs, "f32", world))
+        # SMA, bf16 (auto: the all-to-all fold, fp32 accumulation)
+        vs = [_rand("bf16", 20000 + 3, 300 + r) for r in range(world)]
+        v = _to_dev(vs[rank], "bf16", dev)
+        ex.sma_([v], 0.1)
+        torch.cuda.synchronize()
+        s = oracle.reduce_k(vs, "bf16", "sum")
+        assert np.array_equal(_to_np(v, "bf16"),
+                              oracle.sma_blend(vs[rank], s, "bf16", world, 0.1))
+
+    _loop_ranks(world, body)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_scheduler_orders_across_ranks(world):
+    """NCCLScheduler semantics with several ranks: every rank starts the
+    step's names in its own order; the issue order is the agreed one (step 0:
+    the given order; from step 1 on, rank 0's arrival order of step 0,
+    broadcast over the communicator), the same on every rank, and every
+    all-reduce is right."""
+    import torch
+    from kungfu_amd.exchange import Scheduler
+    dev = _gpu()
+    names = ["grad/%d" % i for i in range(7)]
+    orders = {}
+
+    def body(rank, ex):
+        sch = Scheduler(ex, auto_order=True)
+        rng = np.random.default_rng(rank)
+        got = []
+        for step in range(3):
+            bufs = [torch.full((5000 + i,), float(rank + 1), device=dev) for i in range(7)]
+            sch.begin_step(names)
+            arrival = list(names) if step else [names[i] for i in rng.permutation(7)]
+            if rank == 0 and step == 0:
+                arrival = names[3:] + names[:3]
+            for nm in arrival:
+                sch.start(nm, bufs[names.index(nm)])
+            got.append(sch.wait_all())
+            torch.cuda.synchronize()
+            assert all(torch.all(b == world * (world + 1) / 2) for b in bufs)
+        orders[rank] = got
+
+    _loop_ranks(world, body)
+    for r in range(world):
+        assert orders[r][0] == names
+        assert orders[r][1] == names[3:] + names[:3] == orders[r][2]
