@@ -404,10 +404,11 @@ const char *kf_p2p_last_error(void);
  *                           bf16 with fp32 accumulation and one rounding,
  *                           fp16 rounded per hop — equal to the P2P path;
  *                           same xGMI bytes as the reduce-scatter.
- *   KF_ALGO_AUTO            reduce-scatter for integers and f32/f64 SUM
- *                           (RCCL's own order; integers exact), all-to-all
- *                           for f16/bf16 and float MIN/MAX (the build's
- *                           defined semantics) and for u16/i16.
+ *   KF_ALGO_AUTO            reduce-scatter for integers and f32/f64
+ *                           (RCCL's own order; integers exact; float MIN/MAX
+ *                           differ from std::min/max only on NaN inputs),
+ *                           all-to-all for f16/bf16 (the build's defined
+ *                           semantics) and for u16/i16 (no RCCL type).
  * A count that does not split into world shards sends its last count % world
  * elements through an all-gather and the same rank-order fold. Everything
  * is queued on the caller's stream (no host sync, like RCCL); calls on one

@@ -95,15 +95,15 @@ def coalesce_runs(buckets):
 def resolve_algo(algo, dtype, op, world):
     """"rs" (RCCL reduce-scatter) or "a2a" (all-to-all + HIP rank-order fold)
     for one bucket dtype; "auto" keeps RCCL's reduce-scatter where its order
-    cannot change the defined result's meaning (integers; f32/f64 SUM, the
-    north_star's path) and folds on the GPU where the build defines the
-    arithmetic (f16/bf16, float MIN/MAX; kf_exchange.hip resolve_algo)."""
+    cannot change what the result means (integers; f32/f64, the north_star's
+    path; for MIN/MAX only NaN inputs could select differently) and folds on
+    the GPU where the build defines the arithmetic: f16 (per-hop rounding) and
+    bf16 (fp32 accumulation, one rounding) — kf_exchange.hip resolve_algo."""
     if algo in ("rs", "a2a"):
         return algo
     if algo != "auto":
         raise ValueError("algo must be 'auto', 'rs' or 'a2a'")
-    own = dtype in (torch.float16, torch.bfloat16) or (
-        dtype.is_floating_point and op in (OP.MIN, OP.MAX))
+    own = dtype in (torch.float16, torch.bfloat16)
     return "a2a" if own and world <= 16 else "rs"
 
 

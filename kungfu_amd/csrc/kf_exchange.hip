@@ -507,8 +507,8 @@ static int resolve_algo(int algo, KungFu_Datatype dt, KungFu_Op op, int world, i
         return KF_OK;
     }
     if (algo != KF_ALGO_AUTO) return fail(KF_ERR_ARG, "unknown algo");
-    const bool own_semantics = dt == KungFu_FLOAT16 || dt == KungFu_BFLOAT16 ||
-                               (is_float(dt) && (op == KungFu_MIN || op == KungFu_MAX));
+    (void)op;  // MIN/MAX through RCCL differ from std::min/max only on NaN inputs
+    const bool own_semantics = dt == KungFu_FLOAT16 || dt == KungFu_BFLOAT16;
     if (world <= KF_MAX_INPUTS && (own_semantics || !rs_ok)) {
         *out = KF_ALGO_ALL_TO_ALL;
     } else if (rs_ok) {

@@ -10,9 +10,9 @@ buckets to ONE native call:
 
   algo="rs"   ncclReduceScatter -> HIP /np on the shard -> ncclAllGather
   algo="a2a"  ncclAllToAll -> HIP rank-order fold (/np fused) -> ncclAllGather
-  algo="auto" rs for integers and f32/f64 SUM, a2a for f16/bf16 and float
-              MIN/MAX (the build's defined semantics: bf16 accumulates in fp32
-              and rounds once, bit-identical to the P2P exchange and the oracle)
+  algo="auto" rs for integers and f32/f64, a2a for f16/bf16 (the build's
+              defined semantics: bf16 accumulates in fp32 and rounds once,
+              bit-identical to the P2P exchange and the oracle)
 
 Each phase of a call is one grouped RCCL launch and all shard epilogues one
 batched HIP launch, so a step of 64 buckets costs 3 launches whatever the
