@@ -12,6 +12,41 @@ import torch.distributed as dist
 from ..collective import Exchange, padded_count
 
 _exchange = None
+_native = [None, False]  # the C++ op module once its exchange is up; tried?
+
+
+def native_ops():
+    """The C++ extension with the reference's op signatures
+    (kungfu_amd/csrc/torch_ops.cpp: all_reduce_cuda(input, output, type, op),
+    all_reduce_cuda_async(..., name) -> handle, wait_handle), its exchange
+    initialised from the process group: RCCL needs one GPU per rank, so only
+    with the nccl backend (or a single process). None where it cannot run."""
+    if _native[1]:
+        return _native[0]
+    _native[1] = True
+    if not torch.cuda.is_available():
+        return None
+    if dist.is_initialized() and dist.get_backend() != "nccl":
+        return None
+    from .. import kungfu_amd_torch_ops as m
+    from ..exchange import NativeExchange
+    uid = NativeExchange.shared_id()
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    m.init_exchange(uid, rank, _world(), torch.cuda.current_device())
+    _native[0] = m
+    return m
+
+
+def _op_maps():
+    """clib.py's maps (srcs/python/kungfu/torch/ops/clib.py:13-38): tensor
+    type string -> op, for the CUDA types the C++ op serves."""
+    m = native_ops()
+    if m is None:
+        return {}, {}
+    types = ("torch.cuda.FloatTensor", "torch.cuda.DoubleTensor", "torch.cuda.HalfTensor",
+             "torch.cuda.BFloat16Tensor", "torch.cuda.IntTensor", "torch.cuda.LongTensor")
+    return ({t: m.all_reduce_cuda for t in types},
+            {t: m.all_reduce_cuda_async for t in types})
 
 
 def _ex():
@@ -52,6 +87,11 @@ def all_reduce_fn(x, op=None):
 def inplace_all_reduce_op(x, op=None):
     """x <- all-reduce(x) in place (collective.py:16-19)."""
     op = op or "sum"
+    if x.is_cuda and x.is_contiguous():
+        m = native_ops()
+        if m is not None:
+            m.all_reduce_cuda(x, x, x.type(), op)
+            return x
     if _world() == 1:
         return x
     buf = _staged(x)
@@ -67,6 +107,12 @@ def inplace_all_reduce_async_op(x, name, op=None):
     op = op or "sum"
     h = _next[0]
     _next[0] += 1
+    if x.is_cuda and x.is_contiguous():
+        m = native_ops()
+        if m is not None:
+            nh = m.all_reduce_cuda_async(x, x, x.type(), op, name)
+            _handles[h] = _Handle([], lambda: m.wait_handle(nh))
+            return h
     if _world() == 1:
         _handles[h] = _Handle([], lambda: None)
         return h
