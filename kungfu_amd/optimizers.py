@@ -107,12 +107,16 @@ class _SyncSGD(_Bucketed):
         self._kf_launch_ready()
 
     def _kf_launch_ready(self):
+        # every bucket that is ready in index order goes out in ONE start_
+        # call: the native exchange runs a call's buckets as one grouped RCCL
+        # launch per phase and one batched HIP epilogue (kf_bucket_reduce_batch)
+        first = self._kf_next
         while self._kf_next < len(self._kf_slots) and self._kf_missing[self._kf_next] <= 0:
-            b, _ = self._kf_slots[self._kf_next]
-            self._kf_handles.append(self._kf_ex.start_(
-                [b], op=self._kf_op, average=self._kf_average, coalesce=False,
-                key="ovl%d" % self._kf_next))
             self._kf_next += 1
+        if self._kf_next > first:
+            self._kf_handles.append(self._kf_ex.start_(
+                [b for b, _ in self._kf_slots[first:self._kf_next]], op=self._kf_op,
+                average=self._kf_average, coalesce=False, key="ovl%d" % first))
 
     def _kf_finish_overlap(self):
         # parameters that got no gradient this step contribute zeros

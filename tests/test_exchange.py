@@ -358,3 +358,66 @@ def test_scheduler_orders_across_ranks(world):
     for r in range(world):
         assert orders[r][0] == names
         assert orders[r][1] == names[3:] + names[:3] == orders[r][2]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_optimizers_over_native_exchange(world):
+    """SynchronousSGDOptimizer / SynchronousAveragingOptimizer with
+    exchange=NativeExchange (loopback ranks): the exchanged gradients are the
+    rank-order average bit for bit (both algos fold in rank order here), and
+    SMA gives the oracle's blend of the rank-order sum."""
+    import torch
+    from kungfu_amd import ops
+    from kungfu_amd.optimizers import SynchronousAveragingOptimizer, SynchronousSGDOptimizer
+    dev = _gpu()
+
+    def model(seed):
+        g = torch.Generator(device=dev).manual_seed(seed)
+        m = torch.nn.Sequential(torch.nn.Linear(33, 65), torch.nn.Tanh(),
+                                torch.nn.Linear(65, 7)).to(dev)
+        with torch.no_grad():
+            for p in m.parameters():
+                p.copy_(torch.randn(p.shape, device=dev, generator=g) * 0.1)
+        return m
+
+    def loss(m, r, step):
+        g = torch.Generator(device=dev).manual_seed(100 * step + r)
+        return (m(torch.randn(16, 33, device=dev, generator=g)) ** 2).mean()
+
+    def body(rank, ex):
+        for algo in ("auto", "a2a"):
+            ex.algo = algo
+            m = model(0)
+            opt = SynchronousSGDOptimizer(torch.optim.SGD(m.parameters(), lr=0.1),
+                                          named_parameters=m.named_parameters(), exchange=ex)
+            for step in range(2):
+                snap = [p.detach().clone() for p in m.parameters()]
+                grads = []
+                for r in range(world):
+                    mr = model(0)
+                    with torch.no_grad():
+                        for a, b in zip(mr.parameters(), snap):
+                            a.copy_(b)
+                    loss(mr, r, step).backward()
+                    grads.append([p.grad.detach().clone() for p in mr.parameters()])
+                opt.zero_grad()
+                loss(m, rank, step).backward()
+                opt.step()
+                for j, p in enumerate(m.parameters()):
+                    avg = ops.bucket_reduce_avg([grads[r][j].reshape(-1) for r in range(world)],
+                                                world).view_as(p)
+                    assert torch.equal(p.grad, avg), (algo, step, j)
+        m = model(rank)
+        allp = [[p.detach().clone() for p in model(r).parameters()] for r in range(world)]
+        opt = SynchronousAveragingOptimizer(torch.optim.SGD(m.parameters(), lr=0.0), alpha=0.1,
+                                            exchange=ex)
+        loss(m, rank, 0).backward()
+        opt.step()
+        for j, p in enumerate(m.parameters()):
+            s = ops.bucket_reduce([allp[r][j].reshape(-1) for r in range(world)])
+            want = allp[rank][j].reshape(-1).clone()
+            ops.sma_blend_(want, s, world, 0.1)
+            assert torch.equal(p.detach().reshape(-1), want), j
+
+    _loop_ranks(world, body)
