@@ -157,3 +157,16 @@ def test_cross_host_device_sessions():
         pytest.skip("no GPU")
     _run([1, 1], use_gpu=True)
     _run([1, 1, 1], use_gpu=True)
+
+
+@pytest.mark.gpu
+def test_two_hosts_two_gpus_each_device():
+    """2 emulated hosts x 2 ranks, all on cuda:0: the intra-host step moves GPU
+    tensors (gloo standing in for RCCL, which refuses ranks sharing a device),
+    the HIP /np epilogue runs on the shard, the cross-host step is a
+    device-mode native session per local rank (HIP folds in HBM) — the whole
+    2-D path on the GPU; and 2 + 1 ranks through the masters."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _run([2, 2], use_gpu=True)
+    _run([2, 1], use_gpu=True)
