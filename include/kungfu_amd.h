@@ -467,8 +467,10 @@ int kf_exchange_start(kf_exchange_t *ex, const char *name, const void *send, voi
                       size_t count, KungFu_Datatype dt, KungFu_Op op, int average, int algo,
                       void *stream, kf_done_fn done, void *arg);
 /* Wait until every started all-reduce of the step has completed; the first
- * failure, else KF_OK. *order (if not NULL, n entries) receives the issue
- * order used. */
+ * failure (its message in kf_exchange_last_error on this thread), else KF_OK.
+ * *order (if not NULL, n entries) receives the issue order used. Destroy an
+ * exchange only after this returned: tasks still queued are not issued and
+ * their done callbacks never run. */
 int kf_exchange_wait_all(kf_exchange_t *ex, int32_t *order);
 /* KF_OK, or KF_ERR_RCCL after an asynchronous RCCL failure
  * (ncclCommGetAsyncError). */

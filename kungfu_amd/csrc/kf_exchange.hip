@@ -451,6 +451,7 @@ struct kf_exchange {
     size_t issued = 0, completed = 0, ntasks = 0;
     int steps      = 0;
     int sstatus    = KF_OK;
+    std::string serr;  // the first failure's message (the worker threads' own)
     bool stop      = false;
     std::deque<Done> cq;
     std::thread issuer, completer;
@@ -666,6 +667,7 @@ void kf_exchange::issue_loop()
             void *rp       = t.recv;
             rc = batch(&sp, &rp, &t.count, 1, t.dt, t.op, t.average, t.algo, t.stream);
         }
+        const std::string why = rc == KF_OK ? std::string() : t_ex_error;
         hipEvent_t ev = nullptr;
         if (rc == KF_OK && hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess) {
             if (hipEventRecord(ev, t.stream) != hipSuccess) {
@@ -677,6 +679,7 @@ void kf_exchange::issue_loop()
             rc = fail(KF_ERR_HIP, "hipEventCreate");
         }
         lk.lock();
+        if (rc != KF_OK && serr.empty()) serr = why.empty() ? t_ex_error : why;
         cq.push_back(Done{ev, t.done, t.arg, rc});
         ++issued;
         scv.notify_all();
@@ -707,7 +710,10 @@ void kf_exchange::complete_loop()
         }
         if (d.done) d.done(rc, d.arg);
         lk.lock();
-        if (rc != KF_OK && sstatus == KF_OK) sstatus = rc;
+        if (rc != KF_OK && sstatus == KF_OK) {
+            sstatus = rc;
+            if (serr.empty()) serr = "an issued all-reduce failed on the device or in RCCL";
+        }
         ++completed;
         scv.notify_all();
     }
@@ -924,6 +930,7 @@ int kf_exchange_begin_step(kf_exchange_t *ex, const char *const *names, int n, i
     ex->issued = ex->completed = 0;
     ex->ntasks  = n;
     ex->sstatus = KF_OK;
+    ex->serr.clear();
     ex->steps++;
     if (!ex->issuer.joinable()) {
         ex->issuer    = std::thread([ex] { ex->issue_loop(); });
@@ -962,6 +969,7 @@ int kf_exchange_wait_all(kf_exchange_t *ex, int32_t *order)
     std::unique_lock<std::mutex> lk(ex->smu);
     ex->scv.wait(lk, [&] { return ex->completed == ex->ntasks; });
     if (order) std::copy(ex->order.begin(), ex->order.end(), order);
+    if (ex->sstatus != KF_OK) t_ex_error = ex->serr;  // the message, on the caller's thread
     return ex->sstatus;
 }
 
