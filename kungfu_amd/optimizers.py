@@ -20,7 +20,6 @@ flat padded device buckets (``collective.GradBuckets``); ``p.grad`` (S-SGD) or
 defuse copies. If a training loop replaces ``p.grad`` (``zero_grad`` with
 ``set_to_none=True``), the new gradient is copied into the bucket view once.
 """
-import torch
 
 from .collective import Exchange, GradBuckets
 

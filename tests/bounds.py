@@ -4,7 +4,6 @@
 order) differ by at most twice that. An SGD / SMA update on top adds the
 roundings of its own few operations (u per operation and operand magnitude).
 Nothing here is an ad-hoc atol."""
-import torch
 
 U32 = 2.0 ** -24
 

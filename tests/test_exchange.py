@@ -81,10 +81,6 @@ def _gpu():
     return torch.device("cuda:0")
 
 
-DTS = {"f32": "float32", "bf16": "bfloat16", "f16": "float16", "i32": "int32", "i8": "int8",
-       "f64": "float64", "u8": "uint8"}
-
-
 def _rand(name, n, seed):
     rng = np.random.default_rng(seed)
     if name in ("f32", "f64", "f16"):
