@@ -341,9 +341,11 @@ class AutoExchange:
     """Exchange that picks, per bucket list, the fastest of candidates that
     give the SAME bits, by timing them on the real buckets the first time it
     sees them — the way RCCL itself tunes its algorithm per size, lifted one
-    level. The candidates are RCCL's all-to-all + HIP rank-order fold
-    (collective.Exchange(algo="a2a")) and the xGMI P2P exchange (PeerExchange),
-    which both fold the ranks in order 0..n-1 with the same kernel; RCCL's
+    level. The candidates are RCCL's all-to-all + HIP rank-order fold, through
+    torch.distributed (collective.Exchange(algo="a2a")) and through the native
+    C-ABI exchange (exchange.NativeExchange(algo="a2a"), nccl backend only),
+    and the xGMI P2P exchange (PeerExchange), which all fold the ranks in order
+    0..n-1 with the same kernel; RCCL's
     reduce-scatter joins them only where its own order cannot change a bit
     (integer dtypes; two ranks summing f32/f64). So the result never depends
     on which transport won on a given box.
@@ -368,6 +370,7 @@ class AutoExchange:
         self.mode = mode
         self._p2p = None
         self._host_ok = None
+        self._native, self._native_tried = None, False
         self.picked = {}
         self._choice = {}
 
@@ -381,6 +384,32 @@ class AutoExchange:
         if self._p2p is None:
             self._p2p = PeerExchange(self.group, mode=self.mode)
         return self._p2p
+
+    def _native_candidate(self, buckets):
+        """The native C-ABI exchange with the all-to-all + rank-order fold
+        (kungfu_amd.exchange.NativeExchange(algo="a2a")): the same bits as the
+        other candidates, one call per step. Needs RCCL with one GPU per rank
+        (the nccl backend); created once, dropped on every rank if any fails."""
+        if (self.world == 1 or not all(b.is_cuda for b in buckets)
+                or dist.get_backend(self.group) != "nccl"):
+            return None
+        if not self._native_tried:
+            self._native_tried = True
+            nx, ok = None, True
+            try:
+                from .exchange import NativeExchange
+                nx = NativeExchange(self.group, algo="a2a")
+            except Exception as e:
+                import sys
+                print("kungfu_amd AutoExchange: native exchange unavailable on rank %d: %r"
+                      % (self.rank, e), file=sys.stderr)
+                ok = False
+            if not self._agree_all(ok):
+                if nx is not None:
+                    nx.close()
+                nx = None
+            self._native = nx
+        return self._native
 
     def _agree_all(self, flag):
         flags = [None] * self.world
@@ -404,6 +433,9 @@ class AutoExchange:
         cands = [("rccl", self.rccl)]
         if self._rs_exact(buckets, op):
             cands.append(("rccl_rs", self.rccl_rs))
+        native = self._native_candidate(buckets)
+        if native is not None:
+            cands.append(("native", native))
         p2p = self._p2p_candidate(buckets)
         if p2p is not None:
             cands.append(("p2p", p2p))
@@ -469,3 +501,5 @@ class AutoExchange:
     def close(self):
         if self._p2p is not None:
             self._p2p.close()
+        if self._native is not None:
+            self._native.close()
