@@ -27,7 +27,8 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 
 BYTES = 256 << 20
 LAUNCHES = 6
-OURS = ("void kf::reduce_kernel", "void kf::reduce_spread_kernel", "void kf::sma_kernel")
+OURS = ("void kf::reduce_kernel", "void kf::reduce_spread_kernel", "void kf::sma_kernel",
+        "void kf::reduce_batch_kernel")
 
 # (name, inputs read, outputs written) in units of BYTES
 VARIANTS = [
@@ -41,6 +42,8 @@ VARIANTS = [
     ("reduce SUM k=2 bf16", 2, 1),
     ("reduce SUM k=2 i8 (packed 32-bit lanes)", 2, 1),
     ("reduce MAX k=8 i8 (packed 32-bit lanes)", 8, 1),
+    ("batch: 16 buckets x 16 MiB, SUM k=2 f32 (one launch)", 2, 1),
+    ("batch: 16 shards x 16 MiB, /np in place f32 (one launch)", 1, 1),
 ]
 
 
@@ -82,6 +85,17 @@ def run():
         plan.append((lambda ins, out, k=k, op=op: lib.kf_bucket_reduce(
             _lib.ptr_array([t.data_ptr() for t in ins]), k, out.data_ptr(), out.numel(),
             0x10108, op, s), bufs(k, torch.int8)))
+    import ctypes
+    nb, m = 16, n // 16
+    cnts = (ctypes.c_size_t * nb)(*([m] * nb))
+    for k, np_ in ((2, 0), (1, 8)):
+        def batch(ins, out, k=k, np_=np_):
+            src = [ins[j][b * m:(b + 1) * m] for b in range(nb) for j in range(k)]
+            dst = [(out if k > 1 else ins[0])[b * m:(b + 1) * m] for b in range(nb)]
+            return lib.kf_bucket_reduce_batch(_lib.ptr_array([t.data_ptr() for t in src]), k,
+                                              _lib.ptr_array([t.data_ptr() for t in dst]), cnts,
+                                              nb, 0x20408, 0, np_, s)
+        plan.append((batch, bufs(k)))
     assert len(plan) == len(VARIANTS)
     torch.cuda.synchronize()
     for fn, sets in plan:
