@@ -417,3 +417,78 @@ def test_optimizers_over_native_exchange(world):
             assert torch.equal(p.detach().reshape(-1), want), j
 
     _loop_ranks(world, body)
+
+
+@pytest.mark.gpu
+def test_native_exchange_configs_full_size():
+    """The bench's N > 1 code path at BASELINE's sizes, over the loopback
+    transport: C3 (64 x 4 MiB fp32 as 64 grouped buckets, S-SGD, world 2, the
+    primary's reduce-scatter algo), C4 (ResNet-50 in 16 buckets, world 4) and C5
+    (BERT-base bf16 SMA, world 2, all-to-all fold). The loopback's
+    reduce-scatter folds in rank order, so all three are bit-exact against the
+    oracle."""
+    import json
+    import torch
+    from kungfu_amd.collective import GradBuckets
+    from oracle import oracle
+    dev = _gpu()
+    models = json.load(open(os.path.join(HERE, "golden", "models.json")))
+
+    def fill(gb, seed, dtype):
+        g = torch.Generator(device=dev).manual_seed(seed)
+        for v in gb.views:
+            v.copy_(torch.randn(v.numel(), device=dev, generator=g).to(dtype))
+
+    # C3, world 2
+    n = 64 << 20
+
+    def c3(rank, ex):
+        ex.algo = "rs"
+        gb = GradBuckets([n], torch.float32, dev, 2, n_buckets=64)
+        fill(gb, 40 + rank, torch.float32)
+        ex.all_reduce_(gb.buckets, average=True, coalesce=False)
+        torch.cuda.synchronize()
+        xs = []
+        for r in range(2):
+            g2 = GradBuckets([n], torch.float32, dev, 2, n_buckets=64)
+            fill(g2, 40 + r, torch.float32)
+            xs.append(g2.views[0].cpu().numpy())
+        assert np.array_equal(gb.views[0].cpu().numpy(), oracle.reduce_avg(xs, "f32", 2))
+
+    _loop_ranks(2, c3)
+    # C4, world 4
+    sizes = models["resnet50-imagenet"]
+
+    def c4(rank, ex):
+        ex.algo = "auto"
+        gbs = [GradBuckets(sizes, torch.float32, dev, 4, n_buckets=16) for _ in range(4)]
+        for r, gb in enumerate(gbs):
+            fill(gb, 500 + r, torch.float32)
+        want = [oracle.reduce_avg([gb.buckets[j].cpu().numpy() for gb in gbs], "f32", 4)
+                for j in range(16)]
+        mine = gbs[rank]
+        ex.all_reduce_(mine.buckets, average=True, coalesce=False)
+        torch.cuda.synchronize()
+        for j, (b, sp) in enumerate(zip(mine.buckets, mine.spans)):
+            assert np.array_equal(b[:sp].cpu().numpy(), want[j][:sp]), j
+
+    _loop_ranks(4, c4)
+    # C5, world 2
+    bert = models["bert"][:201]
+
+    def c5(rank, ex):
+        ex.algo = "auto"
+        gbs = [GradBuckets(bert, torch.bfloat16, dev, 2, bucket_bytes=16 << 20) for _ in range(2)]
+        for r, gb in enumerate(gbs):
+            fill(gb, 700 + r, torch.bfloat16)
+        mine = gbs[rank]
+        before = [_to_np(b, "bf16") for b in mine.buckets]
+        sums = [oracle.reduce_k([_to_np(gb.buckets[j], "bf16") for gb in gbs], "bf16", "sum")
+                for j in range(len(mine.buckets))]
+        ex.sma_(mine.buckets, 0.1)
+        torch.cuda.synchronize()
+        for j, b in enumerate(mine.buckets):
+            assert np.array_equal(_to_np(b, "bf16"),
+                                  oracle.sma_blend(before[j], sums[j], "bf16", 2, 0.1)), j
+
+    _loop_ranks(2, c5)
