@@ -105,15 +105,36 @@ struct Plan {
 // launch-mode bits passed down the dispatch chain
 enum { LM_NONE = 0, LM_SPREAD = 1 };  // LM_SPREAD: inputs behind different links
 
-// Vector body needs every pointer at the same 16-B residue; the head peels
-// elements until they are aligned.
+// The head peels elements until the OUTPUT is 16-B aligned; the vector body
+// then stores whole aligned 16-B vectors. Inputs need only element alignment:
+// one whose 16-B residue differs from the output's is read with the same
+// global_load_dwordx4 at an unaligned address (gfx950 runs HSA queues in
+// unaligned-access mode; the wave's 1 KiB stays contiguous, so the extra
+// cache line per wave-instruction costs little): 256 MiB with one input off
+// the output's residue runs at 0.80-0.82 of the roofline (f32, bf16, u8), with
+// all three pointers at different residues 0.72-0.79, against 0.29-0.68 for
+// the element-wise kernel this replaces (tools/unaligned_rate.py;
+// profiles/r02/unaligned_rate_{vector,elementwise}.jsonl).
+// KUNGFU_AMD_NO_UNALIGNED_VECTOR=1 keeps such inputs on the element-wise
+// kernel (A/B only).
+bool unaligned_vector_ok()
+{
+    static const bool ok = [] {
+        const char *e = std::getenv("KUNGFU_AMD_NO_UNALIGNED_VECTOR");
+        return !(e && std::atoi(e) != 0);
+    }();
+    return ok;
+}
+
 Plan make_plan(const void *const *in, int k, const void *out, size_t n, int sz)
 {
     Plan p;
     const uintptr_t r = reinterpret_cast<uintptr_t>(out) & 15u;
     if (r % sz != 0) return p;
+    const bool ua = unaligned_vector_ok();
     for (int j = 0; j < k; ++j) {
-        if ((reinterpret_cast<uintptr_t>(in[j]) & 15u) != r) return p;
+        const uintptr_t rj = reinterpret_cast<uintptr_t>(in[j]) & 15u;
+        if (ua ? (rj % sz != 0) : (rj != r)) return p;
     }
     size_t head = r == 0 ? 0 : (16 - r) / sz;
     if (head > n) head = n;
