@@ -2,7 +2,8 @@
 // kungfu::Peer / NCCL-controller binding takes): id from
 // kf_exchange_unique_id, communicator, a batch of buckets all-reduced with the
 // S-SGD epilogue, the ordered scheduler with done callbacks, the SMA batch.
-// One rank (world 1): every all-reduce is the identity, the order is checked.
+// One rank (world 1): every all-reduce is the identity, the order is checked;
+// then three ranks as threads over the loopback transport.
 // Exit 0 = pass, 77 = no device (build checked only).
 //   g++ -std=c++17 -D__HIP_PLATFORM_AMD__ -I include -I /opt/rocm/include
 //       tests/c/test_exchange.cpp -L kungfu_amd -lkungfu_amd -L /opt/rocm/lib
@@ -14,6 +15,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "kungfu_amd.h"
@@ -38,6 +40,69 @@ void on_done(int status, void *arg)
     g_done.push_back(status == KF_OK ? static_cast<int>(reinterpret_cast<intptr_t>(arg)) : -1);
 }
 }  // namespace
+
+// `world` ranks as threads over the loopback transport, each with its own
+// exchange, stream and buckets: S-SGD average of two buckets (one with a tail
+// of count % world) must be the rank-order fold / world on every rank.
+int multi_rank_loopback(int world)
+{
+    kf_loopback_t *g = kf_loopback_create(world);
+    CHECK(g != nullptr);
+    const std::vector<size_t> counts = {3 * 1024 + 1, 100003};
+    std::vector<int> rc(world, 0);
+    std::vector<std::thread> ts;
+    for (int r = 0; r < world; ++r) {
+        ts.emplace_back([&, r] {
+            rc[r] = [&]() -> int {
+                CHECK(hipSetDevice(0) == hipSuccess);
+                kf_exchange_t *ex = kf_exchange_create_loopback(g, r, 0);
+                CHECK(ex != nullptr);
+                hipStream_t s;
+                CHECK(hipStreamCreate(&s) == hipSuccess);
+                std::vector<void *> bufs(2);
+                for (int b = 0; b < 2; ++b) {
+                    std::vector<float> h(counts[b]);
+                    for (size_t i = 0; i < counts[b]; ++i) h[i] = 0.5f * (r + 1) + (i % 97);
+                    CHECK(hipMalloc(&bufs[b], counts[b] * 4) == hipSuccess);
+                    CHECK(hipMemcpy(bufs[b], h.data(), counts[b] * 4, hipMemcpyHostToDevice) ==
+                          hipSuccess);
+                }
+                for (int algo : {KF_ALGO_REDUCE_SCATTER, KF_ALGO_ALL_TO_ALL}) {
+                    if (algo == KF_ALGO_ALL_TO_ALL) {  // reset to the inputs
+                        for (int b = 0; b < 2; ++b) {
+                            std::vector<float> h(counts[b]);
+                            for (size_t i = 0; i < counts[b]; ++i) h[i] = 0.5f * (r + 1) + (i % 97);
+                            CHECK(hipMemcpy(bufs[b], h.data(), counts[b] * 4,
+                                            hipMemcpyHostToDevice) == hipSuccess);
+                        }
+                    }
+                    CHECK(kf_exchange_all_reduce_batch(
+                              ex, const_cast<const void *const *>(bufs.data()), bufs.data(),
+                              counts.data(), 2, KungFu_FLOAT, KungFu_SUM, 1, algo, s) == KF_OK);
+                    CHECK(hipStreamSynchronize(s) == hipSuccess);
+                    for (int b = 0; b < 2; ++b) {
+                        std::vector<float> got(counts[b]);
+                        CHECK(hipMemcpy(got.data(), bufs[b], counts[b] * 4,
+                                        hipMemcpyDeviceToHost) == hipSuccess);
+                        for (size_t i = 0; i < counts[b]; ++i) {
+                            float acc = 0.5f * 1 + (i % 97);
+                            for (int q = 1; q < world; ++q) acc += 0.5f * (q + 1) + (i % 97);
+                            CHECK(got[i] == acc / world);
+                        }
+                    }
+                }
+                for (void *p : bufs) CHECK(hipFree(p) == hipSuccess);
+                CHECK(hipStreamDestroy(s) == hipSuccess);
+                kf_exchange_destroy(ex);
+                return 0;
+            }();
+        });
+    }
+    for (auto &t : ts) t.join();
+    kf_loopback_destroy(g);
+    for (int r = 0; r < world; ++r) CHECK(rc[r] == 0);
+    return 0;
+}
 
 int main()
 {
@@ -116,6 +181,7 @@ int main()
     }
     kf_exchange_destroy(ex);
     CHECK(hipStreamDestroy(s) == hipSuccess);
+    CHECK(multi_rank_loopback(3) == 0);
     std::printf("exchange ok\n");
     return 0;
 }
