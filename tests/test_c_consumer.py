@@ -58,3 +58,45 @@ def test_cpp_exchange_host_on_gpu(exchange_binary):
     r = subprocess.run([exchange_binary], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "exchange ok" in r.stdout
+
+
+@pytest.fixture(scope="module")
+def peer_binary(tmp_path_factory):
+    """tests/c/test_peer.cpp: the reference's own C++ collective tests over
+    include/kungfu_amd.hpp (the Peer facade on the C ABI)."""
+    out = str(tmp_path_factory.mktemp("cp") / "test_peer")
+    lib = os.path.join(ROOT, "kungfu_amd")
+    subprocess.run(["g++", "-std=c++17", "-Wall", "-Wextra", "-Werror", "-D__HIP_PLATFORM_AMD__",
+                    "-I", os.path.join(ROOT, "include"), "-I", "/opt/rocm/include",
+                    os.path.join(ROOT, "tests", "c", "test_peer.cpp"),
+                    "-L", lib, "-lkungfu_amd", "-Wl,-rpath," + lib,
+                    "-L", "/opt/rocm/lib", "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib",
+                    "-lpthread", "-o", out], check=True)
+    return out
+
+
+def test_cpp_peer_one_peer(peer_binary):
+    # test_operations.cpp:3-26 with a single peer: no reduce, no GPU needed
+    r = subprocess.run([peer_binary], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "peer ok" in r.stdout
+
+
+def _peers(binary, np_, mode):
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        ps = [subprocess.Popen([binary, str(r), str(np_), d] + ([mode] if mode else []),
+                               stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+              for r in range(np_)]
+        outs = [p.communicate(timeout=120) for p in ps]
+    for p, (o, e) in zip(ps, outs):
+        assert p.returncode == 0, o + e
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("np_", [2, 3, 4])
+@pytest.mark.parametrize("mode", ["", "dev"])
+def test_cpp_peer_fake_agent(peer_binary, np_, mode):
+    # fake_agent.cpp:15-44: iota summed over np peers == i * np, host buffers
+    # (the drop-in's HIP fold) and HBM buffers (the device session)
+    _peers(peer_binary, np_, mode)
