@@ -339,6 +339,10 @@ int kf_session_all_reduce_async(kf_session_t *s, const void *send, void *recv,
                                 void *arg);
 /* Block until every queued all-reduce has finished; the first failure since
  * the previous wait (its message in kf_session_last_error), else KF_OK. */
+/* Barrier (GoKungfuBarrier, libkungfu-comm/collective.go:17-20; session.go:
+ * 104-115): an all-reduce of size() zero bytes every peer joins. Blocking;
+ * device-mode sessions use a workspace of their own in HBM. */
+int kf_session_barrier(kf_session_t *s);
 int kf_session_wait_all(kf_session_t *s);
 void kf_session_destroy(kf_session_t *s);
 const char *kf_session_last_error(void);

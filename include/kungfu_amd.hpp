@@ -139,12 +139,8 @@ class Peer
         return 0;
     }
 
-    // Barrier (peer.hpp:78): an all-reduce of one int32 every peer joins
-    int Barrier()
-    {
-        int32_t x = 0, y = 0;
-        return AllReduce(&x, &y, 1, KungFu_INT32, KungFu_SUM, "kungfu::Barrier");
-    }
+    // Barrier (peer.hpp:78, GoKungfuBarrier)
+    int Barrier() { return kf_session_barrier(s_) == KF_OK ? 0 : 1; }
 
     // device mode: the HIP stream the folds are queued on (hipStream_t)
     void SetStream(void *stream) { stream_ = stream; }

@@ -51,6 +51,7 @@ EXPORTED = (
     "kf_session_reduce",
     "kf_session_broadcast",
     "kf_session_wait_all",
+    "kf_session_barrier",
     "kf_session_destroy",
     "kf_session_last_error",
     "kf_ipc_export",
@@ -223,6 +224,8 @@ def load():
     lib.kf_session_broadcast.restype = c_int
     lib.kf_session_wait_all.argtypes = [c_void_p]
     lib.kf_session_wait_all.restype = c_int
+    lib.kf_session_barrier.argtypes = [c_void_p]
+    lib.kf_session_barrier.restype = c_int
     lib.kf_session_last_error.argtypes = []
     lib.kf_session_last_error.restype = ctypes.c_char_p
     lib.kf_ipc_export.argtypes = [c_void_p, c_void_p, ctypes.POINTER(c_size_t)]

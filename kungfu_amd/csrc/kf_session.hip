@@ -407,6 +407,7 @@ struct kf_session {
     int batch_fold = 1;         // device mode: k-input fold at multi-predecessor nodes
     char *stage       = nullptr;  // HBM staging: [predecessor arrival][bucket bytes]
     size_t stage_bytes = 0;
+    char *barrier_dev  = nullptr;  // device mode: the barrier's zeroed u8 workspace
     std::deque<Stashed> stash;  // per-name mailbox for early messages
 
     // sender thread
@@ -510,6 +511,7 @@ struct kf_session {
         for (auto e : ev_pool) (void)hipEventDestroy(e);
         if (tx_stream) (void)hipStreamDestroy(tx_stream);
         if (stage) (void)hipFree(stage);
+        if (barrier_dev) (void)hipFree(barrier_dev);
     }
 
     void sender_loop()
@@ -1327,6 +1329,39 @@ int kf_session_all_reduce_async(kf_session_t *s, const void *send, void *recv, s
     AsyncOp a{static_cast<const char *>(send), static_cast<char *>(recv), count, dt, op, name,
               stream, done, arg};
     return s->submit(a);
+}
+
+int kf_session_barrier(kf_session_t *s)
+{
+    // session.go:104-115: an all-reduce (SUM) of size() zero bytes named
+    // "kungfu::barrier" over the global strategies. A device-mode session
+    // moves HBM buffers only, so it keeps a zeroed workspace there.
+    if (!s) return KF_ERR_ARG;
+    t_sess_error.clear();
+    if (s->aworker.joinable() && std::this_thread::get_id() == s->aworker.get_id()) {
+        return fail(KF_ERR_ARG, "barrier from a done callback");
+    }
+    const int rc = s->wait_all();
+    if (rc != KF_OK) return rc;
+    const size_t k = static_cast<size_t>(s->size);
+    if (!s->device_mode) {
+        std::vector<char> send(k, 0), recv(k, 0);
+        return s->all_reduce(send.data(), recv.data(), k, KungFu_UINT8, KungFu_SUM,
+                             "kungfu::barrier", nullptr);
+    }
+    if (!s->barrier_dev) {
+        if (hipMalloc(&s->barrier_dev, 2 * k) != hipSuccess) {
+            s->barrier_dev = nullptr;
+            return fail(KF_ERR_HIP, "hipMalloc barrier workspace");
+        }
+    }
+    // zeroed before every barrier: the sum lands in the second half, the first
+    // half is never written, but a failed barrier may leave the second dirty
+    if (hipMemset(s->barrier_dev, 0, 2 * k) != hipSuccess) {
+        return fail(KF_ERR_HIP, "hipMemset barrier workspace");
+    }
+    return s->all_reduce(s->barrier_dev, s->barrier_dev + k, k, KungFu_UINT8, KungFu_SUM,
+                         "kungfu::barrier", nullptr);
 }
 
 int kf_session_wait_all(kf_session_t *s)

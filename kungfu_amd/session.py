@@ -192,6 +192,11 @@ class Session:
             self._pending = [p for p in self._pending if not p.done()] + [h]
         return h
 
+    def barrier(self):
+        """Session.Barrier (session.go:98-115): returns once every peer has
+        entered it."""
+        _lib.check(self.lib.kf_session_barrier(self._h), "kf_session_barrier")
+
     def wait_all(self):
         """Block until every queued all-reduce has finished."""
         rc = self.lib.kf_session_wait_all(self._h)

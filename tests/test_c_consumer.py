@@ -88,7 +88,13 @@ def _peers(binary, np_, mode):
         ps = [subprocess.Popen([binary, str(r), str(np_), d] + ([mode] if mode else []),
                                stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
               for r in range(np_)]
-        outs = [p.communicate(timeout=120) for p in ps]
+        try:
+            outs = [p.communicate(timeout=90) for p in ps]
+        except subprocess.TimeoutExpired:
+            for p in ps:
+                p.kill()
+            outs = [p.communicate() for p in ps]
+            raise AssertionError("peers hung: %r" % (outs,))
     for p, (o, e) in zip(ps, outs):
         assert p.returncode == 0, o + e
 

@@ -546,6 +546,7 @@ def _subset_body(rank, size, sock_dir, mode, errq):
                 raise AssertionError("bad forest accepted: %r" % bad)
             except KungFuAMDError as e:
                 assert "KF_ERR_ARG" in str(e)
+        s.barrier()
         for j, forest in enumerate(forests):
             want = schedule.subset_all_reduce(xs, "f32", "sum", forest, name="sub%d" % j)[rank]
             y = (torch.zeros_like(x) if mode == "device" else np.zeros_like(x))
@@ -583,3 +584,57 @@ def test_session_subset_all_reduce_device():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     _run_subset("device")
+
+
+def _barrier_body(rank, size, sock_dir, mode, q):
+    """Session.Barrier (session.go:98-115): no peer leaves before the last one
+    has entered; peers enter 0.3 s apart."""
+    sys.path[:0] = [ROOT, HERE]
+    try:
+        import time
+        from kungfu_amd.session import Session
+        s = Session(rank, size, sock_dir, mode=mode,
+                    **({} if mode == "device" else {"host_reduce_fn": oracle_reduce_fn()}))
+        s.barrier()  # everyone connected
+        for i in range(2):
+            time.sleep(0.3 * ((rank + i) % size))
+            t_in = time.time()
+            s.barrier()
+            q.put((i, rank, t_in, time.time()))
+        s.close()
+    except Exception:
+        q.put(("err", rank, traceback.format_exc(), 0))
+
+
+def _run_barrier(mode, size):
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    with tempfile.TemporaryDirectory() as d:
+        ps = [ctx.Process(target=_barrier_body, args=(r, size, d, mode, q)) for r in range(size)]
+        for p in ps:
+            p.start()
+        for p in ps:
+            p.join(timeout=120)
+    rows = []
+    while not q.empty():
+        rows.append(q.get())
+    errs = [r[2] for r in rows if r[0] == "err"]
+    assert not errs, "\n".join(errs)
+    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+    for i in range(2):
+        mine = [r for r in rows if r[0] == i]
+        assert len(mine) == size
+        assert min(r[3] for r in mine) >= max(r[2] for r in mine)
+
+
+@pytest.mark.parametrize("size", [2, 3])
+def test_session_barrier_host(size):
+    _run_barrier("host", size)
+
+
+@pytest.mark.gpu
+def test_session_barrier_device():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _run_barrier("device", 3)
