@@ -64,6 +64,17 @@ from . import _lib
 from .ops import kungfu_dtype
 
 
+def _device_identity(dev):
+    """(host, PCI domain/bus/device) of a GPU, or None when torch does not
+    report the PCI location (every peer is then treated as remote)."""
+    import socket
+    p = torch.cuda.get_device_properties(dev)
+    pci = tuple(getattr(p, a, None) for a in ("pci_domain_id", "pci_bus_id", "pci_device_id"))
+    if any(x is None for x in pci):
+        return None
+    return (socket.gethostname(), pci)
+
+
 class P2PExchange:
     def __init__(self, buckets, group=None, mode="pull", barrier="device", timeout_s=60.0,
                  coalesce=True):
@@ -95,6 +106,16 @@ class P2PExchange:
         self.inboxes = ([torch.empty_like(b) for b in self.buckets]
                         if mode == "push" else [])
         self._bases = {}  # (rank, handle) -> mapped base (one mapping per allocation)
+        # Peers whose buckets live on THIS device (ranks sharing one GPU) are
+        # read from local HBM: the pull fold then takes the register-shape
+        # kernel (kf_bucket_reduce, 0.76 of the roofline at k = 8) rather than
+        # the all-loads-in-flight link spreader (kf_bucket_reduce_peers, 0.72
+        # locally), which exists for inputs behind different xGMI links. Both
+        # are the same rank-order left fold, bit for bit.
+        ids = [None] * self.world
+        dist.all_gather_object(ids, _device_identity(self.buckets[0].device)
+                               if self.buckets else None, group=self.group)
+        self.all_local = ids[0] is not None and all(i == ids[0] for i in ids)
         self.ptrs = self._share([b.data_ptr() for b in self.buckets])  # ptrs[j][r]: bucket j of rank r
         self.inbox_ptrs = self._share([b.data_ptr() for b in self.inboxes])  # same for inboxes
         self.epoch = 0
@@ -194,10 +215,16 @@ class P2PExchange:
             off = rank * shard * isz
             ins = _lib.ptr_array([p + off for p in row])
             out = b.data_ptr() + off
-            # every peer's load in flight at once (all links busy), adds in
-            # rank order
-            rc = self.lib.kf_bucket_reduce_peers(ins, world, out, shard, int(kungfu_dtype(b)),
-                                                 int(OP_NAMES[op]), world if average else 0, s)
+            dt = int(kungfu_dtype(b))
+            if self.all_local:
+                rc = (self.lib.kf_bucket_reduce_avg(ins, world, out, shard, dt, world, s)
+                      if average else
+                      self.lib.kf_bucket_reduce(ins, world, out, shard, dt, int(OP_NAMES[op]), s))
+            else:
+                # every peer's load in flight at once (all links busy), adds
+                # in rank order
+                rc = self.lib.kf_bucket_reduce_peers(ins, world, out, shard, dt,
+                                                     int(OP_NAMES[op]), world if average else 0, s)
             _lib.check(rc, "p2p shard reduce")
         self._barrier()
         for b, row in zip(self.buckets, self.ptrs):

@@ -31,6 +31,7 @@ def _body(rank, world, port, errq, mode, barrier="device"):
         gb = GradBuckets(sizes, torch.float32, dev, world, n_buckets=4)
         ex = P2PExchange(gb.buckets, mode=mode, barrier=barrier)
         assert len(ex.buckets) == 1  # the 4 contiguous buckets run as one
+        assert ex.all_local  # every rank on cuda:0: the register-shape fold
         for step in range(3):  # fresh data every step: no stale shard survives
             xs = [[np.random.default_rng(1000 * r + 100 * step + i).standard_normal(n)
                    .astype(np.float32) for i, n in enumerate(sizes)] for r in range(world)]
@@ -43,6 +44,7 @@ def _body(rank, world, port, errq, mode, barrier="device"):
         # int32 MAX, a second exchange on other buckets, twice (buffer reuse)
         gi = GradBuckets([4099], torch.int32, dev, world, n_buckets=3)
         ex2 = P2PExchange(gi.buckets, mode=mode, barrier=barrier, coalesce=False)
+        ex2.all_local = False  # the link spreader (kf_bucket_reduce_peers), same bits
         for step in range(2):
             gi.views[0].copy_(torch.arange(4099, dtype=torch.int32, device=dev) * (rank + 1 + step))
             ex2.all_reduce_(op="max")
