@@ -29,7 +29,13 @@
 namespace kf
 {
 enum Op { OP_SUM = 0, OP_MIN = 1, OP_MAX = 2, OP_PROD = 3 };
-enum Epi { EPI_NONE = 0, EPI_DIV = 1 };
+// EPI_DIV is what the host asks for (the /np epilogue). Inside a kernel it is
+// split once, at the top, on the uniform np.pow2: EPI_MUL (x * 2^-k, the same
+// correctly rounded value as x / 2^k) or EPI_DIV (a true IEEE division). With
+// the choice made per element instead, the fp32 k = 2 kernel carried 66 scalar
+// branches and 58 division sequences (663 instructions against 172 without
+// the epilogue) and ran at 0.77 of the roofline against 0.82.
+enum Epi { EPI_NONE = 0, EPI_DIV = 1, EPI_MUL = 2 };
 
 // The 1/np epilogue divisor. For np a power of two, x * 2^-k and x / 2^k are
 // the same correctly rounded value, so the multiply is used (bit-identical,
@@ -131,9 +137,9 @@ template <> struct Elt<float> {
             return (a < b) ? b : a;
         }
     }
-    __device__ static S div(Acc a, const Div &dv)
+    template <bool P2> __device__ static S div(Acc a, const Div &dv)
     {
-        return dv.pow2 ? __fmul_rn(a, dv.fi) : __fdiv_rn(a, dv.f);
+        return P2 ? __fmul_rn(a, dv.fi) : __fdiv_rn(a, dv.f);
     }
 };
 
@@ -154,9 +160,9 @@ template <> struct Elt<double> {
             return (a < b) ? b : a;
         }
     }
-    __device__ static S div(Acc a, const Div &dv)
+    template <bool P2> __device__ static S div(Acc a, const Div &dv)
     {
-        return dv.pow2 ? __dmul_rn(a, dv.di) : __ddiv_rn(a, dv.d);
+        return P2 ? __dmul_rn(a, dv.di) : __ddiv_rn(a, dv.d);
     }
 };
 
@@ -173,10 +179,10 @@ template <> struct Elt<f16_t> {
         static_assert(OP == OP_SUM, "fp16 supports SUM only");
         return f32_to_f16(__fadd_rn(f16_to_f32(a), f16_to_f32(b)));
     }
-    __device__ static S div(Acc a, const Div &dv)
+    template <bool P2> __device__ static S div(Acc a, const Div &dv)
     {
         const float x = f16_to_f32(a);
-        return f32_to_f16(dv.pow2 ? __fmul_rn(x, dv.fi) : __fdiv_rn(x, dv.f));
+        return f32_to_f16(P2 ? __fmul_rn(x, dv.fi) : __fdiv_rn(x, dv.f));
     }
 };
 
@@ -211,9 +217,9 @@ template <> struct Elt<bf16_t> {
             return a.bits;
         }
     }
-    __device__ static S div(Acc a, const Div &dv)
+    template <bool P2> __device__ static S div(Acc a, const Div &dv)
     {
-        return f32_to_bf16(dv.pow2 ? __fmul_rn(a.f, dv.fi) : __fdiv_rn(a.f, dv.f));
+        return f32_to_bf16(P2 ? __fmul_rn(a.f, dv.fi) : __fdiv_rn(a.f, dv.f));
     }
 };
 
@@ -244,8 +250,8 @@ template <typename T, typename = void> struct Lane {
     }
     template <int OP, int EPI> __device__ static W emit(const Acc &a, const Div &np)
     {
-        if constexpr (EPI == EPI_DIV) {
-            return Elt<T>::div(a, np);
+        if constexpr (EPI == EPI_DIV || EPI == EPI_MUL) {
+            return Elt<T>::template div<EPI == EPI_MUL>(a, np);
         } else {
             return finish<T, OP>(a);
         }
@@ -342,8 +348,8 @@ fold_scalar(const InPtrs &in, int k, size_t i, const Div &np)
         acc = Elt<T>::template combine<OP>(
             acc, reinterpret_cast<const S *>(in.p[j])[i]);
     }
-    if constexpr (EPI == EPI_DIV) {
-        return Elt<T>::div(acc, np);
+    if constexpr (EPI == EPI_DIV || EPI == EPI_MUL) {
+        return Elt<T>::template div<EPI == EPI_MUL>(acc, np);
     } else {
         return finish<T, OP>(acc);
     }
@@ -488,6 +494,13 @@ __global__ void __launch_bounds__(BLOCK)
     reduce_kernel(InPtrs in, int k, void *out, size_t n, size_t head,
                   size_t nvec, Div np)
 {
+    if constexpr (EPI == EPI_DIV) {
+        if (np.pow2) {
+            reduce_body<T, OP, EPI_MUL, KC, BLOCK, UNROLL, LOADNT, STPLAIN>(
+                in, k, out, n, head, nvec, np, blockIdx.x, gridDim.x);
+            return;
+        }
+    }
     reduce_body<T, OP, EPI, KC, BLOCK, UNROLL, LOADNT, STPLAIN>(in, k, out, n, head, nvec, np,
                                                                blockIdx.x, gridDim.x);
 }
@@ -519,6 +532,13 @@ __global__ void __launch_bounds__(BLOCK) reduce_batch_kernel(BatchArgs a, int k,
     int s            = 0;
     while (s + 1 < a.nseg && b >= a.blk0[s + 1]) ++s;
     const size_t nblk = a.blk0[s + 1] - a.blk0[s];
+    if constexpr (EPI == EPI_DIV) {
+        if (np.pow2) {
+            reduce_body<T, OP, EPI_MUL, KC, BLOCK, UNROLL, 1, 0>(
+                a.in[s], k, a.out[s], a.n[s], a.head[s], a.nvec[s], np, b - a.blk0[s], nblk);
+            return;
+        }
+    }
     reduce_body<T, OP, EPI, KC, BLOCK, UNROLL, 1, 0>(a.in[s], k, a.out[s], a.n[s], a.head[s],
                                                     a.nvec[s], np, b - a.blk0[s], nblk);
 }
@@ -533,9 +553,8 @@ __global__ void __launch_bounds__(BLOCK) reduce_batch_kernel(BatchArgs a, int k,
 // the result is the same left fold bit for bit. One 16-B vector per input per
 // thread per tile; k > 8 goes in groups of 8.
 template <typename T, int OP, int EPI, int BLOCK>
-__global__ void __launch_bounds__(BLOCK)
-    reduce_spread_kernel(InPtrs in, int k, void *out, size_t n, size_t head,
-                         size_t nvec, Div np)
+__device__ __forceinline__ void spread_body(const InPtrs &in, int k, void *out, size_t n,
+                                            size_t head, size_t nvec, const Div &np)
 {
     using S         = typename Elt<T>::S;
     using L         = Lane<T>;
@@ -583,6 +602,20 @@ __global__ void __launch_bounds__(BLOCK)
     }
 }
 
+template <typename T, int OP, int EPI, int BLOCK>
+__global__ void __launch_bounds__(BLOCK)
+    reduce_spread_kernel(InPtrs in, int k, void *out, size_t n, size_t head,
+                         size_t nvec, Div np)
+{
+    if constexpr (EPI == EPI_DIV) {
+        if (np.pow2) {
+            spread_body<T, OP, EPI_MUL, BLOCK>(in, k, out, n, head, nvec, np);
+            return;
+        }
+    }
+    spread_body<T, OP, EPI, BLOCK>(in, k, out, n, head, nvec, np);
+}
+
 // Element-at-a-time kernel for inputs whose 16-B alignment residues differ
 // (e.g. host-side chunk slices at odd offsets). Still coalesced per element.
 template <typename T, int OP, int EPI, int BLOCK>
@@ -590,9 +623,12 @@ __global__ void __launch_bounds__(BLOCK)
     reduce_kernel_unaligned(InPtrs in, int k, void *out, size_t n, Div np)
 {
     using S = typename Elt<T>::S;
+    constexpr int EP = EPI == EPI_DIV ? EPI_MUL : EPI;
+    const bool p2    = EPI == EPI_DIV && np.pow2;
     for (size_t i = static_cast<size_t>(blockIdx.x) * BLOCK + threadIdx.x; i < n;
          i += static_cast<size_t>(gridDim.x) * BLOCK) {
-        reinterpret_cast<S *>(out)[i] = fold_scalar<T, OP, EPI>(in, k, i, np);
+        reinterpret_cast<S *>(out)[i] = p2 ? fold_scalar<T, OP, EP>(in, k, i, np)
+                                           : fold_scalar<T, OP, EPI>(in, k, i, np);
     }
 }
 
@@ -600,43 +636,42 @@ __global__ void __launch_bounds__(BLOCK)
 template <typename T> struct SmaMath;
 template <> struct SmaMath<float> {
     using S = float;
-    __device__ static S blend(S v, S s, float c1, float c2, const Div &dv)
+    template <bool P2> __device__ static S blend(S v, S s, float c1, float c2, const Div &dv)
     {
-        float avg = dv.pow2 ? __fmul_rn(s, dv.fi) : __fdiv_rn(s, dv.f);
+        float avg = P2 ? __fmul_rn(s, dv.fi) : __fdiv_rn(s, dv.f);
         return __fadd_rn(__fmul_rn(c1, v), __fmul_rn(c2, avg));
     }
 };
 template <> struct SmaMath<double> {
     using S = double;
-    __device__ static S blend(S v, S s, double c1, double c2, const Div &dv)
+    template <bool P2> __device__ static S blend(S v, S s, double c1, double c2, const Div &dv)
     {
-        double avg = dv.pow2 ? __dmul_rn(s, dv.di) : __ddiv_rn(s, dv.d);
+        double avg = P2 ? __dmul_rn(s, dv.di) : __ddiv_rn(s, dv.d);
         return __dadd_rn(__dmul_rn(c1, v), __dmul_rn(c2, avg));
     }
 };
 template <> struct SmaMath<f16_t> {
     using S = uint16_t;
-    __device__ static S blend(S v, S s, float c1, float c2, const Div &dv)
+    template <bool P2> __device__ static S blend(S v, S s, float c1, float c2, const Div &dv)
     {
         const float x = f16_to_f32(s);
-        float avg     = dv.pow2 ? __fmul_rn(x, dv.fi) : __fdiv_rn(x, dv.f);
+        float avg     = P2 ? __fmul_rn(x, dv.fi) : __fdiv_rn(x, dv.f);
         return f32_to_f16(__fadd_rn(__fmul_rn(c1, f16_to_f32(v)), __fmul_rn(c2, avg)));
     }
 };
 template <> struct SmaMath<bf16_t> {
     using S = uint16_t;
-    __device__ static S blend(S v, S s, float c1, float c2, const Div &dv)
+    template <bool P2> __device__ static S blend(S v, S s, float c1, float c2, const Div &dv)
     {
         const float x = bf16_to_f32(s);
-        float avg     = dv.pow2 ? __fmul_rn(x, dv.fi) : __fdiv_rn(x, dv.f);
+        float avg     = P2 ? __fmul_rn(x, dv.fi) : __fdiv_rn(x, dv.f);
         return f32_to_bf16(__fadd_rn(__fmul_rn(c1, bf16_to_f32(v)), __fmul_rn(c2, avg)));
     }
 };
 
-template <typename T, typename C, int BLOCK, int UNROLL>
-__global__ void __launch_bounds__(BLOCK)
-    sma_kernel(void *v, const void *s, size_t n, size_t head, size_t nvec,
-               C c1, C c2, Div np, int vec_ok)
+template <typename T, typename C, int BLOCK, int UNROLL, bool P2>
+__device__ __forceinline__ void sma_body(void *v, const void *s, size_t n, size_t head,
+                                         size_t nvec, C c1, C c2, const Div &np, int vec_ok)
 {
     using S         = typename SmaMath<T>::S;
     constexpr int V = Vec<S>::N;
@@ -645,7 +680,7 @@ __global__ void __launch_bounds__(BLOCK)
     const size_t tid = static_cast<size_t>(blockIdx.x) * BLOCK + threadIdx.x;
     if (!vec_ok) {
         for (size_t i = tid; i < n; i += static_cast<size_t>(gridDim.x) * BLOCK) {
-            pv[i] = SmaMath<T>::blend(pv[i], ps[i], c1, c2, np);
+            pv[i] = SmaMath<T>::template blend<P2>(pv[i], ps[i], c1, c2, np);
         }
         return;
     }
@@ -653,7 +688,7 @@ __global__ void __launch_bounds__(BLOCK)
     const size_t nedge = head + (n - vend);
     if (tid < nedge) {
         const size_t i = tid < head ? tid : vend + (tid - head);
-        pv[i]          = SmaMath<T>::blend(pv[i], ps[i], c1, c2, np);
+        pv[i]          = SmaMath<T>::template blend<P2>(pv[i], ps[i], c1, c2, np);
     }
     char *vb       = reinterpret_cast<char *>(v) + head * sizeof(S);
     const char *sb = reinterpret_cast<const char *>(s) + head * sizeof(S);
@@ -673,7 +708,7 @@ __global__ void __launch_bounds__(BLOCK)
                 Vec<S> r;
 #pragma unroll
                 for (int e = 0; e < V; ++e) {
-                    r.e[e] = SmaMath<T>::blend(a[u].e[e], b[u].e[e], c1, c2, np);
+                    r.e[e] = SmaMath<T>::template blend<P2>(a[u].e[e], b[u].e[e], c1, c2, np);
                 }
                 st_vec<S>(vb, v0 + u * BLOCK, r);
             }
@@ -684,10 +719,23 @@ __global__ void __launch_bounds__(BLOCK)
                 Vec<S> a = ld_vec<S, 1>(vb, vi), b = ld_vec<S, 1>(sb, vi);
                 Vec<S> r;
 #pragma unroll
-                for (int e = 0; e < V; ++e) r.e[e] = SmaMath<T>::blend(a.e[e], b.e[e], c1, c2, np);
+                for (int e = 0; e < V; ++e) r.e[e] = SmaMath<T>::template blend<P2>(a.e[e], b.e[e], c1, c2, np);
                 st_vec<S>(vb, vi, r);
             }
         }
+    }
+}
+
+// the /np choice made once per kernel (see EPI_MUL above)
+template <typename T, typename C, int BLOCK, int UNROLL>
+__global__ void __launch_bounds__(BLOCK)
+    sma_kernel(void *v, const void *s, size_t n, size_t head, size_t nvec,
+               C c1, C c2, Div np, int vec_ok)
+{
+    if (np.pow2) {
+        sma_body<T, C, BLOCK, UNROLL, true>(v, s, n, head, nvec, c1, c2, np, vec_ok);
+    } else {
+        sma_body<T, C, BLOCK, UNROLL, false>(v, s, n, head, nvec, c1, c2, np, vec_ok);
     }
 }
 

@@ -89,8 +89,11 @@ def main():
            timeit(lambda x: ops.bucket_div_(x, 8), sets), dtype="torch.float32")
     sets = [(torch.randn(n, device=dev), torch.randn(n, device=dev), torch.randn(n, device=dev))
             for _ in range(3)]
-    report("reduce_avg k=2 f32 (fused /np)", 3 * BYTES,
+    report("reduce_avg k=2 f32 (fused /np, np=3: IEEE division)", 3 * BYTES,
            timeit(lambda a, b, c: ops.bucket_reduce_avg([a, b], 3, out=c), sets),
+           dtype="torch.float32")
+    report("reduce_avg k=2 f32 (fused /np, np=2: exact multiply)", 3 * BYTES,
+           timeit(lambda a, b, c: ops.bucket_reduce_avg([a, b], 2, out=c), sets),
            dtype="torch.float32")
     sets = [(torch.randn(n, device=dev), torch.randn(n, device=dev)) for _ in range(3)]
     report("sma_blend f32", 3 * BYTES,
