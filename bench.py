@@ -98,6 +98,9 @@ def parse():
     ap.add_argument("--c1-rank", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--c1-mode", default="device", help=argparse.SUPPRESS)
     ap.add_argument("--c1-dir", default="", help=argparse.SUPPRESS)
+    ap.add_argument("--p2p-child", default="", help=argparse.SUPPRESS)
+    ap.add_argument("--p2p-out", default="", help=argparse.SUPPRESS)
+    ap.add_argument("--p2p-timeout", type=float, default=150.0, help=argparse.SUPPRESS)
     ap.add_argument("--profile-only", action="store_true",
                     help="only the timed kernel loop (for rocprofv3 runs)")
     return ap.parse_args()
@@ -414,6 +417,8 @@ def main():
         return c1_child(args)
     if args.config == "c1":
         return c1_parent(args)
+    if args.p2p_child:
+        return p2p_child(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -549,15 +554,9 @@ def main():
                                                           args.buckets, False)),
                  ("c4_torch", lambda: bench_c4(world, rank, dev, steps_x, 5, exchange="torch")),
                  ("c5_torch", lambda: bench_c5(world, rank, dev, steps_x, 5, exchange="torch")),
-                 ("c3_ar", lambda: bench_c3_ar(world, rank, dev, steps_x, 5, n, x)),
-                 # last: the experimental peer-to-peer paths
-                 ("c3_p2p", lambda: bench_c3_p2p(world, rank, dev, steps_x, 5, n, x)),
-                 ("c3_p2p_push", lambda: bench_c3_p2p(world, rank, dev, steps_x, 5, n, x,
-                                                      mode="push")),
-                 ("c3_p2p_hostbar", lambda: bench_c3_p2p(world, rank, dev, steps_x, 5, n, x,
-                                                         barrier="host")),
-                 ("c4_p2p", lambda: bench_c4(world, rank, dev, steps_x, 5, exchange="p2p")),
-                 ("c5_p2p", lambda: bench_c5(world, rank, dev, steps_x, 5, exchange="p2p")))
+                 ("c3_ar", lambda: bench_c3_ar(world, rank, dev, steps_x, 5, n, x)))
+        # last: the experimental peer-to-peer paths, in child processes
+        extra += tuple(_p2p_runs(world, rank, dev, steps_x, n, x).items())
         # The primary number is measured by now: a sub-benchmark that hangs
         # (a peer mapping refused in a way that blocks, a stuck collective)
         # must not take it down. Past --extras-timeout every rank dumps its
@@ -569,11 +568,12 @@ def main():
                               (args, rank, world, sets, s_bytes, n, hot_s, prim, out))
         dog.daemon = True
         dog.start()
+        t_extras = time.perf_counter()
         wanted = args.extras.split(",")
         for key, fn in extra:
             if args.no_extra:
                 break
-            if key not in wanted:
+            if key not in wanted or key in P2P_KEYS:
                 continue
             _progress(rank, "sub-benchmark %s" % key)
             out["_running"] = key
@@ -588,6 +588,12 @@ def main():
                 res = {"error": err or "failed on another rank"}
             res["wall_s"] = round(time.perf_counter() - t0, 2)
             out[key] = res
+        p2p = [k for k, _ in extra if k in P2P_KEYS and k in wanted and not args.no_extra]
+        if p2p:
+            _progress(rank, "sub-benchmarks %s (child processes)" % ",".join(p2p))
+            out["_running"] = "p2p children"
+            left = args.extras_timeout - (time.perf_counter() - t_extras) - 20.0
+            out.update(p2p_extras(args, rank, world, local_rank, dev, p2p, left))
         out.pop("_running", None)
         dog.cancel()
         if native is not None:
@@ -733,6 +739,127 @@ def _fill(gb, rank_seed, dev, dtype):
 
 
 _NATIVE = {}  # the primary's NativeExchange, reused by the sub-benchmarks
+
+# The peer-to-peer sub-benchmarks map every peer's buckets and signal words
+# over xGMI (HIP IPC) and spin on device barriers: the one part of the line
+# that has never run across devices before the driver's multi-GPU node. They
+# run in one child process per rank (own process group on its own port), so a
+# fault or an abort there ends the child, not the ranks holding the line.
+P2P_KEYS = ("c3_p2p", "c3_p2p_push", "c3_p2p_hostbar", "c4_p2p", "c5_p2p")
+
+
+def _p2p_runs(world, rank, dev, steps, n, x):
+    return {
+        "c3_p2p": lambda: bench_c3_p2p(world, rank, dev, steps, 5, n, x),
+        "c3_p2p_push": lambda: bench_c3_p2p(world, rank, dev, steps, 5, n, x, mode="push"),
+        "c3_p2p_hostbar": lambda: bench_c3_p2p(world, rank, dev, steps, 5, n, x, barrier="host"),
+        "c4_p2p": lambda: bench_c4(world, rank, dev, steps, 5, exchange="p2p"),
+        "c5_p2p": lambda: bench_c5(world, rank, dev, steps, 5, exchange="p2p"),
+    }
+
+
+def p2p_extras(args, rank, world, local_rank, dev, keys, seconds):
+    """Every rank starts `bench.py --p2p-child` and waits for it (bounded);
+    rank 0 returns the children's results, or an error per sub-benchmark."""
+    import subprocess
+    import tempfile
+    if not _agree(seconds >= 30.0, dev):
+        return {k: {"error": "not run: %.0f s of --extras-timeout left" % seconds} for k in keys}
+    port = torch.tensor([_free_port() if rank == 0 else 0], dtype=torch.int64, device=dev)
+    dist.broadcast(port, 0)
+    port = int(port.item())
+    path = os.path.join(tempfile.gettempdir(), "kf_bench_p2p_%d_%d.json" % (port, rank))
+    # not the launcher's rendezvous: the child group has its own TCP store
+    env = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC")}
+    env.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(local_rank),
+               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    cmd = [sys.executable, os.path.abspath(__file__), "--p2p-child", ",".join(keys),
+           "--p2p-out", path, "--p2p-timeout", str(seconds - 10.0),
+           "--elems", str(args.elems), "--steps", str(min(args.steps, 50)),
+           "--dist-backend", args.dist_backend]
+    if args.device_index is not None:
+        cmd += ["--device-index", str(args.device_index)]
+    t0 = time.perf_counter()
+    p = subprocess.Popen(cmd, env=env)
+    try:
+        rc = p.wait(timeout=seconds)
+    except subprocess.TimeoutExpired:
+        p.kill()
+        p.wait()
+        rc = "timeout"
+    ok = _agree(rc == 0, dev)
+    res = {}
+    if rank == 0 and os.path.exists(path):
+        with open(path) as f:
+            res = json.load(f)
+    if os.path.exists(path):
+        os.unlink(path)
+    for k in keys:
+        if k not in res:
+            res[k] = {"error": "child process of rank %d ended with %s before finishing it" %
+                      (rank, rc) if rc != 0 else ("failed on another rank's child" if not ok
+                                                  else "no result written")}
+    res["p2p_children"] = {"rc_rank0": rc, "all_ok": ok, "wall_s": round(time.perf_counter() - t0, 2)}
+    return res
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def p2p_child(args):
+    """One rank of the peer-to-peer sub-benchmarks (see P2P_KEYS): its own
+    process group, the same synthetic x as the parent, the results of rank 0
+    written to --p2p-out. Bounded by its own watchdog."""
+    world = int(os.environ["WORLD_SIZE"])
+    rank = int(os.environ["RANK"])
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    def give_up():
+        print("[bench] p2p child rank %d: not done within %.0f s" % (rank, args.p2p_timeout),
+              file=sys.stderr, flush=True)
+        import faulthandler
+        faulthandler.dump_traceback(file=sys.stderr, all_threads=True)
+        os._exit(5)
+
+    dog = threading.Timer(args.p2p_timeout, give_up)
+    dog.daemon = True
+    dog.start()
+    dev_index = local_rank if args.device_index is None else args.device_index
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
+    init = "tcp://127.0.0.1:%s" % os.environ["MASTER_PORT"]
+    if args.dist_backend == "nccl":
+        dist.init_process_group("nccl", init_method=init, rank=rank, world_size=world,
+                                device_id=dev)
+    else:
+        dist.init_process_group(args.dist_backend, init_method=init, rank=rank, world_size=world)
+    _progress(rank, "p2p children: process group of %d up" % world)
+    n = args.elems
+    x = torch.randn(n, device=dev, generator=torch.Generator(device=dev).manual_seed(2 * rank))
+    runs = _p2p_runs(world, rank, dev, args.steps, n, x)
+    out = {}
+    for key in args.p2p_child.split(","):
+        _progress(rank, "sub-benchmark %s" % key)
+        t0 = time.perf_counter()
+        try:
+            res, err = runs[key](), None
+        except Exception as e:
+            res, err = None, repr(e)[:300]
+        if not _agree(err is None, dev):
+            res = {"error": err or "failed on another rank"}
+        res["wall_s"] = round(time.perf_counter() - t0, 2)
+        out[key] = res
+        if rank == 0:  # what finished survives a later fault
+            with open(args.p2p_out, "w") as f:
+                json.dump(out, f)
+    dog.cancel()
+    dist.barrier()
+    dist.destroy_process_group()
+    return 0
 
 
 def _primary_exchange(args, rank, world, dev):
