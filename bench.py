@@ -429,9 +429,9 @@ def main():
     dev = torch.device("cuda", dev_index)
     if world > 1:
         if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            _quiet(dist.init_process_group, "nccl", device_id=dev)
         else:
-            dist.init_process_group(args.dist_backend)
+            _quiet(dist.init_process_group, args.dist_backend)
 
     from kungfu_amd import _lib
     lib = _lib.load()
@@ -780,7 +780,9 @@ def p2p_extras(args, rank, world, local_rank, dev, keys, seconds):
     if args.device_index is not None:
         cmd += ["--device-index", str(args.device_index)]
     t0 = time.perf_counter()
-    p = subprocess.Popen(cmd, env=env)
+    # the child's stdout (gloo prints there) goes to stderr: stdout carries
+    # only the line
+    p = subprocess.Popen(cmd, env=env, stdout=sys.stderr.fileno())
     try:
         rc = p.wait(timeout=seconds)
     except subprocess.TimeoutExpired:
@@ -801,6 +803,20 @@ def p2p_extras(args, rank, world, local_rank, dev, keys, seconds):
                                                   else "no result written")}
     res["p2p_children"] = {"rc_rank0": rc, "all_ok": ok, "wall_s": round(time.perf_counter() - t0, 2)}
     return res
+
+
+def _quiet(fn, *a, **kw):
+    """fn with file descriptor 1 pointed at stderr: gloo announces its mesh on
+    stdout, which carries only the JSON line."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        return fn(*a, **kw)
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
 
 
 def _free_port():
@@ -833,10 +849,11 @@ def p2p_child(args):
     dev = torch.device("cuda", dev_index)
     init = "tcp://127.0.0.1:%s" % os.environ["MASTER_PORT"]
     if args.dist_backend == "nccl":
-        dist.init_process_group("nccl", init_method=init, rank=rank, world_size=world,
-                                device_id=dev)
+        _quiet(dist.init_process_group, "nccl", init_method=init, rank=rank, world_size=world,
+               device_id=dev)
     else:
-        dist.init_process_group(args.dist_backend, init_method=init, rank=rank, world_size=world)
+        _quiet(dist.init_process_group, args.dist_backend, init_method=init, rank=rank,
+               world_size=world)
     _progress(rank, "p2p children: process group of %d up" % world)
     n = args.elems
     x = torch.randn(n, device=dev, generator=torch.Generator(device=dev).manual_seed(2 * rank))
