@@ -34,6 +34,46 @@ def kungfu_dtype(t):
         raise TypeError("kungfu_amd: unsupported dtype %s" % t.dtype)
 
 
+# The reference's TF dtype map, as it is (tensorflow/ops.h:14-33): no fp16,
+# and DT_BFLOAT16 -> KungFu_FLOAT16, so a bf16 tensor's bit patterns are
+# reduced as fp16 numbers. The build's own map (kungfu_dtype) gives bf16 its
+# own code and fp32-accumulated semantics; this one exists so that a caller
+# that wants the reference's exact bits can ask for them (pass the code as
+# `dtype` to the device ops).
+TF_DTYPES = {
+    "int32": DataType.I32,
+    "int64": DataType.I64,
+    "bfloat16": DataType.F16,
+    "float32": DataType.F32,
+    "float64": DataType.F64,
+    "bool": DataType.BOOL,
+}
+
+
+def to_kungfu_type(tf_dtype):
+    """ops.h:14-33 to_kungfu_type: a TF dtype name ("float32", "bfloat16", ...
+    or anything with such a `name`) -> KungFu code; anything else raises, as
+    the reference's `throw std::invalid_argument("unsupported dtype")`."""
+    name = getattr(tf_dtype, "name", tf_dtype)
+    try:
+        return TF_DTYPES[name]
+    except KeyError:
+        raise ValueError("unsupported dtype")
+
+
+def _dtype_for(t, dtype):
+    """The KungFu code a device op runs with: the tensor's own, or an explicit
+    one of the same element size (e.g. to_kungfu_type("bfloat16") on a bf16
+    tensor, the reference's TF semantics)."""
+    if dtype is None:
+        return kungfu_dtype(t)
+    dt = DataType(int(dtype))
+    if dt.size() != t.element_size():
+        raise ValueError("dtype %s does not match the tensor's %d-byte elements"
+                         % (dt.name, t.element_size()))
+    return dt
+
+
 def _op(op):
     if op is None:
         return OP.SUM
@@ -56,8 +96,10 @@ def _stream(stream, dev):
     return s.cuda_stream
 
 
-def bucket_reduce(inputs, out=None, op="sum", stream=None):
-    """out = inputs[0] op inputs[1] op ... (left fold, in the given order)."""
+def bucket_reduce(inputs, out=None, op="sum", stream=None, dtype=None):
+    """out = inputs[0] op inputs[1] op ... (left fold, in the given order).
+    `dtype`: a KungFu code to reduce with instead of the tensors' own
+    (same element size)."""
     inputs = list(inputs)
     if out is None:
         out = torch.empty_like(inputs[0])
@@ -69,7 +111,7 @@ def bucket_reduce(inputs, out=None, op="sum", stream=None):
     lib = _lib.load()
     rc = lib.kf_bucket_reduce(_lib.ptr_array([t.data_ptr() for t in inputs]),
                               len(inputs), out.data_ptr(), n,
-                              int(kungfu_dtype(out)), int(_op(op)),
+                              int(_dtype_for(out, dtype)), int(_op(op)),
                               _stream(stream, out.device))
     _lib.check(rc, "kf_bucket_reduce")
     return out

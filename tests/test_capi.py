@@ -174,3 +174,23 @@ def test_go_overlay_binds_declared_symbols():
             if name in libc:
                 continue
             assert re.search(r"\b%s\b" % re.escape(name), header), (path, name)
+
+
+def test_tf_dtype_map_is_the_reference_one():
+    """kungfu_amd.ops.TF_DTYPES / to_kungfu_type restate tensorflow/ops.h:14-33
+    (bf16 -> KungFu_FLOAT16 included); the fixture was read from the
+    reference's headers by tests/golden/gen_tf_dtype_map.py."""
+    import json
+    from kungfu_amd import ops
+    with open(os.path.join(ROOT, "tests", "golden", "tf_dtype_map.json")) as f:
+        ref = json.load(f)["map"]
+    assert {k: int(v) for k, v in ops.TF_DTYPES.items()} == {k: v["code"] for k, v in ref.items()}
+    for name, v in ref.items():
+        assert int(ops.to_kungfu_type(name)) == v["code"]
+
+    class TfLike:  # anything with a `name`, as a tf.DType
+        name = "bfloat16"
+    assert int(ops.to_kungfu_type(TfLike())) == 0x20208
+    for bad in ("float16", "uint8", "complex64"):  # ops.h: no DT_HALF, throws
+        with pytest.raises(ValueError, match="unsupported dtype"):
+            ops.to_kungfu_type(bad)

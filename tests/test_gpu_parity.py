@@ -628,3 +628,29 @@ def test_bf16_two_input_sum_matches_torch_gpu(dev):
         got = ops.bucket_reduce([x, y])
         want = x + y
         assert torch.equal(got.view(torch.int16), want.view(torch.int16)), n
+
+
+# ---- a15: the reference's TF dtype map on a bf16 tensor ----
+
+def test_bf16_tensor_with_reference_tf_mapping(dev, lib, orc):
+    """tensorflow/ops.h:14-33 maps DT_BFLOAT16 to KungFu_FLOAT16, so the
+    reference reduces a bf16 tensor's bit patterns as fp16 numbers (per-hop
+    fp16 rounding, f16.c:16-50). Asked for that code (ops.to_kungfu_type), the
+    device op gives exactly those bits: the oracle's fp16 fold of the raw
+    bf16 patterns, k = 2 and k = 4."""
+    from kungfu_amd import ops
+    g = torch.Generator(device=dev).manual_seed(15)
+    for k in (2, 4):
+        xs = [torch.randn(100003, device=dev, generator=g).bfloat16() for _ in range(k)]
+        out = ops.bucket_reduce(xs, dtype=ops.to_kungfu_type("bfloat16"))
+        torch.cuda.synchronize()
+        bits = [x.view(torch.int16).cpu().numpy().view(np.uint16) for x in xs]
+        want = orc.reduce_k(bits, "f16")
+        assert np.array_equal(out.view(torch.int16).cpu().numpy().view(np.uint16), want)
+        # the build's own map: fp32 accumulation, one rounding
+        own = ops.bucket_reduce(xs)
+        torch.cuda.synchronize()
+        assert np.array_equal(own.view(torch.int16).cpu().numpy().view(np.uint16),
+                              orc.reduce_k(bits, "bf16"))
+    with pytest.raises(ValueError):
+        ops.bucket_reduce(xs, dtype=ops.to_kungfu_type("float32"))  # 4-byte code, 2-byte data
