@@ -297,8 +297,13 @@ def c1_child(args):
     """One peer of the C1 run. Rank 0 (the star root) reduces with:
     device   — page-locked ingest + HIP fold, bucket resident in HBM;
     dropin   — host buffers, std_transform_2 of libkungfu_amd.so per chunk;
-    cpu      — host buffers, the oracle's restatement of the reference reduce
-               (this is bench.py's CPU-baseline leg)."""
+    cpu      — host buffers, the reference's own reduce (oracle/_ref) or the
+               oracle's restatement of it (this is bench.py's CPU-baseline leg);
+    cpu_dev  — the bucket resident in HBM as in `device`, reduced the way the
+               reference does for GPU tensors (its collective op is a CPU
+               kernel, so the framework copies the tensor to the host and
+               back): D2H into a page-locked buffer, the `cpu` all-reduce,
+               H2D, all inside the timed step."""
     from kungfu_amd.session import Session
     r, npeers = args.c1_rank, args.c1_np
     x = ((r + 1) * (np.arange(C1_ELEMS) % 1024) / 1024).astype(np.float32)
@@ -315,7 +320,7 @@ def c1_child(args):
         xs, ys = x, np.zeros_like(x)
         fn = None
         cpu_kind = None
-        if args.c1_mode == "cpu":
+        if args.c1_mode in ("cpu", "cpu_dev"):
             # the reference's own std_transform_2 (oracle/_ref) when built,
             # else the oracle's restatement of it
             from oracle import oracle
@@ -330,13 +335,28 @@ def c1_child(args):
         sess = Session(r, npeers, args.c1_dir, mode="host", host_reduce_fn=fn)
         result = lambda: ys  # noqa: E731
     name = "NegotiatedGrad_0/AllReduce"
+    step = lambda: sess.all_reduce(xs, ys, name)  # noqa: E731
+    if args.c1_mode == "cpu_dev":
+        dev = torch.device("cuda", 0)
+        xd, yd = torch.from_numpy(x).to(dev), torch.zeros(C1_ELEMS, device=dev)
+        xh = torch.empty(C1_ELEMS, dtype=torch.float32).pin_memory()
+        yh = torch.empty(C1_ELEMS, dtype=torch.float32).pin_memory()
+        xs, ys = xh.numpy(), yh.numpy()
+
+        def step():
+            xh.copy_(xd, non_blocking=True)
+            torch.cuda.synchronize()
+            sess.all_reduce(xs, ys, name)
+            yd.copy_(yh, non_blocking=True)
+            torch.cuda.synchronize()
+        result = lambda: yd.cpu().numpy()  # noqa: E731
     for _ in range(args.warmup):
-        sess.all_reduce(xs, ys, name)
+        step()
     ok = bool(np.array_equal(result(), want))
     ts = []
     for _ in range(args.steps):
         t0 = time.perf_counter()
-        sess.all_reduce(xs, ys, name)
+        step()
         ts.append(time.perf_counter() - t0)
     ok = ok and bool(np.array_equal(result(), want))
     sess.close()
@@ -348,7 +368,7 @@ def c1_child(args):
                "latency_ms_median": round(med * 1e3, 4),
                "latency_ms_min": round(ts[0] * 1e3, 4),
                "rate_GiBps": round(4 * (npeers - 1) * nbytes / med / 2**30, 3)}
-        if args.c1_mode == "cpu":
+        if args.c1_mode in ("cpu", "cpu_dev"):
             rec["kind"] = cpu_kind
         print(json.dumps(rec), flush=True)
 
@@ -385,18 +405,21 @@ def c1_summary(steps=100, warmup=10):
     one 4 MiB fp32 bucket, median latency and 4(np-1)*bytes/t
     (kungfu-bench-allreduce.go:73-80); the device session against the
     reference's own CPU fold (oracle/_ref) in the same session engine."""
-    res = c1_run(2, ("device", "cpu"), steps, warmup, timeout=180)
+    res = c1_run(2, ("device", "cpu", "cpu_dev"), steps, warmup, timeout=180)
     out = {"workload": "C1: np=2 localhost, one 4 MiB fp32 bucket, 4 x 1 MiB chunks, STAR "
                        "at rank 0, rchannel framing over unix sockets",
-           "np": 2, "steps": steps, "unit": "GiB/s (4(np-1)*bytes/t, median)"}
+           "np": 2, "steps": steps, "unit": "GiB/s (4(np-1)*bytes/t, median)",
+           "modes": "device: bucket in HBM, HIP fold; cpu: bucket in host memory, the "
+                    "reference's CPU fold; cpu_dev: bucket in HBM reduced the reference's "
+                    "way for GPU tensors (D2H, the cpu all-reduce, H2D)"}
     out.update(res)
     out["correct"] = all(r.get("correct") is True for r in res.values())
     return out
 
 
 def c1_parent(args):
-    modes = ("device", "device_chain", "dropin", "cpu") if args.c1_np > 2 else \
-        ("device", "dropin", "cpu")
+    modes = ("device", "device_chain", "dropin", "cpu", "cpu_dev") if args.c1_np > 2 else \
+        ("device", "dropin", "cpu", "cpu_dev")
     res = c1_run(args.c1_np, modes, args.steps, args.warmup)
     line = {
         "metric": "C1 all-reduce rate 4(np-1)*bytes/t (kungfu-bench-allreduce.go:73-80)",
