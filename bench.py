@@ -300,10 +300,11 @@ def c1_child(args):
     cpu      — host buffers, the reference's own reduce (oracle/_ref) or the
                oracle's restatement of it (this is bench.py's CPU-baseline leg);
     cpu_dev  — the bucket resident in HBM as in `device`, reduced the way the
-               reference does for GPU tensors (its collective op is a CPU
-               kernel, so the framework copies the tensor to the host and
-               back): D2H into a page-locked buffer, the `cpu` all-reduce,
-               H2D, all inside the timed step."""
+               reference does for GPU tensors (KungfuAllReduce is registered
+               for DEVICE_CPU only, tensorflow/ops/cpu/collective.cpp:103, so
+               the framework copies the tensor to the host and back): D2H into
+               a page-locked buffer, the `cpu` all-reduce, H2D, all inside the
+               timed step."""
     from kungfu_amd.session import Session
     r, npeers = args.c1_rank, args.c1_np
     x = ((r + 1) * (np.arange(C1_ELEMS) % 1024) / 1024).astype(np.float32)
