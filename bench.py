@@ -71,6 +71,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-staged", action="store_true")
+    ap.add_argument("--no-kernels", action="store_true",
+                    help="N=1: skip the other kernel families' rates")
     ap.add_argument("--dist-backend", default="nccl",
                     help="rehearsal only: gloo lets N ranks share one GPU")
     ap.add_argument("--device-index", type=int, default=None,
@@ -152,6 +154,106 @@ def time_local_reduce(lib, sets, steps, warmup, world):
     err = lib.kf_last_error()
     kernel_s = ev0.elapsed_time(ev1) / 1e3 / steps
     return kernel_s, wall, err
+
+
+def kernel_families(lib, dev):
+    """Every other kernel family behind the C ABI, timed in the driver's own
+    run the way the headline is (HIP events on the launch stream, launches
+    cycling over independent buffer sets, median of 5 x 20), each against the
+    8 TB/s roofline in algorithmic bytes and checked once against a torch
+    restatement on the same buffers (bit-exact: these are the same IEEE
+    operations). The placement of each allocation moves these rates by up to
+    5 %."""
+    from kungfu_amd import _lib, ops
+    s = torch.cuda.current_stream()
+    sp = s.cuda_stream
+    mib = 1 << 20
+    out = {}
+
+    def timed(launch, nsets):
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for i in range(nsets):
+            _lib.check(launch(i), "launch")
+        ts = []
+        for _ in range(5):
+            ev0.record(s)
+            for i in range(20):
+                launch(i % nsets)
+            ev1.record(s)
+            torch.cuda.synchronize()
+            ts.append(ev0.elapsed_time(ev1) * 1e3 / 20)
+        ts.sort()
+        return ts[2]
+
+    def report(name, algo_bytes, us, ok, what):
+        out[name] = {"us": round(us, 2), "algorithmic_bytes": algo_bytes,
+                     "frac": round(algo_bytes / us / 1e3 / HBM_PEAK_GBPS, 4),
+                     "correct": bool(ok), "what": what}
+
+    n = 256 * mib // 4
+    g = torch.Generator(device=dev).manual_seed(7)
+    for k in (4, 8):  # the k-input fold (star root, all-to-all fold)
+        sets = []
+        for _ in range(3):
+            ins = [torch.randn(n, device=dev, generator=g) for _ in range(k)]
+            sets.append((_lib.ptr_array([t.data_ptr() for t in ins]), torch.empty(n, device=dev), ins))
+        us = timed(lambda i: lib.kf_bucket_reduce(sets[i][0], k, sets[i][1].data_ptr(), n,
+                                                  KF_FLOAT, KF_SUM, sp), 3)
+        want = sets[0][2][0].clone()
+        for t in sets[0][2][1:]:
+            want += t
+        report("fold_k%d_f32" % k, (k + 1) * 256 * mib, us, torch.equal(sets[0][1], want),
+               "kf_bucket_reduce, %d inputs of 256 MiB, left fold" % k)
+        del sets, want
+        torch.cuda.empty_cache()
+    sets = [tuple(torch.randn(n, device=dev, generator=g) for _ in range(3)) for _ in range(3)]
+    us = timed(lambda i: lib.kf_bucket_reduce_avg(
+        _lib.ptr_array([sets[i][0].data_ptr(), sets[i][1].data_ptr()]), 2, sets[i][2].data_ptr(),
+        n, KF_FLOAT, 3, sp), 3)
+    x, y, z = sets[0]
+    report("avg_k2_np3_f32", 3 * 256 * mib, us,
+           torch.equal(z, (x + y) / torch.full_like(x, 3.0)),
+           "kf_bucket_reduce_avg, S-SGD fused (x + y) / 3, IEEE division")
+    xs = [t[0] for t in sets]
+    ref = xs[0].clone()
+    _lib.check(lib.kf_bucket_div(xs[0].data_ptr(), n, KF_FLOAT, 8, sp), "kf_bucket_div")
+    ok = torch.equal(xs[0], ref / torch.full_like(ref, 8.0))
+    us = timed(lambda i: lib.kf_bucket_div(xs[i].data_ptr(), n, KF_FLOAT, 8, sp), 3)
+    report("div_shard_np8_f32", 2 * 256 * mib, us, ok,
+           "kf_bucket_div in place, the shard /np between reduce-scatter and all-gather")
+    del sets, xs, ref
+    torch.cuda.empty_cache()
+    nb = 128 * mib  # bf16 elements in 256 MiB
+    vs = [torch.randn(nb, device=dev, generator=g).bfloat16() for _ in range(3)]
+    sm = [torch.randn(nb, device=dev, generator=g).bfloat16() for _ in range(3)]
+    v0 = vs[0].clone()
+    _lib.check(lib.kf_sma_blend(v0.data_ptr(), sm[0].data_ptr(), nb, 0x20209, 8, 0.1, sp), "sma")
+    want = ((1 - 0.1) * vs[0].float() + 0.1 * (sm[0].float() / 8))  # fp32 restatement
+    ok = bool(((v0.float() - want).abs() <= want.abs() * 2 ** -7 + 1e-30).all())
+    us = timed(lambda i: lib.kf_sma_blend(vs[i].data_ptr(), sm[i].data_ptr(), nb, 0x20209, 8,
+                                          0.1, sp), 3)
+    report("sma_blend_bf16", 3 * 256 * mib, us, ok,
+           "kf_sma_blend in place, v = 0.9 v + 0.1 (s / 8), bf16 (within one bf16 rounding "
+           "of the fp32 value; bit-exact checks in tests/)")
+    del vs, sm, v0, want
+    torch.cuda.empty_cache()
+    nbk, bk = 16, 4 * mib // 4  # 16 buckets of 4 MiB fp32 per launch
+    sets = []
+    for _ in range(6):
+        xs = [torch.randn(bk, device=dev, generator=g) for _ in range(nbk)]
+        ys = [torch.randn(bk, device=dev, generator=g) for _ in range(nbk)]
+        zs = [torch.empty(bk, device=dev) for _ in range(nbk)]
+        ins = _lib.ptr_array([p for a, b in zip(xs, ys) for p in (a.data_ptr(), b.data_ptr())])
+        sets.append((ins, _lib.ptr_array([t.data_ptr() for t in zs]),
+                     (ctypes.c_size_t * nbk)(*[bk] * nbk), xs, ys, zs))
+    us = timed(lambda i: lib.kf_bucket_reduce_batch(sets[i][0], 2, sets[i][1], sets[i][2], nbk,
+                                                    KF_FLOAT, KF_SUM, 0, sp), 6)
+    ok = all(torch.equal(z, x + y) for x, y, z in zip(*sets[0][3:]))
+    report("batch_16x4MiB_f32", nbk * 3 * 4 * mib, us, ok,
+           "kf_bucket_reduce_batch: 16 buckets of 4 MiB (C3's size), z = x + y, one launch")
+    del sets
+    torch.cuda.empty_cache()
+    return out
 
 
 def cpu_baseline(x, y, seconds):
@@ -628,6 +730,12 @@ def main():
                        parallelism=parallelism))
     res.update(out)
     if rank == 0 and world == 1:
+        if not args.no_kernels:
+            _progress(rank, "kernel families")
+            try:
+                res["kernels"] = kernel_families(lib, dev)
+            except Exception as e:  # the C2 line stands on its own
+                res["kernels"] = {"error": repr(e)[:300]}
         if not args.no_host_staged:
             res["host_staged"] = host_staged(lib, x, y)
         if not args.no_cpu_baseline:
