@@ -171,7 +171,10 @@ class NativeExchange:
         _lib.check(self.lib.kf_exchange_check(self._h), "kf_exchange_check")
 
     def finish(self):
-        """Nothing to settle: RCCL and the HIP epilogues are stream-ordered."""
+        """RCCL and the HIP epilogues are stream-ordered, so nothing waits;
+        an asynchronous RCCL error is raised here (the optimizers call this
+        before their update)."""
+        self.check()
 
     def close(self):
         if getattr(self, "_h", None):
