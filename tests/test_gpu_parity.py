@@ -654,3 +654,58 @@ def test_bf16_tensor_with_reference_tf_mapping(dev, lib, orc):
                               orc.reduce_k(bits, "bf16"))
     with pytest.raises(ValueError):
         ops.bucket_reduce(xs, dtype=ops.to_kungfu_type("float32"))  # 4-byte code, 2-byte data
+
+
+# ---- B2 under stream capture: the device API is graph-safe ----
+
+def test_b2_ops_capture_and_replay(dev, lib):
+    """kf_bucket_reduce / _avg / kf_bucket_div / kf_sma_blend /
+    kf_bucket_reduce_batch queued into a HIP graph (torch.cuda.CUDAGraph over
+    hipStreamBeginCapture) and replayed give the eager results bit for bit:
+    no allocation, no host sync and no pointer query inside the calls."""
+    import ctypes
+    from kungfu_amd import _lib
+    g = torch.Generator(device=dev).manual_seed(11)
+    n = 300007
+    x, y, w = (torch.randn(n, device=dev, generator=g) for _ in range(3))
+    v = torch.randn(n, device=dev, generator=g).bfloat16()
+    sb = torch.randn(n, device=dev, generator=g).bfloat16()
+    shards = [torch.randn(4099 + 17 * i, device=dev, generator=g) for i in range(8)]
+    z, a = torch.empty_like(x), torch.empty_like(x)
+
+    def work(s):
+        sp = s.cuda_stream
+        assert lib.kf_bucket_reduce(_lib.ptr_array([x.data_ptr(), y.data_ptr(), w.data_ptr()]), 3,
+                                    z.data_ptr(), n, 0x20408, 0, sp) == 0
+        assert lib.kf_bucket_reduce_avg(_lib.ptr_array([x.data_ptr(), y.data_ptr()]), 2,
+                                        a.data_ptr(), n, 0x20408, 3, sp) == 0
+        assert lib.kf_bucket_div(w.data_ptr(), n, 0x20408, 4, sp) == 0
+        assert lib.kf_sma_blend(v.data_ptr(), sb.data_ptr(), n, 0x20209, 4, 0.1, sp) == 0
+        ptrs = [t.data_ptr() for t in shards]
+        assert lib.kf_bucket_reduce_batch(
+            _lib.ptr_array(ptrs), 1, _lib.ptr_array(ptrs),
+            (ctypes.c_size_t * len(shards))(*[t.numel() for t in shards]), len(shards),
+            0x20408, 0, 8, sp) == 0
+
+    keep = [t.clone() for t in (w, v, *shards)]
+    work(torch.cuda.current_stream())  # eager
+    torch.cuda.synchronize()
+    want = [t.clone() for t in (z, a, w, v, *shards)]
+    for t, k in zip((w, v, *shards), keep):  # restore the in-place inputs
+        t.copy_(k)
+    z.zero_()
+    a.zero_()
+    graph = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(graph, stream=s):
+            work(s)
+    torch.cuda.synchronize()
+    for t, k in zip((w, v, *shards), keep):  # capture ran nothing; be sure
+        t.copy_(k)
+    graph.replay()
+    torch.cuda.synchronize()
+    got = (z, a, w, v, *shards)
+    for i, (gt, wt) in enumerate(zip(got, want)):
+        assert torch.equal(gt, wt), i
