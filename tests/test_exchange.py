@@ -492,3 +492,71 @@ def test_native_exchange_configs_full_size():
                                   oracle.sma_blend(before[j], sums[j], "bf16", 2, 0.1)), j
 
     _loop_ranks(2, c5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", ["c4", "c5"])
+def test_native_exchange_configs_world8(cfg):
+    """C4 and C5 at the world size BASELINE names for them (8 GPUs), full size,
+    through the native exchange over the loopback transport: C4 = ResNet-50's
+    25,583,592 fp32 in 16 buckets, S-SGD /np, both algos (auto -> RCCL-shaped
+    reduce-scatter, a2a -> rank-order fold); C5 = BERT-base's first 201 tensors
+    (109,483,778 bf16), SMA alpha 0.1 (auto -> a2a). The oracle's rank-order
+    fold of all 8 ranks is computed once; every rank's buckets must equal it
+    bit for bit."""
+    import json
+    import torch
+    from kungfu_amd.collective import GradBuckets
+    from oracle import oracle
+    dev = _gpu()
+    world = 8
+    models = json.load(open(os.path.join(HERE, "golden", "models.json")))
+
+    def filled(sizes, dtype, seed, **kw):
+        gb = GradBuckets(sizes, dtype, dev, world, **kw)
+        g = torch.Generator(device=dev).manual_seed(seed)
+        for v in gb.views:
+            v.copy_(torch.randn(v.numel(), device=dev, generator=g).to(dtype))
+        return gb
+
+    if cfg == "c4":
+        sizes = models["resnet50-imagenet"]
+        assert sum(sizes) == 25583592
+        mk = [lambda r=r: filled(sizes, torch.float32, 900 + r, n_buckets=16) for r in range(world)]
+        ref = [mk[r]() for r in range(world)]
+        want = [oracle.reduce_avg([gb.buckets[j].cpu().numpy() for gb in ref], "f32", world)
+                for j in range(16)]
+        del ref
+        for algo in ("auto", "a2a"):
+            def body(rank, ex, algo=algo):
+                ex.algo = algo
+                mine = mk[rank]()
+                ex.all_reduce_(mine.buckets, average=True, coalesce=False)
+                torch.cuda.synchronize()
+                for j, (b, sp) in enumerate(zip(mine.buckets, mine.spans)):
+                    assert np.array_equal(b[:sp].cpu().numpy(), want[j][:sp]), (algo, j)
+
+            _loop_ranks(world, body)
+    else:
+        bert = models["bert"][:201]
+        assert sum(bert) == 109483778
+        kw = dict(bucket_bytes=16 << 20)
+        mk = [lambda r=r: filled(bert, torch.bfloat16, 1700 + r, **kw) for r in range(world)]
+        ref = [mk[r]() for r in range(world)]
+        nb = len(ref[0].buckets)
+        sums = [oracle.reduce_k([_to_np(gb.buckets[j], "bf16") for gb in ref], "bf16", "sum")
+                for j in range(nb)]
+        before = [[_to_np(b, "bf16") for b in gb.buckets] for gb in ref]
+        del ref
+
+        def body(rank, ex):
+            ex.algo = "auto"
+            mine = mk[rank]()
+            ex.sma_(mine.buckets, 0.1)
+            torch.cuda.synchronize()
+            for j, b in enumerate(mine.buckets):
+                assert np.array_equal(_to_np(b, "bf16"),
+                                      oracle.sma_blend(before[rank][j], sums[j], "bf16", world,
+                                                       0.1)), (rank, j)
+
+        _loop_ranks(world, body)
