@@ -31,6 +31,7 @@
 #include <rccl/rccl.h>
 
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <map>
@@ -200,6 +201,19 @@ ncclRedOp_t nccl_op(KungFu_Op op)
 }
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// Testing only: KUNGFU_AMD_EXCHANGE_W1_COLLECTIVES=1 sends a one-rank
+// exchange through the RCCL calls and the batched epilogue instead of the
+// identity copy, so a one-GPU box exercises librccl's own entry points with
+// the exchange's exact arguments (RCCL refuses two ranks on one device).
+bool w1_collectives()
+{
+    static const bool on = [] {
+        const char *e = std::getenv("KUNGFU_AMD_EXCHANGE_W1_COLLECTIVES");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
 
 // ---------------------------------------------------------------------------
 // Loopback transport (testing): the RCCL entry points the exchange uses,
@@ -527,7 +541,7 @@ int kf_exchange::batch(const void *const *sends, void *const *recvs, const size_
     const Rccl &R = *this->R;
     const int sz  = tsize(dt);
     const int W = world, r = rank;
-    if (W == 1) {  // a single peer: the sum is the bucket, x / 1 == x
+    if (W == 1 && !w1_collectives()) {  // a single peer: the sum is the bucket, x / 1 == x
         for (int b = 0; b < nb; ++b) {
             if (counts[b] && sends[b] != recvs[b]) {
                 KF_HIP(hipMemcpyAsync(recvs[b], sends[b], counts[b] * sz, hipMemcpyDeviceToDevice, s));

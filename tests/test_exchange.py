@@ -560,3 +560,104 @@ def test_native_exchange_configs_world8(cfg):
                                                        0.1)), (rank, j)
 
         _loop_ranks(world, body)
+
+
+_W1_CHILD = r"""
+import ctypes, sys
+import numpy as np
+import torch
+sys.path.insert(0, %r)
+from kungfu_amd import _lib
+from kungfu_amd.collective import GradBuckets
+from kungfu_amd.exchange import NativeExchange, Scheduler
+from oracle import oracle
+dev = torch.device("cuda:0")
+torch.cuda.set_device(0)
+lib = _lib.load()
+g = torch.Generator(device=dev).manual_seed(7)
+def rnd(n, dt):
+    if dt.is_floating_point:
+        return torch.randn(n, device=dev, generator=g).to(dt)
+    info = torch.iinfo(dt)
+    return torch.randint(max(info.min, -2**31), min(info.max, 2**31 - 1), (n,), device=dev,
+                         generator=g).to(dt)
+for algo in ("rs", "a2a", "auto"):
+    ex = NativeExchange(algo=algo, device=dev)
+    # C3's shape: 64 grouped 4 MiB buckets, S-SGD average (x / 1 == x)
+    gb = GradBuckets([64 << 20], torch.float32, dev, 1, n_buckets=64)
+    gb.views[0].copy_(rnd(64 << 20, torch.float32))
+    want = gb.views[0].clone()
+    ex.all_reduce_(gb.buckets, average=True, coalesce=False)
+    torch.cuda.synchronize()
+    assert torch.equal(gb.views[0], want), (algo, "c3")
+    cases = [(torch.bfloat16, "sum", True), (torch.float16, "sum", False),
+             (torch.int32, "max", False), (torch.int64, "sum", False),
+             (torch.uint8, "sum", False), (torch.float64, "sum", True),
+             (torch.int16, "sum", False)]
+    for dt, op, avg in cases:
+        bs = [rnd(n, dt) for n in (1 << 20, 4097, 1, 333)]
+        w = [b.clone() for b in bs]
+        try:
+            ex.all_reduce_(bs, op=op, average=avg, coalesce=False)
+        except _lib.KungFuAMDError as e:
+            # int16 has no RCCL reduction type: only the forced rs algo refuses it
+            assert algo == "rs" and dt == torch.int16, (algo, dt, e)
+            continue
+        torch.cuda.synchronize()
+        assert all(torch.equal(a, b) for a, b in zip(bs, w)), (algo, dt)
+    # out of place, single-bucket entry
+    x = rnd(1 << 20, torch.float32)
+    y = torch.empty_like(x)
+    _lib.check(lib.kf_exchange_all_reduce(ex._h, x.data_ptr(), y.data_ptr(), y.numel(),
+                                          0x20408, 0, 1, {"auto": 0, "rs": 1, "a2a": 2}[algo],
+                                          torch.cuda.current_stream().cuda_stream), "ar")
+    torch.cuda.synchronize()
+    assert torch.equal(x, y), (algo, "out of place")
+    # SMA batch: v <- (1 - a) v + a (v / 1)
+    for dt, name in ((torch.float32, "f32"), (torch.bfloat16, "bf16")):
+        vs = [rnd(n, dt) for n in (30001, 1 << 18)]
+        v0 = [v.cpu().view(torch.int16).numpy().view(np.uint16).copy() if name == "bf16"
+              else v.cpu().numpy().copy() for v in vs]
+        ex.sma_(vs, 0.1)
+        torch.cuda.synchronize()
+        for v, a in zip(vs, v0):
+            got = (v.cpu().view(torch.int16).numpy().view(np.uint16) if name == "bf16"
+                   else v.cpu().numpy())
+            assert np.array_equal(got, oracle.sma_blend(a, a, name, 1, 0.1)), (algo, name)
+    # overlap handle + the ordered scheduler (its order broadcast is an RCCL call)
+    b = rnd(5000, torch.float32)
+    w = b.clone()
+    ex.start_([b], average=True).wait()
+    sch = Scheduler(ex, auto_order=True)
+    names = ["g%%d" %% i for i in range(4)]
+    bufs = [rnd(1000 + i, torch.float32) for i in range(4)]
+    keep = [t.clone() for t in bufs]
+    for step in range(2):
+        sch.begin_step(names)
+        for nm in names[::-1]:
+            sch.start(nm, bufs[names.index(nm)], average=True)
+        sch.wait_all()
+    torch.cuda.synchronize()
+    assert torch.equal(b, w) and all(torch.equal(a, c) for a, c in zip(bufs, keep))
+    ex.check()
+    ex.close()
+print("W1_RCCL_OK")
+"""
+
+
+@pytest.mark.gpu
+def test_world1_rccl_entry_points():
+    """A one-rank exchange forced through librccl's own entry points
+    (KUNGFU_AMD_EXCHANGE_W1_COLLECTIVES=1: reduce-scatter / all-to-all /
+    all-gather groups, the batched epilogue, the order broadcast) with the
+    exchange's exact arguments — C3's 64 grouped buckets, every RCCL dtype
+    and the all-to-all-only int16, in and out of place, SMA, the scheduler —
+    so the real RCCL calls run on a one-GPU box (two ranks on one device
+    are refused by RCCL; the multi-rank logic is the loopback tests')."""
+    import subprocess
+    import sys
+    _gpu()
+    env = dict(os.environ, KUNGFU_AMD_EXCHANGE_W1_COLLECTIVES="1")
+    r = subprocess.run([sys.executable, "-c", _W1_CHILD % os.path.dirname(HERE)], env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "W1_RCCL_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
