@@ -53,6 +53,7 @@ BUCKET_ELEMS = 64 << 20  # 256 MiB of fp32
 KF_FLOAT = 0x20408
 KF_SUM = 0
 REDUCE_KERNEL = "reduce_kernel<float, SUM, NONE, 2>"
+PIPE_GROUPS = 4  # kf_exchange_set_pipeline groups of the *_pipe sub-benchmarks
 
 
 def parse():
@@ -79,7 +80,7 @@ def parse():
                     help="rehearsal only: put every rank on this GPU")
     ap.add_argument("--no-extra", action="store_true",
                     help="N>1: skip the C4/C5/P2P sub-benchmarks")
-    ap.add_argument("--extras", default="c4,c5,c3_a2a,c3_fused,c3_torch_fused,c3_per_bucket,c4_torch,"
+    ap.add_argument("--extras", default="c4,c5,c5_pipe,c4_pipe,c3_pipe,c3_a2a,c3_fused,c3_torch_fused,c3_per_bucket,c4_torch,"
                                         "c5_torch,c3_ar,c3_p2p,c3_p2p_push,c3_p2p_hostbar,"
                                         "c4_p2p,c5_p2p",
                     help="N>1: which sub-benchmarks to run (comma list)")
@@ -670,6 +671,12 @@ def main():
         # the other multi-GPU configs of BASELINE.json, reported beside `value`
         extra = (("c4", lambda: bench_c4(world, rank, dev, steps_x, 5, exchange="native")),
                  ("c5", lambda: bench_c5(world, rank, dev, steps_x, 5, exchange="native")),
+                 ("c5_pipe", lambda: bench_c5(world, rank, dev, steps_x, 5,
+                                              exchange="native_pipe")),
+                 ("c4_pipe", lambda: bench_c4(world, rank, dev, steps_x, 5,
+                                              exchange="native_pipe")),
+                 ("c3_pipe", lambda: bench_c3_native(world, rank, dev, steps_x, 5, n, x, "rs",
+                                                     args.buckets, pipe=True)),
                  ("c3_a2a", lambda: bench_c3_native(world, rank, dev, steps_x, 5, n, x,
                                                     "a2a", args.buckets)),
                  ("c3_fused", lambda: bench_c3_native(world, rank, dev, steps_x, 5, n, x,
@@ -1057,27 +1064,30 @@ def _exchange(kind):
     if kind == "p2p":
         from kungfu_amd.p2p import PeerExchange
         return PeerExchange(timeout_s=5.0)
-    if kind == "native":
+    if kind in ("native", "native_pipe"):
         ex = _NATIVE.get("ex")
         if ex is None:
             raise RuntimeError("native exchange unavailable (see collective.native_exchange_error)")
-        return _AlgoView(ex, "auto")
+        return _AlgoView(ex, "auto", PIPE_GROUPS if kind == "native_pipe" else 1)
     from kungfu_amd.collective import Exchange
     return Exchange()
 
 
 class _AlgoView:
-    """The primary NativeExchange with another algo (one communicator)."""
+    """The primary NativeExchange with another algo and pipeline setting (one
+    communicator)."""
 
-    def __init__(self, ex, algo):
-        self.ex, self.algo, self.world = ex, algo, ex.world
+    def __init__(self, ex, algo, groups=1):
+        self.ex, self.algo, self.groups, self.world = ex, algo, groups, ex.world
 
     def _run(self, fn, *a, **kw):
         saved, self.ex.algo = self.ex.algo, self.algo
+        self.ex.set_pipeline(self.groups)
         try:
             return fn(*a, **kw)
         finally:
             self.ex.algo = saved
+            self.ex.set_pipeline(1)
 
     def all_reduce_(self, *a, **kw):
         return self._run(self.ex.all_reduce_, *a, **kw)
@@ -1086,7 +1096,7 @@ class _AlgoView:
         return self._run(self.ex.sma_, *a, **kw)
 
 
-def bench_c3_native(world, rank, dev, steps, warmup, n, x, algo, nb, fused=False):
+def bench_c3_native(world, rank, dev, steps, warmup, n, x, algo, nb, fused=False, pipe=False):
     """C3 through the native exchange with another algo or layout: "a2a" =
     RCCL all-to-all of every bucket's shards -> HIP rank-order fold (/np
     fused) -> RCCL all-gather, bit-exact against the local rank-order fold at
@@ -1094,7 +1104,7 @@ def bench_c3_native(world, rank, dev, steps, warmup, n, x, algo, nb, fused=False
     nccl_fusion, sync_sgd.py:87-92) instead of 64 grouped ones."""
     from kungfu_amd import ops
     from kungfu_amd.collective import GradBuckets
-    ex = _exchange("native")
+    ex = _exchange("native_pipe" if pipe else "native")
     ex.algo = algo
     gb = GradBuckets([n], torch.float32, dev, world, n_buckets=nb)
     gb.views[0].copy_(x)
@@ -1116,6 +1126,8 @@ def bench_c3_native(world, rank, dev, steps, warmup, n, x, algo, nb, fused=False
     busbw = 2 * (world - 1) / world * s_bytes / step_s / 1e9
     how = ("RCCL all-to-all -> HIP rank-order fold + /np -> RCCL all-gather" if algo == "a2a"
            else "RCCL reduce-scatter -> HIP /np -> RCCL all-gather")
+    if pipe:
+        how += ", pipelined in %d groups (HIP work on a second stream)" % PIPE_GROUPS
     return {"workload": "C3 via the native exchange, %s, algo %s (%s)" % (
                 "one fused 256 MiB bucket" if fused else "%d grouped buckets" % nb, algo, how),
             "ms_per_step": round(step_s * 1e3, 4),
@@ -1196,6 +1208,9 @@ def bench_c4(world, rank, dev, steps, warmup, exchange="native"):
     busbw = 2 * (world - 1) / world * s_bytes / step_s / 1e9
     how = {"native": "native C-ABI exchange: RCCL RS -> HIP /np -> RCCL AG, 16 buckets "
                      "in one call",
+           "native_pipe": "native C-ABI exchange: RCCL RS -> HIP /np -> RCCL AG, 16 buckets "
+                          "in one call pipelined in %d groups (HIP /np on a second stream "
+                          "between the groups' collectives)" % PIPE_GROUPS,
            "torch": "torch.distributed RCCL RS -> HIP /np -> RCCL AG",
            "p2p": "xGMI P2P pull: rank-order shard fold from peers' HBM + gather, "
                   "device barriers"}[exchange]
@@ -1335,6 +1350,10 @@ def bench_c5(world, rank, dev, steps, warmup, alpha=0.1, exchange="native"):
     busbw = 2 * (world - 1) / world * s_bytes / step_s / 1e9
     how = {"native": "native C-ABI exchange: RCCL all-to-all -> HIP rank-order bf16 fold "
                      "(fp32 accumulation) -> RCCL all-gather -> HIP blend, all buckets in one call",
+           "native_pipe": "native C-ABI exchange: RCCL all-to-all -> HIP rank-order bf16 fold "
+                          "(fp32 accumulation) -> RCCL all-gather -> HIP blend, all buckets in "
+                          "one call pipelined in %d groups (folds and blends on a second stream "
+                          "between the groups' collectives)" % PIPE_GROUPS,
            "torch": "torch.distributed all-to-all -> HIP rank-order fold -> all-gather -> "
                     "HIP blend, pipelined",
            "p2p": "xGMI P2P pull sum, device barriers -> HIP blend"}[exchange]

@@ -457,6 +457,14 @@ int kf_exchange_all_reduce_batch(kf_exchange_t *ex, const void *const *sends, vo
 int kf_exchange_sma_batch(kf_exchange_t *ex, void *const *vs, void *const *sums,
                           const size_t *counts, int nb, KungFu_Datatype dt, double alpha,
                           int algo, void *stream);
+/* Pipelined schedule for the batch calls (default 1 = off): the buckets of a
+ * call are split into `groups` groups of consecutive buckets of about equal
+ * bytes; the RCCL phases stay on the caller's stream in the same order on
+ * every rank (group g+1's reduce-scatter / all-to-all before group g's
+ * all-gather), and the element-wise work of group g (its shard epilogue or
+ * rank-order fold, and for SMA its blends) runs on the exchange's own stream
+ * meanwhile, ordered by events. Same results bit for bit. */
+int kf_exchange_set_pipeline(kf_exchange_t *ex, int groups);
 /* Ordered issue of concurrently produced all-reduces, the reference's
  * NCCLScheduler / LinearExecutor (srcs/cpp/src/nccl/scheduler.cpp:8-130):
  * begin_step fixes this step's names in an order every rank shares;

@@ -71,6 +71,7 @@ EXPORTED = (
     "kf_exchange_all_reduce",
     "kf_exchange_all_reduce_batch",
     "kf_exchange_sma_batch",
+    "kf_exchange_set_pipeline",
     "kf_exchange_begin_step",
     "kf_exchange_start",
     "kf_exchange_wait_all",
@@ -280,6 +281,8 @@ def load():
     lib.kf_exchange_wait_all.restype = c_int
     lib.kf_exchange_check.argtypes = [c_void_p]
     lib.kf_exchange_check.restype = c_int
+    lib.kf_exchange_set_pipeline.argtypes = [c_void_p, c_int]
+    lib.kf_exchange_set_pipeline.restype = c_int
     lib.kf_exchange_info.argtypes = [c_void_p, P(c_int), P(c_int), P(c_int)]
     lib.kf_exchange_info.restype = c_int
     lib.kf_exchange_destroy.argtypes = [c_void_p]

@@ -30,6 +30,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
@@ -456,6 +457,14 @@ struct kf_exchange {
     bool ws_used        = false;
     hipStream_t own     = nullptr;  // internal (order broadcast)
 
+    // pipelined schedule (kf_exchange_set_pipeline): the buckets of a call in
+    // `groups` groups; RCCL phases on the caller's stream, the element-wise
+    // work (folds, /np, SMA blends) on `comp`, so group g's HIP work runs
+    // while group g+1's collectives move bytes
+    int groups         = 1;
+    hipStream_t comp   = nullptr;
+    std::vector<hipEvent_t> pev;  // 3 per group
+
     // NCCLScheduler / LinearExecutor
     std::mutex smu;
     std::condition_variable scv;
@@ -472,8 +481,11 @@ struct kf_exchange {
 
     int ensure_ws(size_t bytes, hipStream_t s);
     void release_ws(hipStream_t s);
+    // sma_alpha != nullptr: SMA, sends = the variables, recvs = the sum workspaces,
+    // each variable blended once its sum is gathered
     int batch(const void *const *sends, void *const *recvs, const size_t *counts, int nb,
-              KungFu_Datatype dt, KungFu_Op op, int average, int algo, hipStream_t s);
+              KungFu_Datatype dt, KungFu_Op op, int average, int algo, hipStream_t s,
+              const double *sma_alpha = nullptr);
     void issue_loop();
     void complete_loop();
     ~kf_exchange();
@@ -536,16 +548,22 @@ static int resolve_algo(int algo, KungFu_Datatype dt, KungFu_Op op, int world, i
 
 int kf_exchange::batch(const void *const *sends, void *const *recvs, const size_t *counts,
                        int nb, KungFu_Datatype dt, KungFu_Op op, int average, int algo,
-                       hipStream_t s)
+                       hipStream_t s, const double *sma_alpha)
 {
     const Rccl &R = *this->R;
     const int sz  = tsize(dt);
     const int W = world, r = rank;
+    const bool sma = sma_alpha != nullptr;
     if (W == 1 && !w1_collectives()) {  // a single peer: the sum is the bucket, x / 1 == x
         for (int b = 0; b < nb; ++b) {
             if (counts[b] && sends[b] != recvs[b]) {
                 KF_HIP(hipMemcpyAsync(recvs[b], sends[b], counts[b] * sz, hipMemcpyDeviceToDevice, s));
             }
+        }
+        for (int b = 0; sma && b < nb; ++b) {
+            const int rc = kf_sma_blend(const_cast<void *>(sends[b]), recvs[b], counts[b], dt, W,
+                                        *sma_alpha, s);
+            if (rc != KF_OK) return fail(rc, "kf_sma_blend");
         }
         return KF_OK;
     }
@@ -583,79 +601,160 @@ int kf_exchange::batch(const void *const *sends, void *const *recvs, const size_
     };
 
     // phase 1: every bucket's reduce-scatter (or all-to-all) and tail gather
-    KF_NCCL(R.GroupStart());
-    rc = KF_OK;
-    for (int b = 0; b < nb && rc == KF_OK; ++b) {
-        const size_t q = counts[b] / W, t = counts[b] % W;
-        const char *snd = static_cast<const char *>(sends[b]);
-        char *rcv       = static_cast<char *>(recvs[b]);
-        ncclResult_t e  = ncclSuccess;
-        if (q && a == KF_ALGO_REDUCE_SCATTER) {
-            e = R.ReduceScatter(snd, rcv + r * q * sz, q, nt, nccl_op(op), comm, s);
-        } else if (q) {
-            e = R.AllToAll(snd, wsp + wsoff[b], q * sz, ncclUint8, comm, s);
+    auto phase1 = [&](int b0, int b1) -> int {
+        KF_NCCL(R.GroupStart());
+        int rc1 = KF_OK;
+        for (int b = b0; b < b1 && rc1 == KF_OK; ++b) {
+            const size_t q = counts[b] / W, t = counts[b] % W;
+            const char *snd = static_cast<const char *>(sends[b]);
+            char *rcv       = static_cast<char *>(recvs[b]);
+            ncclResult_t e  = ncclSuccess;
+            if (q && a == KF_ALGO_REDUCE_SCATTER) {
+                e = R.ReduceScatter(snd, rcv + r * q * sz, q, nt, nccl_op(op), comm, s);
+            } else if (q) {
+                e = R.AllToAll(snd, wsp + wsoff[b], q * sz, ncclUint8, comm, s);
+            }
+            if (e == ncclSuccess && t) {
+                e = R.AllGather(snd + q * W * sz, wsp + toff[b], t * sz, ncclUint8, comm, s);
+            }
+            if (e != ncclSuccess) rc1 = nccl_fail(e, "phase-1 collective");
         }
-        if (e == ncclSuccess && t) {
-            e = R.AllGather(snd + q * W * sz, wsp + toff[b], t * sz, ncclUint8, comm, s);
-        }
-        if (e != ncclSuccess) rc = nccl_fail(e, "phase-1 collective");
-    }
-    rc = group_end(rc);
-    if (rc != KF_OK) return rc;
+        return group_end(rc1);
+    };
 
     // phase 2: the element-wise work, batched over the buckets
-    std::vector<const void *> ins;
-    std::vector<void *> outs;
-    std::vector<size_t> cnts;
-    if (a == KF_ALGO_REDUCE_SCATTER && average) {
-        for (int b = 0; b < nb; ++b) {
-            const size_t q = counts[b] / W;
-            if (!q) continue;
-            char *sh = static_cast<char *>(recvs[b]) + r * q * sz;
-            ins.push_back(sh);
-            outs.push_back(sh);
-            cnts.push_back(q);
+    auto phase2 = [&](int b0, int b1, hipStream_t cs) -> int {
+        std::vector<const void *> ins;
+        std::vector<void *> outs;
+        std::vector<size_t> cnts;
+        if (a == KF_ALGO_REDUCE_SCATTER && average) {
+            for (int b = b0; b < b1; ++b) {
+                const size_t q = counts[b] / W;
+                if (!q) continue;
+                char *sh = static_cast<char *>(recvs[b]) + r * q * sz;
+                ins.push_back(sh);
+                outs.push_back(sh);
+                cnts.push_back(q);
+            }
+            if (!outs.empty()) {
+                const int e = kf_bucket_reduce_batch(ins.data(), 1, outs.data(), cnts.data(),
+                                                     static_cast<int>(outs.size()), dt, KungFu_SUM,
+                                                     W, cs);
+                if (e != KF_OK) return fail(e, "shard /np epilogue");
+            }
+            ins.clear();
+            outs.clear();
+            cnts.clear();
+        }
+        for (int b = b0; b < b1; ++b) {  // rank-order folds: shards and tails
+            const size_t q = counts[b] / W, t = counts[b] % W;
+            char *rcv      = static_cast<char *>(recvs[b]);
+            if (q && a == KF_ALGO_ALL_TO_ALL) {
+                for (int j = 0; j < W; ++j) ins.push_back(wsp + wsoff[b] + j * q * sz);
+                outs.push_back(rcv + r * q * sz);
+                cnts.push_back(q);
+            }
+            if (t) {
+                for (int j = 0; j < W; ++j) ins.push_back(wsp + toff[b] + j * t * sz);
+                outs.push_back(rcv + q * W * sz);
+                cnts.push_back(t);
+            }
         }
         if (!outs.empty()) {
-            rc = kf_bucket_reduce_batch(ins.data(), 1, outs.data(), cnts.data(),
-                                        static_cast<int>(outs.size()), dt, KungFu_SUM, W, s);
-            if (rc != KF_OK) return fail(rc, "shard /np epilogue");
+            const int e = kf_bucket_reduce_batch(ins.data(), W, outs.data(), cnts.data(),
+                                                 static_cast<int>(outs.size()), dt, op,
+                                                 average ? W : 0, cs);
+            if (e != KF_OK) return fail(e, "rank-order fold of the received shards");
         }
-        ins.clear();
-        outs.clear();
-        cnts.clear();
-    }
-    for (int b = 0; b < nb; ++b) {  // rank-order folds: shards and tails
-        const size_t q = counts[b] / W, t = counts[b] % W;
-        char *rcv      = static_cast<char *>(recvs[b]);
-        if (q && a == KF_ALGO_ALL_TO_ALL) {
-            for (int j = 0; j < W; ++j) ins.push_back(wsp + wsoff[b] + j * q * sz);
-            outs.push_back(rcv + r * q * sz);
-            cnts.push_back(q);
-        }
-        if (t) {
-            for (int j = 0; j < W; ++j) ins.push_back(wsp + toff[b] + j * t * sz);
-            outs.push_back(rcv + q * W * sz);
-            cnts.push_back(t);
-        }
-    }
-    if (!outs.empty()) {
-        rc = kf_bucket_reduce_batch(ins.data(), W, outs.data(), cnts.data(),
-                                    static_cast<int>(outs.size()), dt, op, average ? W : 0, s);
-        if (rc != KF_OK) return fail(rc, "rank-order fold of the received shards");
-    }
+        return KF_OK;
+    };
 
     // phase 3: in-place all-gather of every reduced shard
-    KF_NCCL(R.GroupStart());
-    rc = KF_OK;
-    for (int b = 0; b < nb && rc == KF_OK; ++b) {
-        const size_t q = counts[b] / W;
-        if (!q) continue;
-        char *rcv      = static_cast<char *>(recvs[b]);
-        ncclResult_t e = R.AllGather(rcv + r * q * sz, rcv, q * sz, ncclUint8, comm, s);
-        if (e != ncclSuccess) rc = nccl_fail(e, "ncclAllGather");
+    auto phase3 = [&](int b0, int b1) -> int {
+        KF_NCCL(R.GroupStart());
+        int rc3 = KF_OK;
+        for (int b = b0; b < b1 && rc3 == KF_OK; ++b) {
+            const size_t q = counts[b] / W;
+            if (!q) continue;
+            char *rcv      = static_cast<char *>(recvs[b]);
+            ncclResult_t e = R.AllGather(rcv + r * q * sz, rcv, q * sz, ncclUint8, comm, s);
+            if (e != ncclSuccess) rc3 = nccl_fail(e, "ncclAllGather");
+        }
+        return group_end(rc3);
+    };
+
+    // SMA: v = (1 - alpha) v + alpha (sum / world), once the sum is gathered
+    auto blend = [&](int b0, int b1, hipStream_t cs) -> int {
+        for (int b = b0; sma && b < b1; ++b) {
+            const int e = kf_sma_blend(const_cast<void *>(sends[b]), recvs[b], counts[b], dt, W,
+                                       *sma_alpha, cs);
+            if (e != KF_OK) return fail(e, "kf_sma_blend");
+        }
+        return KF_OK;
+    };
+
+    const int G = std::min(groups, nb);
+    if (G <= 1) {
+        rc = phase1(0, nb);
+        if (rc == KF_OK) rc = phase2(0, nb, s);
+        if (rc == KF_OK) rc = phase3(0, nb);
+        if (rc == KF_OK) rc = blend(0, nb, s);
+        if (rc != KF_OK) return rc;
+        if (need) release_ws(s);
+        return KF_OK;
     }
-    rc = group_end(rc);
+
+    // pipelined: groups of consecutive buckets with about equal bytes;
+    //   caller stream s: p1(0) p1(1) [wait p2(0)] p3(0) p1(2) [wait p2(1)] p3(1) ...
+    //   comp stream:     [wait p1(0)] p2(0) [wait p1(1)] p2(1) [wait p3(0)] blend(0) ...
+    // every wait is on an event recorded earlier on the other stream, so
+    // neither stream can wait on the other in a cycle; the RCCL calls keep the
+    // same order on every rank
+    std::vector<int> gb(1, 0);  // group g = buckets [gb[g], gb[g+1])
+    {
+        size_t total = 0, acc = 0;
+        for (int b = 0; b < nb; ++b) total += counts[b];
+        for (int b = 0; b < nb; ++b) {
+            acc += counts[b];
+            const int left = nb - b - 1, want = G - static_cast<int>(gb.size());
+            if (want > 0 && left >= want && acc * G >= total * gb.size()) gb.push_back(b + 1);
+        }
+        gb.push_back(nb);
+    }
+    const int ng = static_cast<int>(gb.size()) - 1;
+    if (!comp) KF_HIP(hipStreamCreateWithFlags(&comp, hipStreamNonBlocking));
+    while (pev.size() < static_cast<size_t>(3 * ng + 1)) {
+        hipEvent_t e;
+        KF_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        pev.push_back(e);
+    }
+    auto e1 = [&](int g) { return pev[3 * g]; };
+    auto e2 = [&](int g) { return pev[3 * g + 1]; };
+    auto e3 = [&](int g) { return pev[3 * g + 2]; };
+    hipEvent_t e_end = pev[3 * ng];
+    auto finish = [&](int g) -> int {  // gather group g, then blend it
+        KF_HIP(hipStreamWaitEvent(s, e2(g), 0));
+        int f = phase3(gb[g], gb[g + 1]);
+        if (f != KF_OK || !sma) return f;
+        KF_HIP(hipEventRecord(e3(g), s));
+        KF_HIP(hipStreamWaitEvent(comp, e3(g), 0));
+        return blend(gb[g], gb[g + 1], comp);
+    };
+    for (int g = 0; g < ng && rc == KF_OK; ++g) {
+        rc = phase1(gb[g], gb[g + 1]);
+        if (rc != KF_OK) break;
+        KF_HIP(hipEventRecord(e1(g), s));
+        KF_HIP(hipStreamWaitEvent(comp, e1(g), 0));
+        rc = phase2(gb[g], gb[g + 1], comp);
+        if (rc != KF_OK) break;
+        KF_HIP(hipEventRecord(e2(g), comp));
+        if (g > 0) rc = finish(g - 1);
+    }
+    if (rc == KF_OK) rc = finish(ng - 1);
+    if (rc == KF_OK && sma) {  // the caller's stream ends after the last blend
+        KF_HIP(hipEventRecord(e_end, comp));
+        KF_HIP(hipStreamWaitEvent(s, e_end, 0));
+    }
     if (rc != KF_OK) return rc;
     if (need) release_ws(s);
     return KF_OK;
@@ -747,6 +846,8 @@ kf_exchange::~kf_exchange()
     if (ws) (void)hipFree(ws);
     if (ws_ev) (void)hipEventDestroy(ws_ev);
     if (own) (void)hipStreamDestroy(own);
+    if (comp) (void)hipStreamDestroy(comp);
+    for (auto e : pev) (void)hipEventDestroy(e);
 }
 
 extern "C" {
@@ -888,12 +989,14 @@ int kf_exchange_sma_batch(kf_exchange_t *ex, void *const *vs, void *const *sums,
     std::lock_guard<std::mutex> lk(ex->mu);
     hipStream_t s = static_cast<hipStream_t>(stream);
     std::vector<const void *> snd(vs, vs + nb);
-    rc = ex->batch(snd.data(), sums, counts, nb, dt, KungFu_SUM, 0, algo, s);
-    if (rc != KF_OK) return rc;
-    for (int b = 0; b < nb; ++b) {
-        rc = kf_sma_blend(vs[b], sums[b], counts[b], dt, ex->world, alpha, stream);
-        if (rc != KF_OK) return fail(rc, "kf_sma_blend");
-    }
+    return ex->batch(snd.data(), sums, counts, nb, dt, KungFu_SUM, 0, algo, s, &alpha);
+}
+
+int kf_exchange_set_pipeline(kf_exchange_t *ex, int groups)
+{
+    if (!ex || groups < 1) return fail(KF_ERR_ARG, "kf_exchange_set_pipeline: groups >= 1");
+    std::lock_guard<std::mutex> lk(ex->mu);
+    ex->groups = groups;
     return KF_OK;
 }
 

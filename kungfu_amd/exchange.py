@@ -94,6 +94,15 @@ class NativeExchange:
         self._h, self._side, self._sums = h, None, {}
         return self
 
+    def set_pipeline(self, groups):
+        """kf_exchange_set_pipeline: split every batch call into `groups`
+        groups of buckets whose HIP work (folds, /np, SMA blends) overlaps the
+        next group's RCCL phases (1 = off, the default). Same bits."""
+        _lib.check(self.lib.kf_exchange_set_pipeline(self._h, int(groups)),
+                   "kf_exchange_set_pipeline")
+        self.groups = int(groups)
+        return self
+
     # -- the optimizers' interface (collective.Exchange) --------------------
     def _check(self, buckets):
         for b in buckets:

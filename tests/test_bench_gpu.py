@@ -43,3 +43,48 @@ def test_bench_n2_rehearsal_with_p2p_children():
         assert "error" not in d[k], d[k]
         assert d[k]["ms_per_step"] > 0
     assert d["p2p_children"]["all_ok"] is True
+
+
+_NATIVE_CHILD = r"""
+import os, sys
+sys.path.insert(0, %r)
+import torch
+import torch.distributed as dist
+import bench
+from kungfu_amd.exchange import NativeExchange
+dev = torch.device("cuda:0")
+torch.cuda.set_device(0)
+dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+bench._NATIVE["ex"] = NativeExchange(algo="rs", device=dev)
+n = 16 << 20
+x = torch.randn(n, device=dev, generator=torch.Generator(device=dev).manual_seed(0))
+res = {
+    "c4": bench.bench_c4(1, 0, dev, 3, 1, exchange="native"),
+    "c4_pipe": bench.bench_c4(1, 0, dev, 3, 1, exchange="native_pipe"),
+    "c5": bench.bench_c5(1, 0, dev, 3, 1, exchange="native"),
+    "c5_pipe": bench.bench_c5(1, 0, dev, 3, 1, exchange="native_pipe"),
+    "c3_a2a": bench.bench_c3_native(1, 0, dev, 3, 1, n, x, "a2a", 64),
+    "c3_fused": bench.bench_c3_native(1, 0, dev, 3, 1, n, x, "rs", 64, fused=True),
+    "c3_pipe": bench.bench_c3_native(1, 0, dev, 3, 1, n, x, "rs", 64, pipe=True),
+}
+bad = {k: v for k, v in res.items() if "error" in v or not v.get("ms_per_step", 0) > 0}
+bench._NATIVE.pop("ex").close()
+dist.destroy_process_group()
+print("NATIVE_SUB_OK" if not bad else "NATIVE_SUB_BAD %%r" %% bad)
+"""
+
+
+def test_bench_native_subbenchmarks_world1_rccl():
+    """bench.py's native sub-benchmark bodies (c4, c5, c3_a2a, c3_fused and the
+    pipelined c3/c4/c5) run end to end — parity check, timed loop — over a
+    one-rank RCCL communicator forced through librccl's collectives
+    (KUNGFU_AMD_EXCHANGE_W1_COLLECTIVES=1), so the code the driver's multi-GPU
+    node runs first has run on real RCCL here."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    env = dict(os.environ, KUNGFU_AMD_EXCHANGE_W1_COLLECTIVES="1", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(_port()))
+    r = subprocess.run([sys.executable, "-c", _NATIVE_CHILD % ROOT], env=env, capture_output=True,
+                       text=True, timeout=240, cwd=ROOT)
+    assert r.returncode == 0 and "NATIVE_SUB_OK" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]

@@ -249,19 +249,23 @@ def _loop_ranks(world, body):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 3, 4, 8])
-def test_exchange_multi_rank_loopback(world):
+@pytest.mark.parametrize("world,groups", [(2, 1), (3, 1), (4, 1), (8, 1), (2, 3), (3, 2),
+                                          (8, 4)])
+def test_exchange_multi_rank_loopback(world, groups):
     """The N > 1 code of kf_exchange (shards, tails of count % world, the
     workspace, batched folds, in-place all-gather, SMA) at worlds 2-8 on one
     GPU: the loopback transport moves the bytes where RCCL would, its
     reduce-scatter folds in rank order, so every algo is bit-exact against the
-    oracle's rank-order fold."""
+    oracle's rank-order fold. groups > 1: the pipelined schedule
+    (kf_exchange_set_pipeline), whose folds and blends run on the exchange's
+    own stream between the groups' collectives — the same bits."""
     import torch
     from oracle import oracle
     dev = _gpu()
     counts = [1, 7, world * 1000 + 3, 262147, world * 4096]
 
     def body(rank, ex):
+        ex.set_pipeline(groups)
         for algo in ("rs", "a2a", "auto"):
             for name, avg in (("f32", True), ("bf16", True), ("f16", False), ("i32", False)):
                 if algo == "rs" and name in ("bf16", "f16"):
@@ -307,14 +311,18 @@ def test_exchange_multi_rank_loopback(world):
         torch.cuda.synchronize()
         assert np.array_equal(_to_np(x, "f32"), xs[rank])
         assert np.array_equal(_to_np(y, "f32"), oracle.reduce_avg(xs, "f32", world))
-        # SMA, bf16 (auto: the all-to-all fold, fp32 accumulation)
-        vs = [_rand("bf16", 20000 + 3, 300 + r) for r in range(world)]
-        v = _to_dev(vs[rank], "bf16", dev)
-        ex.sma_([v], 0.1)
-        torch.cuda.synchronize()
-        s = oracle.reduce_k(vs, "bf16", "sum")
-        assert np.array_equal(_to_np(v, "bf16"),
-                              oracle.sma_blend(vs[rank], s, "bf16", world, 0.1))
+        # SMA, bf16 (auto: the all-to-all fold, fp32 accumulation), one and
+        # five buckets (the pipelined schedule blends group by group)
+        for sizes in ([20003], [20003, 5, world * 777, 65536 + 1, 3]):
+            vs = [[_rand("bf16", n, 300 + 10 * r + j) for j, n in enumerate(sizes)]
+                  for r in range(world)]
+            v = [_to_dev(vs[rank][j], "bf16", dev) for j in range(len(sizes))]
+            ex.sma_(v, 0.1)
+            torch.cuda.synchronize()
+            for j in range(len(sizes)):
+                s = oracle.reduce_k([vs[r][j] for r in range(world)], "bf16", "sum")
+                assert np.array_equal(_to_np(v[j], "bf16"),
+                                      oracle.sma_blend(vs[rank][j], s, "bf16", world, 0.1)), j
 
     _loop_ranks(world, body)
 
@@ -495,15 +503,15 @@ def test_native_exchange_configs_full_size():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg", ["c4", "c5"])
-def test_native_exchange_configs_world8(cfg):
+@pytest.mark.parametrize("cfg,groups", [("c4", 1), ("c5", 1), ("c4", 4), ("c5", 4)])
+def test_native_exchange_configs_world8(cfg, groups):
     """C4 and C5 at the world size BASELINE names for them (8 GPUs), full size,
     through the native exchange over the loopback transport: C4 = ResNet-50's
     25,583,592 fp32 in 16 buckets, S-SGD /np, both algos (auto -> RCCL-shaped
     reduce-scatter, a2a -> rank-order fold); C5 = BERT-base's first 201 tensors
     (109,483,778 bf16), SMA alpha 0.1 (auto -> a2a). The oracle's rank-order
     fold of all 8 ranks is computed once; every rank's buckets must equal it
-    bit for bit."""
+    bit for bit, with the pipelined schedule (groups = 4) as without it."""
     import json
     import torch
     from kungfu_amd.collective import GradBuckets
@@ -530,6 +538,7 @@ def test_native_exchange_configs_world8(cfg):
         for algo in ("auto", "a2a"):
             def body(rank, ex, algo=algo):
                 ex.algo = algo
+                ex.set_pipeline(groups)
                 mine = mk[rank]()
                 ex.all_reduce_(mine.buckets, average=True, coalesce=False)
                 torch.cuda.synchronize()
@@ -551,6 +560,7 @@ def test_native_exchange_configs_world8(cfg):
 
         def body(rank, ex):
             ex.algo = "auto"
+            ex.set_pipeline(groups)
             mine = mk[rank]()
             ex.sma_(mine.buckets, 0.1)
             torch.cuda.synchronize()
@@ -590,6 +600,20 @@ for algo in ("rs", "a2a", "auto"):
     ex.all_reduce_(gb.buckets, average=True, coalesce=False)
     torch.cuda.synchronize()
     assert torch.equal(gb.views[0], want), (algo, "c3")
+    ex.set_pipeline(4)  # the pipelined schedule: a second stream, events per group
+    ex.all_reduce_(gb.buckets, average=True, coalesce=False)
+    torch.cuda.synchronize()
+    assert torch.equal(gb.views[0], want), (algo, "c3 pipelined")
+    vs = [rnd(n, torch.bfloat16) for n in (30001, 1 << 18, 5, 4097)]
+    v0 = [v.clone() for v in vs]
+    ex.sma_(vs, 0.1)
+    torch.cuda.synchronize()
+    for v, a in zip(vs, v0):
+        want_b = oracle.sma_blend(a.cpu().view(torch.int16).numpy().view(np.uint16),
+                                  a.cpu().view(torch.int16).numpy().view(np.uint16),
+                                  "bf16", 1, 0.1)
+        assert np.array_equal(v.cpu().view(torch.int16).numpy().view(np.uint16), want_b), algo
+    ex.set_pipeline(1)
     cases = [(torch.bfloat16, "sum", True), (torch.float16, "sum", False),
              (torch.int32, "max", False), (torch.int64, "sum", False),
              (torch.uint8, "sum", False), (torch.float64, "sum", True),
