@@ -53,6 +53,7 @@ BUCKET_ELEMS = 64 << 20  # 256 MiB of fp32
 KF_FLOAT = 0x20408
 KF_SUM = 0
 REDUCE_KERNEL = "reduce_kernel<float, SUM, NONE, 2>"
+XGMI_LINK_GBPS = 153.0  # per link per direction
 PIPE_GROUPS = 4  # kf_exchange_set_pipeline groups of the *_pipe sub-benchmarks
 
 
@@ -653,8 +654,8 @@ def main():
         out["collective"] = {
             "busbw_GBps": round(busbw, 2),
             "algbw_GiBps_per_gpu": round(s_bytes / step_s / 2**30, 3),
-            "xgmi_bound_GBps": round(153.0 * (world - 1), 1),
-            "frac_of_xgmi": round(busbw / (153.0 * (world - 1)), 4),
+            "xgmi_bound_GBps": round(XGMI_LINK_GBPS * (world - 1), 1),
+            "frac_of_xgmi": _xgmi_frac(busbw, world),
             "buckets": args.buckets,
             "exchange": how,
         }
@@ -845,6 +846,12 @@ def _within(got, want, absum, world):
     u = 2.0 ** -24
     bound = 2 * (world - 1) * u * absum / world + 2 * u * want.abs() + 1e-38
     return bool(((got - want).abs() <= bound * 1.0001).all())
+
+
+def _xgmi_frac(busbw, world):
+    """busbw against the xGMI bound: one 153 GB/s link per peer (world - 1
+    links per GPU on a fully connected node); None for a single rank."""
+    return round(busbw / (XGMI_LINK_GBPS * (world - 1)), 4) if world > 1 else None
 
 
 def _agree(ok, dev):
@@ -1133,7 +1140,7 @@ def bench_c3_native(world, rank, dev, steps, warmup, n, x, algo, nb, fused=False
             "ms_per_step": round(step_s * 1e3, 4),
             "GiBps_per_gpu": round(s_bytes / step_s / 2**30, 3),
             "busbw_GBps": round(busbw, 2),
-            "frac_of_xgmi": round(busbw / (153.0 * (world - 1)), 4),
+            "frac_of_xgmi": _xgmi_frac(busbw, world),
             "parity": ("bit-exact vs the rank-order fold (every N)" if algo == "a2a" else
                        "N=2 bit-exact, N>2 within the order bound")}
 
@@ -1219,7 +1226,7 @@ def bench_c4(world, rank, dev, steps, warmup, exchange="native"):
             "bytes": s_bytes, "ms_per_step": round(step_s * 1e3, 4),
             "GiBps_per_gpu": round(s_bytes / step_s / 2**30, 3),
             "busbw_GBps": round(busbw, 2),
-            "frac_of_xgmi": round(busbw / (153.0 * (world - 1)), 4)}
+            "frac_of_xgmi": _xgmi_frac(busbw, world)}
 
 
 def bench_c3_ar(world, rank, dev, steps, warmup, n, x):
@@ -1253,7 +1260,7 @@ def bench_c3_ar(world, rank, dev, steps, warmup, n, x):
             "ms_per_step": round(step_s * 1e3, 4),
             "GiBps_per_gpu": round(s_bytes / step_s / 2**30, 3),
             "busbw_GBps": round(busbw, 2),
-            "frac_of_xgmi": round(busbw / (153.0 * (world - 1)), 4)}
+            "frac_of_xgmi": _xgmi_frac(busbw, world)}
 
 
 def bench_c3_p2p(world, rank, dev, steps, warmup, n, x, mode="pull", barrier="device"):
@@ -1310,7 +1317,7 @@ def bench_c3_p2p(world, rank, dev, steps, warmup, n, x, mode="pull", barrier="de
             "ms_per_step": round(step_s * 1e3, 4),
             "GiBps_per_gpu": round(s_bytes / step_s / 2**30, 3),
             "busbw_GBps": round(busbw, 2),
-            "frac_of_xgmi": round(busbw / (153.0 * (world - 1)), 4),
+            "frac_of_xgmi": _xgmi_frac(busbw, world),
             "parity": "bit-exact vs rank-order fold before timing: yes; after timing, "
                       "two fresh inputs: %s" % ("yes" if after else "NO")}
 
@@ -1362,7 +1369,7 @@ def bench_c5(world, rank, dev, steps, warmup, alpha=0.1, exchange="native"):
             "bytes": s_bytes, "ms_per_step": round(step_s * 1e3, 4),
             "GiBps_per_gpu": round(s_bytes / step_s / 2**30, 3),
             "busbw_GBps": round(busbw, 2),
-            "frac_of_xgmi": round(busbw / (153.0 * (world - 1)), 4),
+            "frac_of_xgmi": _xgmi_frac(busbw, world),
             "parity": "bf16 unpinned (DESIGN.md); bit-exact vs the local rank-order fold "
                       "+ blend"}
 
