@@ -105,6 +105,9 @@ def parse():
     ap.add_argument("--p2p-child", default="", help=argparse.SUPPRESS)
     ap.add_argument("--p2p-out", default="", help=argparse.SUPPRESS)
     ap.add_argument("--p2p-timeout", type=float, default=150.0, help=argparse.SUPPRESS)
+    ap.add_argument("--rehearse-exchange", action="store_true",
+                    help="testing: run the N > 1 branch (native exchange over RCCL, "
+                         "sub-benchmarks, line) with a single rank")
     ap.add_argument("--profile-only", action="store_true",
                     help="only the timed kernel loop (for rocprofv3 runs)")
     return ap.parse_args()
@@ -555,7 +558,8 @@ def main():
     dev_index = local_rank if args.device_index is None else args.device_index
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
-    if world > 1:
+    multi = world > 1 or args.rehearse_exchange
+    if multi:
         if args.dist_backend == "nccl":
             _quiet(dist.init_process_group, "nccl", device_id=dev)
         else:
@@ -588,7 +592,7 @@ def main():
     hot_s, _, _ = time_local_reduce(lib, sets[:1], args.steps, args.warmup, world)
 
     out = {}
-    if world == 1:
+    if not multi:
         step_s = wall_local / args.steps
         value = s_bytes / kernel_s / 2**30
         # parity check of every timed output (full oracle check: tests/)
@@ -622,7 +626,7 @@ def main():
             try:
                 prim_ex.all_reduce_(pieces, average=True, coalesce=coalesce)
                 got = gb.views[0]
-                ok = (bool(torch.equal(got, want)) if world == 2 else
+                ok = (bool(torch.equal(got, want)) if world <= 2 else
                       _within(got, want, absum, world))
             except Exception as e:
                 print("[bench] rank %d: primary exchange failed: %r" % (rank, e), file=sys.stderr,
@@ -737,7 +741,7 @@ def main():
                   dict(value=value, step_s=step_s, kernel_s=kernel_s, workload=workload,
                        parallelism=parallelism))
     res.update(out)
-    if rank == 0 and world == 1:
+    if rank == 0 and not multi:
         if not args.no_kernels:
             _progress(rank, "kernel families")
             try:
@@ -756,7 +760,7 @@ def main():
                 res["c1"] = {"error": repr(e)[:300]}
     if rank == 0:
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if multi:
         dist.barrier()
         dist.destroy_process_group()
 

@@ -88,3 +88,29 @@ def test_bench_native_subbenchmarks_world1_rccl():
     r = subprocess.run([sys.executable, "-c", _NATIVE_CHILD % ROOT], env=env, capture_output=True,
                        text=True, timeout=240, cwd=ROOT)
     assert r.returncode == 0 and "NATIVE_SUB_OK" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]
+
+
+def test_bench_exchange_branch_single_rank_rccl():
+    """bench.py's whole N > 1 branch — shared id, the native exchange as the
+    primary (RCCL), its parity check, the timed C3 step, the agreed
+    sub-benchmark loop and the JSON line — run by one rank on real RCCL
+    (--rehearse-exchange, the one-rank communicator forced through librccl's
+    collectives): the primary must be the native exchange, not the fallback."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    env = dict(os.environ, KUNGFU_AMD_EXCHANGE_W1_COLLECTIVES="1", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(_port()), RANK="0", LOCAL_RANK="0", WORLD_SIZE="1")
+    extras = "c4,c5,c5_pipe,c4_pipe,c3_pipe,c3_a2a,c3_fused,c4_torch,c5_torch"
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--rehearse-exchange", "--steps", "3",
+           "--warmup", "1", "--elems", str(4 << 20), "--extras", extras,
+           "--extras-timeout", "200"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=260, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["value"] > 0 and d["collective"]["exchange"].startswith("native"), d["collective"]
+    assert "native_exchange_error" not in d["collective"], d["collective"]
+    for k in extras.split(","):
+        assert "error" not in d[k] and d[k]["ms_per_step"] > 0, (k, d[k])
