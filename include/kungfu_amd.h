@@ -183,6 +183,12 @@ int kf_host_unregister(void *p);
  * 2-input path — unroll in {1,2,4,8} vectors per thread, grid cap in blocks,
  * non-temporal loads, plain stores. Not thread-safe; call before launching. */
 int kf_set_geometry(int unroll, int grid_cap, int loadnt, int stplain);
+/* Tuning hook (A/B tools only): occupancy cap of the HBM streaming kernels
+ * (kf_bucket_reduce*, kf_bucket_div, kf_sma_blend; not the batched launch), as
+ * dynamic LDS bytes per 256-thread block (0 = none, at most 64 KiB) for the
+ * k <= 2 kernels (two-input sum, /np, SMA) and for the k >= 3 folds.
+ * Defaults: 0 and 48 KiB (three blocks per CU). Not thread-safe. */
+int kf_set_occupancy(int lds_small, int lds_fold);
 
 /* Host-pointer reduce with a status code instead of exit(): the path
  * std_transform_2 takes. Synchronous, per-thread stream and device scratch.

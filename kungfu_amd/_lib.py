@@ -70,6 +70,7 @@ EXPORTED = (
     "kf_exchange_create_session",
     "kf_exchange_all_reduce",
     "kf_exchange_all_reduce_batch",
+    "kf_set_occupancy",
     "kf_exchange_sma_batch",
     "kf_exchange_set_pipeline",
     "kf_exchange_begin_step",
@@ -156,6 +157,8 @@ def load():
                                        c_int, c_int]
     lib.kf_transform2_host.restype = c_int
     lib.kf_set_geometry.argtypes = [c_int, c_int, c_int, c_int]
+    lib.kf_set_occupancy.argtypes = [c_int, c_int]
+    lib.kf_set_occupancy.restype = c_int
     lib.kf_set_geometry.restype = c_int
     lib.kf_host_register.argtypes = [c_void_p, c_size_t]
     lib.kf_host_register.restype = c_int

@@ -42,6 +42,20 @@ struct Geometry {
     int grid_cap = 1 << 20;  // blocks; grid-stride beyond (8 GiB fp32 buckets)
     int loadnt   = 1;        // non-temporal read streams
     int stplain  = 0;        // plain (not non-temporal) stores
+    // Occupancy cap of reduce_kernel, as dynamic LDS per block the kernel
+    // never touches (160 KiB per CU / bytes = resident blocks per CU). Three
+    // 256-thread blocks per CU instead of eight narrows the window of every
+    // stream that is open at once, and the k-input fold gains: in one process
+    // on the same buffers k = 3/4/6/8 0.806/0.808/0.800/0.790 of 8 TB/s against
+    // 0.795/0.790/0.765/0.748 uncapped (tools/explore/kfold_occ.hip), in the
+    // product k = 3/4/8 +1.0/+2.1/+1.8 % (tools/ab_occupancy.py); a grid-stride
+    // grid of the same residency loses instead. k <= 2 (the C2 sum, /np, SMA)
+    // and the batched launch show no gain beyond the noise and stay uncapped;
+    // the batched launch also runs beside RCCL kernels in the exchange's
+    // pipelined schedule, where LDS held idle would keep their blocks out
+    // (profiles/r02/kfold_occ*.jsonl, ab_occupancy.jsonl).
+    int occ_small = 0;          // k <= 2
+    int occ_fold  = 48 << 10;   // k >= 3
 };
 
 Geometry &geometry()
@@ -156,6 +170,14 @@ unsigned grid_for(size_t nvec, size_t nedge, int unroll, int cap = 0)
     return static_cast<unsigned>(blocks);
 }
 
+// dynamic LDS of an HBM streaming launch over k inputs (Geometry::occ_*); none
+// for a launch over the host link (its grid is small already)
+unsigned occ_lds(int k, bool host_link = false)
+{
+    if (host_link) return 0;
+    return static_cast<unsigned>(k >= 3 ? geometry().occ_fold : geometry().occ_small);
+}
+
 template <typename T, int OP, int EPI, int KC, int UNROLL, int LOADNT, int STPLAIN = 0>
 void launch_vec(const InPtrs &ptrs, int k, void *out, size_t n, const Plan &p,
                 const Div &np, hipStream_t s)
@@ -164,7 +186,7 @@ void launch_vec(const InPtrs &ptrs, int k, void *out, size_t n, const Plan &p,
     const size_t ned = p.head + (n - p.head - p.nvec * V);
     const unsigned g = grid_for(p.nvec, ned, UNROLL, p.grid_cap);
     reduce_kernel<T, OP, EPI, KC, kBlock, UNROLL, LOADNT, STPLAIN>
-        <<<g, kBlock, 0, s>>>(ptrs, k, out, n, p.head, p.nvec, np);
+        <<<g, kBlock, occ_lds(k, p.grid_cap > 0), s>>>(ptrs, k, out, n, p.head, p.nvec, np);
 }
 
 // The tuned fp32 2-input SUM (the headline path) carries every geometry
@@ -428,7 +450,7 @@ int launch_sma(void *v, const void *sum, size_t n, int np, C c1, C c2,
         blocks = (n + kBlock - 1) / kBlock;
         if (blocks > 8192) blocks = 8192;
     }
-    sma_kernel<T, C, kBlock, 4><<<static_cast<unsigned>(blocks), kBlock, 0, s>>>(
+    sma_kernel<T, C, kBlock, 4><<<static_cast<unsigned>(blocks), kBlock, occ_lds(1), s>>>(
         v, sum, n, p.head, p.nvec, c1, c2, make_div(np), p.vec_ok ? 1 : 0);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "sma kernel launch");
@@ -739,6 +761,17 @@ int kf_set_geometry(int unroll, int grid_cap, int loadnt, int stplain)
     g.grid_cap  = grid_cap;
     g.loadnt    = loadnt ? 1 : 0;
     g.stplain   = stplain ? 1 : 0;
+    return KF_OK;
+}
+
+int kf_set_occupancy(int lds_small, int lds_fold)
+{
+    if (lds_small < 0 || lds_fold < 0 || lds_small > (64 << 10) || lds_fold > (64 << 10)) {
+        return KF_ERR_ARG;
+    }
+    Geometry &g = geometry();
+    g.occ_small = lds_small;
+    g.occ_fold  = lds_fold;
     return KF_OK;
 }
 

@@ -1,0 +1,111 @@
+#!/usr/bin/env python3
+"""The occupancy cap (kf_set_occupancy: dynamic LDS per block the kernels never
+touch, so fewer blocks are resident per CU) A/B'd in the product, on the SAME
+buffers for every setting (placement moves a streaming kernel by up to 5 %),
+settings interleaved round by round, median of 7 rounds x 10 launches over 3
+rotating sets: the C2 sum (k = 2), the shard /np (k = 1), the bf16 SMA blend,
+the k = 3 / 4 / 8 folds (256 MiB per stream), and the batched launch (uncapped in the
+product; 16 x
+4 MiB buckets at k = 2, and 16 x 2 MiB shards at k = 8 as the all-to-all fold
+of N = 8 runs it). Every setting's output is checked against the uncapped one.
+
+  python tools/ab_occupancy.py > profiles/r02/ab_occupancy.jsonl
+"""
+import ctypes
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+
+F32, BF16 = 0x20408, 0x20209
+SETTINGS = {"none": (0, 0), "fold48": (0, 48 << 10), "all48": (48 << 10, 48 << 10),
+            "all32_fold48": (32 << 10, 48 << 10)}
+
+
+def main():
+    from kungfu_amd import _lib
+    lib = _lib.load()
+    dev = torch.device("cuda:0")
+    s = torch.cuda.current_stream().cuda_stream
+    P = _lib.ptr_array
+    n = 64 << 20
+    fams = {}
+
+    def fold_family(k):
+        sets = []
+        for _ in range(3):
+            ins = [torch.randn(n, device=dev) for _ in range(k)]
+            sets.append((P([t.data_ptr() for t in ins]), torch.empty(n, device=dev), ins))
+        return (lambda st: lib.kf_bucket_reduce(st[0], k, st[1].data_ptr(), n, F32, 0, s),
+                sets, (k + 1) * 4 * n)
+
+    for k in (2, 3, 4, 8):
+        fams["sum_k%d" % k] = fold_family(k)
+    sets = [(None, torch.randn(n, device=dev), None) for _ in range(3)]
+    fams["div_np8"] = (lambda st: lib.kf_bucket_div(st[1].data_ptr(), n, F32, 8, s), sets, 8 * n)
+    sets = [(torch.randn(n, device=dev).to(torch.bfloat16), torch.randn(n, device=dev).to(torch.bfloat16),
+             None) for _ in range(3)]
+    fams["sma_bf16"] = (lambda st: lib.kf_sma_blend(st[1].data_ptr(), st[0].data_ptr(), n, BF16, 8,
+                                                    ctypes.c_double(0.1), s), sets, 6 * n)
+
+    def batch_family(nb, per, k):
+        sets = []
+        for _ in range(3):
+            ins = [[torch.randn(per, device=dev) for _ in range(k)] for _ in range(nb)]
+            outs = [torch.empty(per, device=dev) for _ in range(nb)]
+            ptrs = P([t.data_ptr() for row in ins for t in row])
+            sets.append((ptrs, outs, ins))
+        cnt = (ctypes.c_size_t * nb)(*([per] * nb))
+        return (lambda st: lib.kf_bucket_reduce_batch(st[0], k, P([o.data_ptr() for o in st[1]]),
+                                                      cnt, nb, F32, 0, 0, s),
+                sets, nb * (k + 1) * 4 * per)
+
+    fams["batch16x4MiB_k2"] = batch_family(16, 1 << 20, 2)
+    fams["batch16x2MiB_k8"] = batch_family(16, 1 << 19, 8)
+
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ts = {(f, c): [] for f in fams for c in SETTINGS}
+    for _ in range(7):
+        for f, (fn, sets, _) in fams.items():
+            for c, (a, b) in SETTINGS.items():
+                assert lib.kf_set_occupancy(a, b) == 0
+                assert fn(sets[0]) == 0
+                e0.record()
+                for i in range(10):
+                    fn(sets[i % 3])
+                e1.record()
+                torch.cuda.synchronize()
+                ts[(f, c)].append(e0.elapsed_time(e1) * 1e3 / 10)
+    # same bits under every setting (fresh outputs of set 0)
+    ok = {}
+    for f, (fn, sets, _) in fams.items():
+        if f in ("div_np8", "sma_bf16"):
+            continue  # in place: checked by the parity tests under the default
+        ref = None
+        for c, (a, b) in SETTINGS.items():
+            lib.kf_set_occupancy(a, b)
+            fn(sets[0])
+            torch.cuda.synchronize()
+            out = sets[0][1]
+            got = [o.clone() for o in out] if isinstance(out, list) else out.clone()
+            if ref is None:
+                ref = got
+            else:
+                same = (all(torch.equal(x, y) for x, y in zip(got, ref)) if isinstance(got, list)
+                        else torch.equal(got, ref))
+                ok[f] = ok.get(f, True) and same
+    lib.kf_set_occupancy(0, 48 << 10)
+    for (f, c), t in ts.items():
+        us = statistics.median(t)
+        print(json.dumps({"family": f, "setting": c, "lds_small_fold": SETTINGS[c],
+                          "us": round(us, 2), "min_us": round(min(t), 2),
+                          "frac": round(fams[f][2] / us / 8e6, 4),
+                          "same_bits": ok.get(f)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
