@@ -43,19 +43,23 @@ struct Geometry {
     int loadnt   = 1;        // non-temporal read streams
     int stplain  = 0;        // plain (not non-temporal) stores
     // Occupancy cap of reduce_kernel, as dynamic LDS per block the kernel
-    // never touches (160 KiB per CU / bytes = resident blocks per CU). Three
-    // 256-thread blocks per CU instead of eight narrows the window of every
-    // stream that is open at once, and the k-input fold gains: in one process
-    // on the same buffers k = 3/4/6/8 0.806/0.808/0.800/0.790 of 8 TB/s against
-    // 0.795/0.790/0.765/0.748 uncapped (tools/explore/kfold_occ.hip), in the
-    // product k = 3/4/8 +1.0/+2.1/+1.8 % (tools/ab_occupancy.py); a grid-stride
-    // grid of the same residency loses instead. k <= 2 (the C2 sum, /np, SMA)
-    // and the batched launch show no gain beyond the noise and stay uncapped;
-    // the batched launch also runs beside RCCL kernels in the exchange's
-    // pipelined schedule, where LDS held idle would keep their blocks out
-    // (profiles/r02/kfold_occ*.jsonl, ab_occupancy.jsonl).
+    // never touches (160 KiB per CU / bytes = resident blocks per CU). The
+    // k-input fold runs best with few requests outstanding chip-wide: one
+    // vector in flight per lane past inputs 0 and 1 (ld_vec_serial) and five
+    // 256-thread blocks per CU instead of eight — k = 3/4/6/8 at
+    // 0.803/0.806/0.805/0.801 of 8 TB/s in one process on the same buffers,
+    // against 0.787/0.779/0.768/0.760 for four vectors in flight uncapped
+    // (tools/explore/kfold_mlp.hip, kfold_occ.hip; profiles/r02/kfold_mlp*.jsonl,
+    // kfold_occ*.jsonl). Six to four blocks per CU form a plateau and three
+    // fall off it (k = 8 0.72), so the cap sits in its middle; the product
+    // kernel equals the probe on the same buffers (kfold_prod_vs_probe3.jsonl:
+    // k = 8 0.790, k = 4 0.796). A grid-stride grid of the same residency loses.
+    // k <= 2 (the C2 sum, /np, SMA) shows no gain beyond the noise and stays
+    // uncapped (ab_c2_occupancy.jsonl), and so does the batched launch, which
+    // in the exchange's pipelined schedule runs beside RCCL kernels whose
+    // blocks LDS held idle would keep out.
     int occ_small = 0;          // k <= 2
-    int occ_fold  = 48 << 10;   // k >= 3
+    int occ_fold  = 32 << 10;   // k >= 3: five blocks per CU
 };
 
 Geometry &geometry()

@@ -324,6 +324,27 @@ __device__ __forceinline__ Vec<S> ld_vec(const void *base, size_t vi)
 
 // Store policy: STPLAIN=0 (default) writes non-temporally — the output is not
 // re-read by this kernel; STPLAIN=1 uses plain stores (tuning variant).
+// One 16-B non-temporal load that completes before the next statement: the
+// load and the wait are inline asm, and the wait redefines the loaded
+// registers, so the compiler can neither hoist later loads above it nor use
+// the data early. The runtime-k fold reads inputs 2..k-1 this way, one vector
+// in flight per lane: with fewer requests outstanding chip-wide the DRAM
+// serves the k + 1 streams better — k = 3/4/6/8 at 0.803/0.806/0.805/0.801 of
+// 8 TB/s (five blocks per CU) against 0.787/0.779/0.768/0.760 with all four
+// vectors of an input in flight (tools/explore/kfold_mlp.hip,
+// profiles/r02/kfold_mlp_asm.jsonl). Bit-identical: the adds keep their order.
+template <typename S>
+__device__ __forceinline__ Vec<S> ld_vec_serial(const void *base, size_t vi)
+{
+    const u32x4 *p = reinterpret_cast<const u32x4 *>(base) + vi;
+    u32x4 raw;
+    asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(raw) : "v"(p));
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(raw));
+    Vec<S> v;
+    __builtin_memcpy(&v, &raw, 16);
+    return v;
+}
+
 template <typename S, int STPLAIN = 0>
 __device__ __forceinline__ void st_vec(void *base, size_t vi, const Vec<S> &v)
 {
@@ -422,7 +443,8 @@ __device__ __forceinline__ void reduce_body(const InPtrs &in, int k, void *out, 
                     }
                 }
             } else {
-                // runtime k: inputs 0 and 1 up front, then one input at a time
+                // runtime k: inputs 0 and 1 up front, then one input at a time,
+                // one vector in flight (ld_vec_serial)
                 Vec<W> a[UNROLL];
                 Vec<W> b[UNROLL];
                 const char *s0 = src(0);
@@ -446,9 +468,9 @@ __device__ __forceinline__ void reduce_body(const InPtrs &in, int k, void *out, 
                 for (int j = 2; j < kk; ++j) {
                     const char *sj = src(j);
 #pragma unroll
-                    for (int u = 0; u < UNROLL; ++u) b[u] = ld_vec<W, LOADNT>(sj, v0 + u * BLOCK);
-#pragma unroll
                     for (int u = 0; u < UNROLL; ++u) {
+                        b[u] = LOADNT ? ld_vec_serial<W>(sj, v0 + u * BLOCK)
+                                      : ld_vec<W, LOADNT>(sj, v0 + u * BLOCK);
 #pragma unroll
                         for (int e = 0; e < V; ++e) {
                             acc[u][e] = L::template combine<OP>(acc[u][e], b[u].e[e]);

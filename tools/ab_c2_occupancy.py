@@ -47,7 +47,7 @@ def main():
             rnd[c] = e0.elapsed_time(e1) * 1e3 / 20
             ts[c].append(rnd[c])
         wins[min(rnd, key=rnd.get)] += 1
-    lib.kf_set_occupancy(0, 48 << 10)
+    lib.kf_set_occupancy(0, 32 << 10)
     ok = all(torch.equal(o, x + y) for _, o, x, y in sets)
     for c, t in ts.items():
         us = statistics.median(t)

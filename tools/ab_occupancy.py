@@ -98,7 +98,7 @@ def main():
                 same = (all(torch.equal(x, y) for x, y in zip(got, ref)) if isinstance(got, list)
                         else torch.equal(got, ref))
                 ok[f] = ok.get(f, True) and same
-    lib.kf_set_occupancy(0, 48 << 10)
+    lib.kf_set_occupancy(0, 32 << 10)
     for (f, c), t in ts.items():
         us = statistics.median(t)
         print(json.dumps({"family": f, "setting": c, "lds_small_fold": SETTINGS[c],
