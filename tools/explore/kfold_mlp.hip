@@ -111,6 +111,43 @@ __global__ void __launch_bounds__(256) fold_asm(Ptrs in, int k, f32x4 *out, size
     for (int u = 0; u < 4; ++u) __builtin_nontemporal_store(a[u], out + v0 + u * 256);
 }
 
+// k = 2 (the C2 sum) with pinned schedules: 8 = all 8 vectors of x and y in
+// flight (the product), 4 = (x,y) of two tiles then wait, twice, 2 = one
+// (x,y) pair at a time
+template <int INFL>
+__global__ void __launch_bounds__(256) sum2_asm(Ptrs in, f32x4 *out, size_t nvec)
+{
+    const size_t v0 = static_cast<size_t>(blockIdx.x) * 1024 + threadIdx.x;
+    if (v0 + 768 >= nvec) return;
+    const f32x4 *x = in.p[0] + v0, *y = in.p[1] + v0;
+    f32x4 a[4], b[4];
+    if (INFL == 8) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) a[u] = ld(x + u * 256);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) b[u] = ld(y + u * 256);
+    } else if (INFL == 4) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            a[2 * h] = ld_asm(x + 2 * h * 256);
+            b[2 * h] = ld_asm(y + 2 * h * 256);
+            a[2 * h + 1] = ld_asm(x + (2 * h + 1) * 256);
+            b[2 * h + 1] = ld_asm(y + (2 * h + 1) * 256);
+            WAIT2(a[2 * h], b[2 * h]);
+            WAIT2(a[2 * h + 1], b[2 * h + 1]);
+        }
+    } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            a[u] = ld_asm(x + u * 256);
+            b[u] = ld_asm(y + u * 256);
+            WAIT2(a[u], b[u]);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) __builtin_nontemporal_store(a[u] + b[u], out + v0 + u * 256);
+}
+
 template <int MODE>  // 0: L4, 1: L13, 2: L22, 3: L1
 __global__ void __launch_bounds__(256) fold(Ptrs in, int k, f32x4 *out, size_t nvec)
 {
@@ -190,12 +227,27 @@ Variant make_asm(int k, int lds)
             }};
 }
 
+template <int INFL>
+Variant make_sum2(int lds)
+{
+    return {"S" + std::to_string(INFL) + "_lds" + std::to_string(lds >> 10) + "K", 2,
+            [lds](const Ptrs &p, f32x4 *o, size_t nvec, hipStream_t s) {
+                sum2_asm<INFL><<<static_cast<unsigned>(nvec / 1024), 256, lds, s>>>(p, o, nvec);
+            }};
+}
+
 int main(int argc, char **argv)
 {
     const size_t n = 64ull << 20, bytes = n * 4, nvec = n / 4;
     const int kmax = 8, sets = 3, launches = 10, rounds = 5;
     std::vector<Variant> vs;
-    if (argc > 1) {  // the asm-pinned schedules
+    if (argc > 1 && argv[1][0] == '2') {  // k = 2 schedules
+        for (int lds : {0, 20 << 10, 24 << 10, 32 << 10, 40 << 10}) {
+            vs.push_back(make_sum2<8>(lds));
+            vs.push_back(make_sum2<4>(lds));
+            vs.push_back(make_sum2<2>(lds));
+        }
+    } else if (argc > 1) {  // the asm-pinned schedules
         for (int k : {3, 4, 6, 8})
             for (int lds : {0, 24 << 10, 32 << 10, 40 << 10, 48 << 10}) {
                 vs.push_back(make_asm<4>(k, lds));
