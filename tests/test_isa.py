@@ -114,3 +114,32 @@ def test_div_epilogue_is_chosen_once(kernels):
         assert TWO_BODIES.match(k)
         n = sum(1 for ins in kernels[k] if ins.startswith("s_cbranch"))
         assert n <= 24, (k, n)
+
+
+RUNTIME_K = re.compile(r"^_ZN2kf(13reduce_kernel|19reduce_batch_kernel)I.*?ELi0ELi256ELi4E")
+
+
+def _serial_loads(lines):
+    """16-B loads whose very next memory instruction is `s_waitcnt vmcnt(0)`."""
+    n = 0
+    for i, ins in enumerate(lines):
+        if not ins.startswith("global_load_dwordx4"):
+            continue
+        for nxt in lines[i + 1:]:
+            if nxt.startswith(("global_", "s_waitcnt")):
+                n += nxt.startswith("s_waitcnt vmcnt(0)")
+                break
+    return n
+
+
+def test_runtime_k_fold_keeps_one_vector_in_flight(kernels):
+    """The k-input fold reads inputs 2..k-1 one 16-B vector per lane at a time
+    (ld_vec_serial: inline-asm load + wait), which measured 0.80 of 8 TB/s at
+    k = 3..8 against 0.76-0.79 with an input's four vectors in flight (DESIGN.md
+    §10 item 2). A compiler or refactor that reverts to the batched loads
+    shows here: every runtime-k reduce / batch kernel has at least four loads
+    each followed directly by its wait."""
+    ks = {k: v for k, v in product_kernels(kernels).items() if RUNTIME_K.match(k)}
+    assert len(ks) >= 20, len(ks)
+    bad = [(k, _serial_loads(v)) for k, v in ks.items() if _serial_loads(v) < 4]
+    assert not bad, bad[:5]
