@@ -120,16 +120,25 @@ RUNTIME_K = re.compile(r"^_ZN2kf(13reduce_kernel|19reduce_batch_kernel)I.*?ELi0E
 
 
 def _serial_loads(lines):
-    """16-B loads whose very next memory instruction is `s_waitcnt vmcnt(0)`."""
-    n = 0
-    for i, ins in enumerate(lines):
-        if not ins.startswith("global_load_dwordx4"):
-            continue
-        for nxt in lines[i + 1:]:
-            if nxt.startswith(("global_", "s_waitcnt")):
-                n += nxt.startswith("s_waitcnt vmcnt(0)")
-                break
-    return n
+    """The longest run of 16-B loads each followed, before any other memory
+    instruction, by `s_waitcnt vmcnt(0)` (load, wait, load, wait, ...)."""
+    mem = []
+    for ins in lines:  # memory instructions, repeated waits merged
+        if ins.startswith(("global_", "s_waitcnt vmcnt")):
+            if not (mem and ins.startswith("s_waitcnt") and mem[-1].startswith("s_waitcnt")):
+                mem.append(ins)
+    best = run = 0
+    i = 0
+    while i < len(mem):
+        if (mem[i].startswith("global_load_dwordx4") and i + 1 < len(mem)
+                and mem[i + 1].startswith("s_waitcnt vmcnt(0)")):
+            run += 1
+            best = max(best, run)
+            i += 2
+        else:
+            run = 0
+            i += 1
+    return best
 
 
 def test_runtime_k_fold_keeps_one_vector_in_flight(kernels):
@@ -137,8 +146,8 @@ def test_runtime_k_fold_keeps_one_vector_in_flight(kernels):
     (ld_vec_serial: inline-asm load + wait), which measured 0.80 of 8 TB/s at
     k = 3..8 against 0.76-0.79 with an input's four vectors in flight (DESIGN.md
     §10 item 2). A compiler or refactor that reverts to the batched loads
-    shows here: every runtime-k reduce / batch kernel has at least four loads
-    each followed directly by its wait."""
+    shows here: every runtime-k reduce / batch kernel has a run of four loads
+    (the four vectors of one input) each followed directly by its wait."""
     ks = {k: v for k, v in product_kernels(kernels).items() if RUNTIME_K.match(k)}
     assert len(ks) >= 20, len(ks)
     bad = [(k, _serial_loads(v)) for k, v in ks.items() if _serial_loads(v) < 4]
