@@ -103,6 +103,12 @@ func (e *Exchange) AllReduceBatch(bufs []DevicePtr, counts []int, t DataType, op
 // Check reports an asynchronous RCCL failure.
 func (e *Exchange) Check() error { return exStatus("kf_exchange_check", C.kf_exchange_check(e.h)) }
 
+// SetPipeline splits every batch call into groups whose HIP work overlaps the
+// next group's RCCL phases (kf_exchange_set_pipeline; 1 = off). Same results.
+func (e *Exchange) SetPipeline(groups int) error {
+	return exStatus("kf_exchange_set_pipeline", C.kf_exchange_set_pipeline(e.h, C.int(groups)))
+}
+
 func (e *Exchange) Close() {
 	if e.h != nil {
 		C.kf_exchange_destroy(e.h)
