@@ -118,6 +118,15 @@ __global__ void __launch_bounds__(256) zc_pipe(const f4 *x, const f4 *y, f4 *z, 
     finish<SPIN>(count, flag, seq);
 }
 
+// completion by a second, one-wave kernel queued behind the reduce on the same
+// stream: it starts after the reduce kernel has ended (its stores released),
+// and stores `seq` into host memory for the host to spin on
+__global__ void flag_after(unsigned long long *flag, unsigned long long seq)
+{
+    if (threadIdx.x == 0)
+        __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 template <typename F>
 static double median_us(F f, int reps)
 {
@@ -233,9 +242,31 @@ int main(int argc, char **argv)
                 reps);
             CHECK(hipStreamSynchronize(s));
             check("spin");
+            // the flag kernel behind the reduce; every call checked right
+            // after the flag (fresh y each call, so a stale z would show)
+            int bad = 0;
+            const double spin2 = median_us(
+                [&] {
+                    ++seq;
+                    y[(seq * 7919) % n] = static_cast<float>(seq % 1000);
+                    launch(false, 0);
+                    flag_after<<<1, 64, 0, s>>>(flag, seq);
+                    while (*vflag != seq) {
+                    }
+                    const size_t i = (seq * 7919) % n;
+                    if (z[i] != x[i] + y[i]) ++bad;
+                },
+                reps);
+            CHECK(hipStreamSynchronize(s));
+            if (bad) {
+                fprintf(stderr, "flag kernel: %d stale results\n", bad);
+                exit(3);
+            }
+            check("spin2");
             printf("{\"bytes\": %zu, \"variant\": \"%s\", \"grid\": %d, \"kernel_b2b_us\": %.2f, "
-                   "\"sync_us\": %.2f, \"ev_us\": %.2f, \"qry_us\": %.2f, \"spin_us\": %.2f}\n",
-                   bytes, kname, g, ms * 1e3 / 200, sync, ev, qry, spin);
+                   "\"sync_us\": %.2f, \"ev_us\": %.2f, \"qry_us\": %.2f, \"spin_us\": %.2f, "
+                   "\"flag_kernel_spin_us\": %.2f}\n",
+                   bytes, kname, g, ms * 1e3 / 200, sync, ev, qry, spin, spin2);
             fflush(stdout);
         }
     }
