@@ -43,7 +43,8 @@ void on_done(int status, void *arg)
 
 // `world` ranks as threads over the loopback transport, each with its own
 // exchange, stream and buckets: S-SGD average of two buckets (one with a tail
-// of count % world) must be the rank-order fold / world on every rank.
+// of count % world) must be the rank-order fold / world on every rank, for
+// both algos, unpipelined and pipelined.
 int multi_rank_loopback(int world)
 {
     kf_loopback_t *g = kf_loopback_create(world);
@@ -67,8 +68,12 @@ int multi_rank_loopback(int world)
                     CHECK(hipMemcpy(bufs[b], h.data(), counts[b] * 4, hipMemcpyHostToDevice) ==
                           hipSuccess);
                 }
-                for (int algo : {KF_ALGO_REDUCE_SCATTER, KF_ALGO_ALL_TO_ALL}) {
-                    if (algo == KF_ALGO_ALL_TO_ALL) {  // reset to the inputs
+                // groups 2: the pipelined schedule (kf_exchange_set_pipeline), each
+                // bucket its own group, folds on the exchange's second stream
+                for (int run = 0; run < 4; ++run) {
+                    const int algo = run % 2 ? KF_ALGO_ALL_TO_ALL : KF_ALGO_REDUCE_SCATTER;
+                    CHECK(kf_exchange_set_pipeline(ex, run < 2 ? 1 : 2) == KF_OK);
+                    if (run > 0) {  // reset to the inputs
                         for (int b = 0; b < 2; ++b) {
                             std::vector<float> h(counts[b]);
                             for (size_t i = 0; i < counts[b]; ++i) h[i] = 0.5f * (r + 1) + (i % 97);
