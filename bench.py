@@ -790,6 +790,12 @@ def _result(args, world, sets, s_bytes, n, hot_s, prim):
             "elements": n,
             "parallelism": parallelism,
         },
+        "note": ("BASELINE configs: N = 1 times the local two-input reduce (C2, HBM-bound); "
+                 "N > 1 times the S-SGD all-reduce of 64 x 4 MiB buckets over xGMI (C3, "
+                 "link-bound), value = N x bucket bytes / step; the two are different steps, so "
+                 "value(N) / (N x value(1)) is the exchange's cost relative to one local "
+                 "reduce, not a scaling efficiency of one kernel (DESIGN.md section 7); "
+                 "collective.frac_of_xgmi grades the N > 1 step against its own bound"),
         "roofline": {
             "bound": "hbm",
             "kernel": REDUCE_KERNEL,
