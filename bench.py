@@ -508,15 +508,37 @@ def c1_run(npeers, modes, steps, warmup, timeout=600):
     return res
 
 
-def c1_summary(steps=100, warmup=10):
+def c1_summary(steps=100, warmup=10, repeats=3):
     """BASELINE configs[0] beside the N = 1 line: np = 2 peers on this host,
     one 4 MiB fp32 bucket, median latency and 4(np-1)*bytes/t
     (kungfu-bench-allreduce.go:73-80); the device session against the
-    reference's own CPU fold (oracle/_ref) in the same session engine."""
-    res = c1_run(2, ("device", "cpu", "cpu_dev"), steps, warmup, timeout=180)
+    reference's own CPU fold (oracle/_ref) in the same session engine. The
+    modes run `repeats` times, interleaved: the CPU fold's median moves by 2x
+    between back-to-back runs of the same command on one box
+    (profiles/r02/c1_variants.jsonl), so each mode reports the median of its
+    runs' medians and every run's median beside it."""
+    runs = [c1_run(2, ("device", "cpu", "cpu_dev"), steps, warmup, timeout=180)
+            for _ in range(repeats)]
+    res = {}
+    for mode in ("device", "cpu", "cpu_dev"):
+        recs = [r[mode] for r in runs]
+        ok = [x for x in recs if "error" not in x]
+        if not ok:
+            res[mode] = recs[0]
+            continue
+        meds = sorted(x["latency_ms_median"] for x in ok)
+        rec = dict(ok[0])
+        rec["latency_ms_median"] = meds[len(meds) // 2]
+        rec["latency_ms_min"] = min(x["latency_ms_min"] for x in ok)
+        rec["rate_GiBps"] = round(4 * (2 - 1) * C1_ELEMS * 4 / (rec["latency_ms_median"] / 1e3)
+                                  / 2**30, 3)
+        rec["correct"] = all(x.get("correct") is True for x in recs)
+        rec["run_medians_ms"] = [x["latency_ms_median"] for x in ok]
+        res[mode] = rec
     out = {"workload": "C1: np=2 localhost, one 4 MiB fp32 bucket, 4 x 1 MiB chunks, STAR "
                        "at rank 0, rchannel framing over unix sockets",
-           "np": 2, "steps": steps, "unit": "GiB/s (4(np-1)*bytes/t, median)",
+           "np": 2, "steps": steps, "repeats": repeats,
+           "unit": "GiB/s (4(np-1)*bytes/t, median of the runs' medians)",
            "modes": "device: bucket in HBM, HIP fold; cpu: bucket in host memory, the "
                     "reference's CPU fold; cpu_dev: bucket in HBM reduced the reference's "
                     "way for GPU tensors (D2H, the cpu all-reduce, H2D)"}
