@@ -152,6 +152,11 @@ int kf_bucket_reduce_batch(const void *const *inputs, int k, void *const *outs,
  * as TF converts the Python constants. No FMA contraction. float types only. */
 int kf_sma_blend(void *v, const void *sum, size_t n, KungFu_Datatype dt,
                  int np, double alpha, void *stream);
+/* kf_sma_blend over nb buckets (vs[b] blended with sums[b], counts[b]
+ * elements each, the same dtype, np and alpha) in one launch per 16 buckets;
+ * the same bits as nb kf_sma_blend calls. */
+int kf_sma_blend_batch(void *const *vs, const void *const *sums, const size_t *counts, int nb,
+                       KungFu_Datatype dt, int np, double alpha, void *stream);
 
 /* ---- runtime / diagnostics ---------------------------------------------- */
 

@@ -71,6 +71,7 @@ EXPORTED = (
     "kf_exchange_all_reduce",
     "kf_exchange_all_reduce_batch",
     "kf_set_occupancy",
+    "kf_sma_blend_batch",
     "kf_exchange_sma_batch",
     "kf_exchange_set_pipeline",
     "kf_exchange_begin_step",
@@ -157,6 +158,10 @@ def load():
                                        c_int, c_int]
     lib.kf_transform2_host.restype = c_int
     lib.kf_set_geometry.argtypes = [c_int, c_int, c_int, c_int]
+    lib.kf_sma_blend_batch.argtypes = [ctypes.POINTER(c_void_p), ctypes.POINTER(c_void_p),
+                                       ctypes.POINTER(c_size_t), c_int, c_int, c_int,
+                                       ctypes.c_double, c_void_p]
+    lib.kf_sma_blend_batch.restype = c_int
     lib.kf_set_occupancy.argtypes = [c_int, c_int]
     lib.kf_set_occupancy.restype = c_int
     lib.kf_set_geometry.restype = c_int

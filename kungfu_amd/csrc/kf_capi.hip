@@ -461,6 +461,63 @@ int launch_sma(void *v, const void *sum, size_t n, int np, C c1, C c2,
     return KF_OK;
 }
 
+// nb variable buckets in one launch per kBatchSeg of them (kf_sma_blend_batch)
+template <typename T, typename C>
+int launch_sma_batch(void *const *vs, const void *const *sums, const size_t *counts, int nb,
+                     int np, C c1, C c2, hipStream_t s)
+{
+    using S         = typename SmaMath<T>::S;
+    constexpr int V = Vec<S>::N;
+    const Div dv    = make_div(np);
+    SmaBatchArgs<C> a;
+    a.nseg        = 0;
+    a.c1          = c1;
+    a.c2          = c2;
+    size_t blocks = 0;
+    auto flush    = [&]() -> int {
+        if (a.nseg == 0) return KF_OK;
+        a.blk0[a.nseg] = static_cast<unsigned>(blocks);
+        sma_batch_kernel<T, C, kBlock, 4><<<static_cast<unsigned>(blocks), kBlock, 0, s>>>(a, dv);
+        a.nseg = 0;
+        blocks = 0;
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return hip_fail(e, "sma batch kernel launch");
+        return KF_OK;
+    };
+    for (int b = 0; b < nb; ++b) {
+        const size_t n = counts[b];
+        if (n == 0) continue;
+        const void *ins[1] = {sums[b]};
+        const Plan p       = make_plan(ins, 1, vs[b], n, sizeof(S));
+        size_t nblk;
+        if (p.vec_ok) {
+            const size_t ned = p.head + (n - p.head - p.nvec * V);
+            nblk             = grid_for(p.nvec, ned, 4);
+        } else {
+            nblk = (n + kBlock - 1) / kBlock;
+            if (nblk > 8192) nblk = 8192;
+        }
+        if (blocks + nblk > 0xffffffffu) {
+            int rc = flush();
+            if (rc != KF_OK) return rc;
+        }
+        const int j = a.nseg;
+        a.v[j]      = vs[b];
+        a.s[j]      = sums[b];
+        a.n[j]      = n;
+        a.head[j]   = p.head;
+        a.nvec[j]   = p.nvec;
+        a.vec_ok[j] = p.vec_ok ? 1 : 0;
+        a.blk0[j]   = static_cast<unsigned>(blocks);
+        blocks += nblk;
+        if (++a.nseg == kBatchSeg) {
+            int rc = flush();
+            if (rc != KF_OK) return rc;
+        }
+    }
+    return flush();
+}
+
 // ---------------------------------------------------------------------------
 // B1 support: host pointers
 // ---------------------------------------------------------------------------
@@ -691,6 +748,28 @@ int kf_sma_blend(void *v, const void *sum, size_t n, KungFu_Datatype dt, int np,
     case KungFu_DOUBLE: return launch_sma<double, double>(v, sum, n, np, 1.0 - alpha, alpha, s);
     case KungFu_FLOAT16: return launch_sma<f16_t, float>(v, sum, n, np, c1f, c2f, s);
     case KungFu_BFLOAT16: return launch_sma<bf16_t, float>(v, sum, n, np, c1f, c2f, s);
+    default: return KF_ERR_DTYPE;
+    }
+}
+
+int kf_sma_blend_batch(void *const *vs, const void *const *sums, const size_t *counts, int nb,
+                       KungFu_Datatype dt, int np, double alpha, void *stream)
+{
+    if (nb < 0 || (nb > 0 && (!vs || !sums || !counts))) return KF_ERR_ARG;
+    if (np < 1) return KF_ERR_ARG;
+    for (int b = 0; b < nb; ++b) {
+        if (counts[b] && (!vs[b] || !sums[b])) return KF_ERR_ARG;
+    }
+    if (nb == 0) return KF_OK;
+    hipStream_t s   = static_cast<hipStream_t>(stream);
+    const float c1f = static_cast<float>(1.0 - alpha);  // as kf_sma_blend
+    const float c2f = static_cast<float>(alpha);
+    switch (dt) {
+    case KungFu_FLOAT: return launch_sma_batch<float, float>(vs, sums, counts, nb, np, c1f, c2f, s);
+    case KungFu_DOUBLE:
+        return launch_sma_batch<double, double>(vs, sums, counts, nb, np, 1.0 - alpha, alpha, s);
+    case KungFu_FLOAT16: return launch_sma_batch<f16_t, float>(vs, sums, counts, nb, np, c1f, c2f, s);
+    case KungFu_BFLOAT16: return launch_sma_batch<bf16_t, float>(vs, sums, counts, nb, np, c1f, c2f, s);
     default: return KF_ERR_DTYPE;
     }
 }

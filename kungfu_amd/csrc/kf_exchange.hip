@@ -560,10 +560,12 @@ int kf_exchange::batch(const void *const *sends, void *const *recvs, const size_
                 KF_HIP(hipMemcpyAsync(recvs[b], sends[b], counts[b] * sz, hipMemcpyDeviceToDevice, s));
             }
         }
-        for (int b = 0; sma && b < nb; ++b) {
-            const int rc = kf_sma_blend(const_cast<void *>(sends[b]), recvs[b], counts[b], dt, W,
-                                        *sma_alpha, s);
-            if (rc != KF_OK) return fail(rc, "kf_sma_blend");
+        if (sma) {
+            std::vector<void *> vv(nb);
+            for (int b = 0; b < nb; ++b) vv[b] = const_cast<void *>(sends[b]);
+            const int rc = kf_sma_blend_batch(vv.data(), const_cast<const void *const *>(recvs),
+                                              counts, nb, dt, W, *sma_alpha, s);
+            if (rc != KF_OK) return fail(rc, "kf_sma_blend_batch");
         }
         return KF_OK;
     }
@@ -683,13 +685,15 @@ int kf_exchange::batch(const void *const *sends, void *const *recvs, const size_
         return group_end(rc3);
     };
 
-    // SMA: v = (1 - alpha) v + alpha (sum / world), once the sum is gathered
+    // SMA: v = (1 - alpha) v + alpha (sum / world), once the sum is gathered;
+    // the buckets' blends in one batched launch
     auto blend = [&](int b0, int b1, hipStream_t cs) -> int {
-        for (int b = b0; sma && b < b1; ++b) {
-            const int e = kf_sma_blend(const_cast<void *>(sends[b]), recvs[b], counts[b], dt, W,
-                                       *sma_alpha, cs);
-            if (e != KF_OK) return fail(e, "kf_sma_blend");
-        }
+        if (!sma || b1 <= b0) return KF_OK;
+        std::vector<void *> vv(b1 - b0);
+        for (int b = b0; b < b1; ++b) vv[b - b0] = const_cast<void *>(sends[b]);
+        const int e = kf_sma_blend_batch(vv.data(), const_cast<const void *const *>(recvs + b0),
+                                         counts + b0, b1 - b0, dt, W, *sma_alpha, cs);
+        if (e != KF_OK) return fail(e, "kf_sma_blend_batch");
         return KF_OK;
     };
 

@@ -691,17 +691,20 @@ template <> struct SmaMath<bf16_t> {
     }
 };
 
+// One block `blk` of `nblk` working on one variable bucket (sma_kernel: the
+// grid; sma_batch_kernel: the bucket's share of it).
 template <typename T, typename C, int BLOCK, int UNROLL, bool P2>
 __device__ __forceinline__ void sma_body(void *v, const void *s, size_t n, size_t head,
-                                         size_t nvec, C c1, C c2, const Div &np, int vec_ok)
+                                         size_t nvec, C c1, C c2, const Div &np, int vec_ok,
+                                         size_t blk, size_t nblk)
 {
     using S         = typename SmaMath<T>::S;
     constexpr int V = Vec<S>::N;
     S *pv           = reinterpret_cast<S *>(v);
     const S *ps     = reinterpret_cast<const S *>(s);
-    const size_t tid = static_cast<size_t>(blockIdx.x) * BLOCK + threadIdx.x;
+    const size_t tid = blk * BLOCK + threadIdx.x;
     if (!vec_ok) {
-        for (size_t i = tid; i < n; i += static_cast<size_t>(gridDim.x) * BLOCK) {
+        for (size_t i = tid; i < n; i += nblk * BLOCK) {
             pv[i] = SmaMath<T>::template blend<P2>(pv[i], ps[i], c1, c2, np);
         }
         return;
@@ -716,7 +719,7 @@ __device__ __forceinline__ void sma_body(void *v, const void *s, size_t n, size_
     const char *sb = reinterpret_cast<const char *>(s) + head * sizeof(S);
     const size_t tile   = static_cast<size_t>(BLOCK) * UNROLL;
     const size_t ntiles = (nvec + tile - 1) / tile;
-    for (size_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    for (size_t t = blk; t < ntiles; t += nblk) {
         const size_t v0 = t * tile + threadIdx.x;
         if (v0 + (UNROLL - 1) * BLOCK < nvec) {
             // full tile: every load issued before the first use
@@ -755,9 +758,40 @@ __global__ void __launch_bounds__(BLOCK)
                C c1, C c2, Div np, int vec_ok)
 {
     if (np.pow2) {
-        sma_body<T, C, BLOCK, UNROLL, true>(v, s, n, head, nvec, c1, c2, np, vec_ok);
+        sma_body<T, C, BLOCK, UNROLL, true>(v, s, n, head, nvec, c1, c2, np, vec_ok, blockIdx.x,
+                                            gridDim.x);
     } else {
-        sma_body<T, C, BLOCK, UNROLL, false>(v, s, n, head, nvec, c1, c2, np, vec_ok);
+        sma_body<T, C, BLOCK, UNROLL, false>(v, s, n, head, nvec, c1, c2, np, vec_ok, blockIdx.x,
+                                             gridDim.x);
+    }
+}
+
+// The SMA blend of many variable buckets in ONE launch (an exchange's step
+// blends every bucket of the model; C5's BERT-base is 14 buckets), laid out
+// as the reduce batch: bucket i owns blocks [blk0[i], blk0[i+1]).
+template <typename C> struct SmaBatchArgs {
+    void *v[kBatchSeg];
+    const void *s[kBatchSeg];
+    size_t n[kBatchSeg], head[kBatchSeg], nvec[kBatchSeg];
+    int vec_ok[kBatchSeg];
+    unsigned blk0[kBatchSeg + 1];
+    int nseg;
+    C c1, c2;
+};
+
+template <typename T, typename C, int BLOCK, int UNROLL>
+__global__ void __launch_bounds__(BLOCK) sma_batch_kernel(SmaBatchArgs<C> a, Div np)
+{
+    const unsigned b = blockIdx.x;
+    int i            = 0;
+    while (i + 1 < a.nseg && b >= a.blk0[i + 1]) ++i;
+    const size_t nblk = a.blk0[i + 1] - a.blk0[i];
+    if (np.pow2) {
+        sma_body<T, C, BLOCK, UNROLL, true>(a.v[i], a.s[i], a.n[i], a.head[i], a.nvec[i], a.c1,
+                                            a.c2, np, a.vec_ok[i], b - a.blk0[i], nblk);
+    } else {
+        sma_body<T, C, BLOCK, UNROLL, false>(a.v[i], a.s[i], a.n[i], a.head[i], a.nvec[i], a.c1,
+                                             a.c2, np, a.vec_ok[i], b - a.blk0[i], nblk);
     }
 }
 

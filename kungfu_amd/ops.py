@@ -5,6 +5,8 @@ the caller's current HIP stream (or the stream given). Tensors must be
 contiguous and on the GPU; there is no CPU path — a CPU tensor or a missing
 library raises.
 """
+import ctypes
+
 import torch
 
 from . import _lib
@@ -153,3 +155,25 @@ def sma_blend_(v, summed, np_, alpha, stream=None):
                           _stream(stream, v.device))
     _lib.check(rc, "kf_sma_blend")
     return v
+
+
+def sma_blend_batch_(vs, sums, np_, alpha, stream=None):
+    """sma_blend_ over many buckets (one dtype) in one launch per 16 of them
+    (kf_sma_blend_batch); the same bits as one sma_blend_ per bucket."""
+    vs, sums = list(vs), list(sums)
+    if len(vs) != len(sums):
+        raise ValueError("sma_blend_batch_: one sum per variable bucket")
+    if not vs:
+        return vs
+    _check_dev(vs + sums)
+    for v, s in zip(vs, sums):
+        if v.numel() != s.numel() or v.dtype != vs[0].dtype or s.dtype != v.dtype:
+            raise ValueError("sma_blend_batch_: shape/dtype mismatch")
+    lib = _lib.load()
+    cnt = (ctypes.c_size_t * len(vs))(*[v.numel() for v in vs])
+    rc = lib.kf_sma_blend_batch(_lib.ptr_array([v.data_ptr() for v in vs]),
+                                _lib.ptr_array([s.data_ptr() for s in sums]), cnt, len(vs),
+                                int(kungfu_dtype(vs[0])), int(np_), float(alpha),
+                                _stream(stream, vs[0].device))
+    _lib.check(rc, "kf_sma_blend_batch")
+    return vs

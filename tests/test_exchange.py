@@ -685,3 +685,34 @@ def test_world1_rccl_entry_points():
     r = subprocess.run([sys.executable, "-c", _W1_CHILD % os.path.dirname(HERE)], env=env,
                        capture_output=True, text=True, timeout=240)
     assert r.returncode == 0 and "W1_RCCL_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,np_", [("f32", 8), ("f32", 3), ("bf16", 8), ("bf16", 7),
+                                      ("f16", 2), ("f64", 5)])
+def test_sma_blend_batch_matches_single(name, np_):
+    """kf_sma_blend_batch over 20 ragged buckets (more than one launch of 16;
+    sizes 0, 1, 7, ...; one bucket whose v and sum sit at different residues,
+    so it takes the element-wise body) equals one kf_sma_blend per bucket
+    bit for bit, and the oracle's blend for f32 / bf16."""
+    import torch
+    from kungfu_amd import ops
+    from oracle import oracle
+    dev = _gpu()
+    sizes = [0, 1, 7, 4099, 1 << 20, 262147, 33] + [4096 * (i + 1) + i for i in range(13)]
+    vs0 = [_rand(name, n, 10 + b) for b, n in enumerate(sizes)]
+    ss = [_rand(name, n, 500 + b) for b, n in enumerate(sizes)]
+    a = [_to_dev(v, name, dev) for v in vs0]
+    s = [_to_dev(x, name, dev) for x in ss]
+    # bucket 3: the sum one element past an aligned start, v aligned
+    s[3] = torch.cat([s[3][:1], s[3]])[1:]
+    b = [t.clone() for t in a]
+    ops.sma_blend_batch_(a, s, np_, 0.1)
+    for v, x in zip(b, s):
+        ops.sma_blend_(v, x, np_, 0.1)
+    torch.cuda.synchronize()
+    for j in range(len(sizes)):
+        assert np.array_equal(_to_np(a[j], name), _to_np(b[j], name)), j
+        if name in ("f32", "bf16"):
+            want = oracle.sma_blend(vs0[j], ss[j], name, np_, 0.1)
+            assert np.array_equal(_to_np(a[j], name), want), j

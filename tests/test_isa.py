@@ -27,13 +27,13 @@ OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
 PRODUCT_REDUCE = re.compile(r"^_ZN2kf13reduce_kernelI.*ELi256ELi\d+ELi1ELi0EEEv")
 TUNING_ONLY = re.compile(r"^_ZN2kf13reduce_kernelIfLi0ELi0ELi2ELi256ELi[128]E")
 STREAMING = ("_ZN2kf20reduce_spread_kernelI", "_ZN2kf10sma_kernelI",
-             "_ZN2kf19reduce_batch_kernelI")
+             "_ZN2kf19reduce_batch_kernelI", "_ZN2kf16sma_batch_kernelI")
 # the scalar head/tail and the ragged last tile are the only divergent code
 MAX_EXEC_BRANCHES = 6
 # kernels with the /np epilogue carry two bodies, chosen once on np.pow2
 # (EPI_MUL / EPI_DIV, kf_reduce_kernels.hpp), each with its own edges
 TWO_BODIES = re.compile(r"^_ZN2kf(\d+(reduce_kernel|reduce_batch_kernel|reduce_spread_kernel)"
-                        r"I(f|d|NS_\d+\w+?_tE)Li0ELi1E|10sma_kernelI)")
+                        r"I(f|d|NS_\d+\w+?_tE)Li0ELi1E|10sma_kernelI|16sma_batch_kernelI)")
 
 
 @pytest.fixture(scope="module")
@@ -81,6 +81,7 @@ def test_product_kernels_found(kernels):
     assert any(k.startswith(STREAMING[1]) for k in ks)
     # the multi-bucket launch: 12 dtypes plain (k = 1, 2, runtime) + 4 floats / np
     assert sum(1 for k in ks if k.startswith(STREAMING[2])) >= 40
+    assert sum(1 for k in ks if k.startswith(STREAMING[3])) == 4  # f32 f64 f16 bf16
 
 
 def test_streaming_loads_and_stores_are_nontemporal(kernels):
