@@ -86,6 +86,36 @@ func SMABlend(v, sum DevicePtr, n int, t DataType, np int, alpha float64, s Stre
 	return status("kf_sma_blend", rc)
 }
 
+// SMABlendBatch: SMABlend over many buckets in one launch per 16 of them
+// (kf_sma_blend_batch); vs[i] is blended with sums[i], counts[i] elements.
+func SMABlendBatch(vs, sums []DevicePtr, counts []int, t DataType, np int, alpha float64,
+	s Stream) error {
+	if len(vs) != len(sums) || len(vs) != len(counts) {
+		return errors.New("SMABlendBatch: vs, sums and counts differ in length")
+	}
+	if len(vs) == 0 {
+		return nil
+	}
+	pv := C.malloc(C.size_t(len(vs)) * C.size_t(unsafe.Sizeof(uintptr(0))))
+	ps := C.malloc(C.size_t(len(vs)) * C.size_t(unsafe.Sizeof(uintptr(0))))
+	pc := C.malloc(C.size_t(len(vs)) * C.size_t(unsafe.Sizeof(C.size_t(0))))
+	defer C.free(pv)
+	defer C.free(ps)
+	defer C.free(pc)
+	av := (*[1 << 20]unsafe.Pointer)(pv)[:len(vs):len(vs)]
+	as := (*[1 << 20]unsafe.Pointer)(ps)[:len(vs):len(vs)]
+	ac := (*[1 << 20]C.size_t)(pc)[:len(vs):len(vs)]
+	for i := range vs {
+		av[i] = unsafe.Pointer(uintptr(vs[i]))
+		as[i] = unsafe.Pointer(uintptr(sums[i]))
+		ac[i] = C.size_t(counts[i])
+	}
+	rc := C.kf_sma_blend_batch((*unsafe.Pointer)(pv), (*unsafe.Pointer)(ps), (*C.size_t)(pc),
+		C.int(len(vs)), C.KungFu_Datatype(t), C.int(np), C.double(alpha),
+		unsafe.Pointer(uintptr(s)))
+	return status("kf_sma_blend_batch", rc)
+}
+
 // HostRegister page-locks a C-allocated host buffer so Transform2 reduces it
 // in place over PCIe (zero copy). Go heap memory must not be registered: the
 // collector may move or free it.
