@@ -258,6 +258,32 @@ def kernel_families(lib, dev):
            "kf_bucket_reduce_batch: 16 buckets of 4 MiB (C3's size), z = x + y, one launch")
     del sets
     torch.cuda.empty_cache()
+    # C5's blend step: BERT-base bf16 in the bench's buckets, one batched launch
+    from kungfu_amd.collective import GradBuckets
+    bert = _models()["bert"][:201]
+    sets = []
+    for _ in range(3):
+        gbv = GradBuckets(bert, torch.bfloat16, dev, 8, bucket_bytes=16 << 20)
+        for b in gbv.buckets:
+            b.copy_(torch.randn(b.numel(), device=dev, generator=g).bfloat16())
+        sums = [torch.randn(b.numel(), device=dev, generator=g).bfloat16() for b in gbv.buckets]
+        sets.append((_lib.ptr_array([b.data_ptr() for b in gbv.buckets]),
+                     _lib.ptr_array([t.data_ptr() for t in sums]),
+                     (ctypes.c_size_t * len(sums))(*[t.numel() for t in sums]), gbv, sums))
+    nbs = len(sets[0][4])
+    v0 = [b.clone() for b in sets[0][3].buckets]
+    _lib.check(lib.kf_sma_blend_batch(sets[0][0], sets[0][1], sets[0][2], nbs, 0x20209, 8, 0.1,
+                                      sp), "sma batch")
+    for b, a in zip(v0, sets[0][4]):
+        ops.sma_blend_(b, a, 8, 0.1)  # the per-bucket kernel: the same bits
+    ok = all(torch.equal(a, b) for a, b in zip(sets[0][3].buckets, v0))
+    us = timed(lambda i: lib.kf_sma_blend_batch(sets[i][0], sets[i][1], sets[i][2], nbs, 0x20209,
+                                                8, 0.1, sp), 3)
+    report("sma_batch_c5_bf16", 3 * 2 * sum(t.numel() for t in sets[0][4]), us, ok,
+           "kf_sma_blend_batch: C5's SMA blend step, BERT-base bf16 in %d buckets, one launch "
+           "(bit-identical to one kf_sma_blend per bucket)" % nbs)
+    del sets, v0
+    torch.cuda.empty_cache()
     return out
 
 
