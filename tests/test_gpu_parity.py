@@ -302,6 +302,32 @@ def test_alignment_and_aliasing(lib, orc, dev):
         assert np.array_equal(got, x[:n] + y[:n])
 
 
+@pytest.mark.parametrize("dt,k", [("f32", 5), ("f32", 8), ("bf16", 4), ("f16", 3), ("u8", 6)])
+def test_k_fold_inputs_at_other_residues(lib, orc, dev, dt, k):
+    """The runtime-k fold with inputs at 16-B residues other than the
+    output's: inputs 2..k-1 go through the one-in-flight inline-asm loads
+    (ld_vec_serial) at unaligned addresses; the left fold in input order must
+    equal the oracle's chain."""
+    from kungfu_amd import _lib
+    from oracle.oracle import DT, NP
+    rng = np.random.default_rng(zlib.crc32(("res" + dt).encode()) + k)
+    npdt = NP[dt]
+    isz = np.dtype(npdt).itemsize
+    n = 300007
+    hs = [_rand(orc, rng, dt, n + 16) for _ in range(k)]
+    ts = [torch.from_numpy(np.ascontiguousarray(h).view(np.uint8)).to(dev) for h in hs]
+    s = torch.cuda.current_stream().cuda_stream
+    offs = [(j * 3 + 1) % 7 for j in range(k)]  # element offsets, mixed residues
+    oz = 2
+    out = torch.zeros((n + 16) * isz, dtype=torch.uint8, device=dev)
+    ptrs = _lib.ptr_array([t.data_ptr() + isz * o for t, o in zip(ts, offs)])
+    assert lib.kf_bucket_reduce(ptrs, k, out.data_ptr() + isz * oz, n, DT[dt], 0, s) == 0
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(npdt)[oz:oz + n]
+    want = orc.reduce_k([h[o:o + n] for h, o in zip(hs, offs)], dt, "sum")
+    assert golden_io.same_bits_or_nan(got, want), (dt, k)
+
+
 def test_k1_copy_and_empty(lib, dev):
     from kungfu_amd import _lib
     t = torch.arange(1000, dtype=torch.float32, device=dev)
