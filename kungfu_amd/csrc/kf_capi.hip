@@ -54,6 +54,8 @@ struct Geometry {
     // fall off it (k = 8 0.72), so the cap sits in its middle; the product
     // kernel equals the probe on the same buffers (kfold_prod_vs_probe3.jsonl:
     // k = 8 0.790, k = 4 0.796). A grid-stride grid of the same residency loses.
+    // Both apply to large launches only (kSerialMinBlocks, kCapMinBlocks below):
+    // a grid that fits on the chip at once is latency-bound instead.
     // k <= 2 (the C2 sum, /np, SMA) shows no gain beyond the noise and stays
     // uncapped (ab_c2_occupancy.jsonl), and so does the batched launch, which
     // in the exchange's pipelined schedule runs beside RCCL kernels whose
@@ -174,12 +176,24 @@ unsigned grid_for(size_t nvec, size_t nedge, int unroll, int cap = 0)
     return static_cast<unsigned>(blocks);
 }
 
-// dynamic LDS of an HBM streaming launch over k inputs (Geometry::occ_*); none
-// for a launch over the host link (its grid is small already)
-unsigned occ_lds(int k, bool host_link = false)
+// The runtime-k fold's schedule and residency follow the size of the launch
+// (tools/explore/kfold_mlp.hip s|m|asm; profiles/r02/kfold_mlp_{small,mid}*,
+// kfold_mlp_asm.jsonl; k = 8, time per launch, batched-4 vs one-in-flight):
+// below 2048 blocks (32 MiB per input) the whole grid is resident at once and
+// latency-bound, so an input's four vectors go together (4 MiB: 7.6 vs
+// 14.4 us; 16 MiB: 23.6 vs 24.7 us); from 2048 blocks one vector in flight
+// wins (64 MiB: 92.2 vs 96.3 us), and from 8192 blocks (128 MiB) the
+// residency cap adds to it (256 MiB: 382 vs 391 us uncapped, 405 batched).
+constexpr unsigned kSerialMinBlocks = 2048;
+constexpr unsigned kCapMinBlocks    = 8192;
+
+// dynamic LDS of an HBM streaming launch of `blocks` blocks over k inputs
+// (Geometry::occ_*); none for a launch over the host link (small grid)
+unsigned occ_lds(int k, size_t blocks, bool host_link = false)
 {
     if (host_link) return 0;
-    return static_cast<unsigned>(k >= 3 ? geometry().occ_fold : geometry().occ_small);
+    if (k >= 3) return blocks >= kCapMinBlocks ? static_cast<unsigned>(geometry().occ_fold) : 0;
+    return static_cast<unsigned>(geometry().occ_small);
 }
 
 template <typename T, int OP, int EPI, int KC, int UNROLL, int LOADNT, int STPLAIN = 0>
@@ -189,8 +203,10 @@ void launch_vec(const InPtrs &ptrs, int k, void *out, size_t n, const Plan &p,
     constexpr int V  = Vec<typename Elt<T>::S>::N;
     const size_t ned = p.head + (n - p.head - p.nvec * V);
     const unsigned g = grid_for(p.nvec, ned, UNROLL, p.grid_cap);
+    const int serial = KC == 0 && g >= kSerialMinBlocks ? 1 : 0;
     reduce_kernel<T, OP, EPI, KC, kBlock, UNROLL, LOADNT, STPLAIN>
-        <<<g, kBlock, occ_lds(k, p.grid_cap > 0), s>>>(ptrs, k, out, n, p.head, p.nvec, np);
+        <<<g, kBlock, occ_lds(k, g, p.grid_cap > 0), s>>>(ptrs, k, out, n, p.head, p.nvec, np,
+                                                          serial);
 }
 
 // The tuned fp32 2-input SUM (the headline path) carries every geometry
@@ -353,6 +369,7 @@ int launch_batch_kc(const void *const *in, int k, void *const *outs, const size_
     auto flush      = [&]() -> int {
         if (a.nseg == 0) return KF_OK;
         a.blk0[a.nseg] = static_cast<unsigned>(blocks);
+        a.serial       = KC == 0 && blocks >= kSerialMinBlocks ? 1 : 0;
         reduce_batch_kernel<T, OP, EPI, KC, kBlock, U>
             <<<static_cast<unsigned>(blocks), kBlock, 0, s>>>(a, k, np);
         a.nseg = 0;
@@ -454,7 +471,7 @@ int launch_sma(void *v, const void *sum, size_t n, int np, C c1, C c2,
         blocks = (n + kBlock - 1) / kBlock;
         if (blocks > 8192) blocks = 8192;
     }
-    sma_kernel<T, C, kBlock, 4><<<static_cast<unsigned>(blocks), kBlock, occ_lds(1), s>>>(
+    sma_kernel<T, C, kBlock, 4><<<static_cast<unsigned>(blocks), kBlock, occ_lds(1, blocks), s>>>(
         v, sum, n, p.head, p.nvec, c1, c2, make_div(np), p.vec_ok ? 1 : 0);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "sma kernel launch");

@@ -390,7 +390,7 @@ template <typename T, int OP, int EPI, int KC, int BLOCK, int UNROLL, int LOADNT
           int STPLAIN = 0>
 __device__ __forceinline__ void reduce_body(const InPtrs &in, int k, void *out, size_t n,
                                             size_t head, size_t nvec, const Div &np,
-                                            size_t blk, size_t nblk)
+                                            size_t blk, size_t nblk, int serial)
 {
     using S         = typename Elt<T>::S;
     using L         = Lane<T>;
@@ -443,8 +443,10 @@ __device__ __forceinline__ void reduce_body(const InPtrs &in, int k, void *out, 
                     }
                 }
             } else {
-                // runtime k: inputs 0 and 1 up front, then one input at a time,
-                // one vector in flight (ld_vec_serial)
+                // runtime k: inputs 0 and 1 up front, then one input at a time:
+                // its UNROLL vectors together (small grids, latency-bound), or
+                // one vector in flight (ld_vec_serial) when `serial` (grids
+                // large enough to be bandwidth-bound; chosen by the host)
                 Vec<W> a[UNROLL];
                 Vec<W> b[UNROLL];
                 const char *s0 = src(0);
@@ -467,13 +469,24 @@ __device__ __forceinline__ void reduce_body(const InPtrs &in, int k, void *out, 
                 }
                 for (int j = 2; j < kk; ++j) {
                     const char *sj = src(j);
+                    if (LOADNT && serial) {  // wave-uniform: a kernel argument
 #pragma unroll
-                    for (int u = 0; u < UNROLL; ++u) {
-                        b[u] = LOADNT ? ld_vec_serial<W>(sj, v0 + u * BLOCK)
-                                      : ld_vec<W, LOADNT>(sj, v0 + u * BLOCK);
+                        for (int u = 0; u < UNROLL; ++u) {
+                            b[u] = ld_vec_serial<W>(sj, v0 + u * BLOCK);
 #pragma unroll
-                        for (int e = 0; e < V; ++e) {
-                            acc[u][e] = L::template combine<OP>(acc[u][e], b[u].e[e]);
+                            for (int e = 0; e < V; ++e) {
+                                acc[u][e] = L::template combine<OP>(acc[u][e], b[u].e[e]);
+                            }
+                        }
+                    } else {
+#pragma unroll
+                        for (int u = 0; u < UNROLL; ++u) b[u] = ld_vec<W, LOADNT>(sj, v0 + u * BLOCK);
+#pragma unroll
+                        for (int u = 0; u < UNROLL; ++u) {
+#pragma unroll
+                            for (int e = 0; e < V; ++e) {
+                                acc[u][e] = L::template combine<OP>(acc[u][e], b[u].e[e]);
+                            }
                         }
                     }
                 }
@@ -514,17 +527,17 @@ template <typename T, int OP, int EPI, int KC, int BLOCK, int UNROLL, int LOADNT
           int STPLAIN = 0>
 __global__ void __launch_bounds__(BLOCK)
     reduce_kernel(InPtrs in, int k, void *out, size_t n, size_t head,
-                  size_t nvec, Div np)
+                  size_t nvec, Div np, int serial)
 {
     if constexpr (EPI == EPI_DIV) {
         if (np.pow2) {
             reduce_body<T, OP, EPI_MUL, KC, BLOCK, UNROLL, LOADNT, STPLAIN>(
-                in, k, out, n, head, nvec, np, blockIdx.x, gridDim.x);
+                in, k, out, n, head, nvec, np, blockIdx.x, gridDim.x, serial);
             return;
         }
     }
     reduce_body<T, OP, EPI, KC, BLOCK, UNROLL, LOADNT, STPLAIN>(in, k, out, n, head, nvec, np,
-                                                               blockIdx.x, gridDim.x);
+                                                               blockIdx.x, gridDim.x, serial);
 }
 
 // ---------------------------------------------------------------------------
@@ -545,6 +558,7 @@ struct BatchArgs {
     size_t n[kBatchSeg], head[kBatchSeg], nvec[kBatchSeg];
     unsigned blk0[kBatchSeg + 1];
     int nseg;
+    int serial;  // the runtime-k fold's one-in-flight schedule (reduce_body)
 };
 
 template <typename T, int OP, int EPI, int KC, int BLOCK, int UNROLL>
@@ -557,12 +571,13 @@ __global__ void __launch_bounds__(BLOCK) reduce_batch_kernel(BatchArgs a, int k,
     if constexpr (EPI == EPI_DIV) {
         if (np.pow2) {
             reduce_body<T, OP, EPI_MUL, KC, BLOCK, UNROLL, 1, 0>(
-                a.in[s], k, a.out[s], a.n[s], a.head[s], a.nvec[s], np, b - a.blk0[s], nblk);
+                a.in[s], k, a.out[s], a.n[s], a.head[s], a.nvec[s], np, b - a.blk0[s], nblk,
+                a.serial);
             return;
         }
     }
     reduce_body<T, OP, EPI, KC, BLOCK, UNROLL, 1, 0>(a.in[s], k, a.out[s], a.n[s], a.head[s],
-                                                    a.nvec[s], np, b - a.blk0[s], nblk);
+                                                    a.nvec[s], np, b - a.blk0[s], nblk, a.serial);
 }
 
 // Fold for inputs that sit behind DIFFERENT links (the P2P shard fold reads

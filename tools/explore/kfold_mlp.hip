@@ -238,10 +238,24 @@ Variant make_sum2(int lds)
 
 int main(int argc, char **argv)
 {
-    const size_t n = 64ull << 20, bytes = n * 4, nvec = n / 4;
-    const int kmax = 8, sets = 3, launches = 10, rounds = 5;
+    // argv[2]: elements per input (default 64 Mi = 256 MiB)
+    const size_t n = argc > 2 ? std::strtoull(argv[2], nullptr, 10) : (64ull << 20);
+    const size_t bytes = n * 4, nvec = n / 4;
+    const int kmax = 8, sets = 3, launches = 50, rounds = 5;
     std::vector<Variant> vs;
-    if (argc > 1 && argv[1][0] == '2') {  // k = 2 schedules
+    if (argc > 1 && argv[1][0] == 's') {  // small sizes: A4 vs A1, uncapped
+        for (int k : {3, 4, 8}) {
+            vs.push_back(make_asm<7>(k, 0));
+            vs.push_back(make_asm<6>(k, 0));
+            vs.push_back(make_asm<4>(k, 0));
+        }
+    } else if (argc > 1 && argv[1][0] == 'm') {  // mid sizes: A4 uncapped vs A1 capped
+        for (int k : {3, 4, 8}) {
+            vs.push_back(make_asm<7>(k, 0));
+            vs.push_back(make_asm<6>(k, 0));
+            vs.push_back(make_asm<6>(k, 32 << 10));
+        }
+    } else if (argc > 1 && argv[1][0] == '2') {  // k = 2 schedules
         for (int lds : {0, 20 << 10, 24 << 10, 32 << 10, 40 << 10}) {
             vs.push_back(make_sum2<8>(lds));
             vs.push_back(make_sum2<4>(lds));
