@@ -192,7 +192,8 @@ int kf_set_geometry(int unroll, int grid_cap, int loadnt, int stplain);
  * (kf_bucket_reduce*, kf_bucket_div, kf_sma_blend; not the batched launch), as
  * dynamic LDS bytes per 256-thread block (0 = none, at most 64 KiB) for the
  * k <= 2 kernels (two-input sum, /np, SMA) and for the k >= 3 folds.
- * Defaults: 0 and 32 KiB (five blocks per CU). Not thread-safe. */
+ * Defaults: 0 and 32 KiB (five blocks per CU); the fold's cap applies to
+ * launches of at least 8192 blocks (128 MiB per fp32 input). Not thread-safe. */
 int kf_set_occupancy(int lds_small, int lds_fold);
 
 /* Host-pointer reduce with a status code instead of exit(): the path
