@@ -4,6 +4,7 @@ values come from the oracle / the reference's known answers."""
 import json
 import os
 import socket
+import tempfile
 import sys
 import traceback
 
@@ -25,11 +26,13 @@ def free_port():
     return p
 
 
-def _entry(rank, world, port, fn_name, errq, use_gpu):
+def _entry(rank, world, store, fn_name, errq, use_gpu):
     sys.path[:0] = [ROOT, HERE]
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     try:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        # a file store, not a TCP port: parallel test workers (pytest -n) once
+        # raced for the same free port
+        dist.init_process_group("gloo", init_method="file://" + store, rank=rank,
+                                world_size=world)
         import test_collective_gloo as mod
         getattr(mod, fn_name)(rank, world, use_gpu)
         dist.barrier()
@@ -44,8 +47,8 @@ def _entry(rank, world, port, fn_name, errq, use_gpu):
 def run_world(fn_name, world, use_gpu=False):
     ctx = mp.get_context("spawn")
     errq = ctx.SimpleQueue()
-    port = free_port()
-    procs = [ctx.Process(target=_entry, args=(r, world, port, fn_name, errq, use_gpu))
+    store = os.path.join(tempfile.mkdtemp(prefix="kfgloo"), "store")
+    procs = [ctx.Process(target=_entry, args=(r, world, store, fn_name, errq, use_gpu))
              for r in range(world)]
     for p in procs:
         p.start()
