@@ -12,11 +12,12 @@ granularity). value = bucket GiB/s = S / t.
 
 N > 1 (configs[2], C3 geometry): one step = the S-SGD all-reduce of 64 x 4 MiB
 fp32 gradient buckets (256 MiB) per rank: per bucket RCCL reduce-scatter(sum)
--> HIP /np epilogue on the shard -> RCCL all-gather over xGMI, buckets
-pipelined (kungfu_amd.collective). Per-GPU work is fixed
-(scaling "weak"); value = N * S / t (whole job). The local-reduce kernel is
-also timed on every rank so the roofline object always describes the HIP
-reduce kernel.
+-> HIP /np epilogue on the shard -> RCCL all-gather over xGMI, all 64 in one
+native call (kf_exchange_all_reduce_batch). Per-GPU work is fixed (scaling
+"weak"); value = S / t, the bucket GiB/s each GPU reduces (the metric is "per
+GPU"), with the whole job's N * S / t beside it as value_aggregate. The
+local-reduce kernel is also timed on every rank so the roofline object always
+describes the HIP reduce kernel.
 
 Roofline: algorithmic bytes per launch = 3 * S (read x, read y, write z)
 (SURVEY.md §8d), achieved = 3S / (average launch duration from HIP events on
@@ -284,6 +285,107 @@ def kernel_families(lib, dev):
            "(bit-identical to one kf_sma_blend per bucket)" % nbs)
     del sets, v0
     torch.cuda.empty_cache()
+    out.update(exchange_phase2(lib, dev, g))
+    return out
+
+
+def exchange_phase2(lib, dev, g, world=8):
+    """The element-wise step the native exchange launches between its two
+    collectives, at the shapes it has on BASELINE's 8-GPU configs (phase 2 of
+    kf_exchange.hip's batch): C5's rank-order fold of the 8 received bf16
+    shards per bucket with /8 fused (all-to-all algo), and the in-place shard
+    /np of C4 (ResNet-50, 16 buckets) and C3 (64 x 4 MiB) after their
+    reduce-scatters — each ONE kf_bucket_reduce_batch call on the exact
+    pointers and counts the exchange passes. Launches cycle over enough
+    independent sets (>= 0.75 GiB) that none is served from the Infinity
+    Cache; each checked against the oracle-equivalent torch restatement."""
+    from kungfu_amd import _lib
+    from kungfu_amd.collective import GradBuckets
+    sp = torch.cuda.current_stream().cuda_stream
+    out = {}
+    models = _models()
+
+    def timed(launch, nsets):
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for i in range(nsets):
+            _lib.check(launch(i), "launch")
+        ts = []
+        for _ in range(5):
+            ev0.record()
+            for i in range(4 * nsets):
+                launch(i % nsets)
+            ev1.record()
+            torch.cuda.synchronize()
+            ts.append(ev0.elapsed_time(ev1) * 1e3 / (4 * nsets))
+        ts.sort()
+        return ts[2]
+
+    def report(name, algo_bytes, us, ok, what, nb):
+        out[name] = {"us": round(us, 2), "algorithmic_bytes": algo_bytes,
+                     "frac": round(algo_bytes / us / 1e3 / HBM_PEAK_GBPS, 4),
+                     "correct": bool(ok), "buckets": nb, "what": what}
+
+    # C5 at N = 8: per bucket, the workspace holds the 8 received shards back to
+    # back (q elements each) and the fold writes shard `rank` of the bucket
+    bert = models["bert"][:201]
+    counts = [b.numel() for b in GradBuckets(bert, torch.bfloat16, dev, world,
+                                             bucket_bytes=16 << 20).buckets]
+    qs = [c // world for c in counts]
+    per_set = sum((world + 1) * q * 2 for q in qs)
+    nsets = max(2, -(-(768 << 20) // per_set))
+    sets = []
+    for _ in range(nsets):
+        ws = [torch.randn(world * q, device=dev, generator=g).bfloat16() for q in qs]
+        outs = [torch.empty(q, device=dev, dtype=torch.bfloat16) for q in qs]
+        ins = _lib.ptr_array([w.data_ptr() + j * q * 2 for w, q in zip(ws, qs)
+                              for j in range(world)])
+        sets.append((ins, _lib.ptr_array([o.data_ptr() for o in outs]),
+                     (ctypes.c_size_t * len(qs))(*qs), ws, outs))
+    us = timed(lambda i: lib.kf_bucket_reduce_batch(sets[i][0], world, sets[i][1], sets[i][2],
+                                                    len(qs), 0x20209, KF_SUM, world, sp), nsets)
+    ok = True
+    for w, o, q in zip(sets[0][3], sets[0][4], qs):
+        acc = w[:q].float()
+        for j in range(1, world):
+            acc = acc + w[j * q:(j + 1) * q].float()  # fp32 accumulation, rank order
+        ok = ok and torch.equal(o, (acc / world).bfloat16())
+    report("c5_a2a_fold_n8_bf16", per_set, us, ok,
+           "C5 at N=8: kf_bucket_reduce_batch, k=8 received bf16 shards per bucket "
+           "(%d buckets, shards of %.2f MiB), rank-order fold, /8 fused" %
+           (len(qs), qs[0] * 2 / 2**20), len(qs))
+    del sets
+    torch.cuda.empty_cache()
+
+    def shard_div(name, counts, what):
+        qs = [c // world for c in counts]
+        per_set = sum(2 * q * 4 for q in qs)
+        nsets = max(2, -(-(768 << 20) // per_set))
+        sets = []
+        for _ in range(nsets):
+            bs = [torch.randn(c, device=dev, generator=g) for c in counts]
+            shard = [b[q * 3:q * 4] for b, q in zip(bs, qs)]  # rank 3's shard
+            ptrs = _lib.ptr_array([s.data_ptr() for s in shard])
+            sets.append((ptrs, (ctypes.c_size_t * len(qs))(*qs), bs, shard))
+        ref = [s.clone() for s in sets[0][3]]
+        _lib.check(lib.kf_bucket_reduce_batch(sets[0][0], 1, sets[0][0], sets[0][1], len(qs),
+                                              KF_FLOAT, KF_SUM, world, sp), name)
+        ok = all(torch.equal(s, r / torch.full_like(r, float(world)))
+                 for s, r in zip(sets[0][3], ref))
+        us = timed(lambda i: lib.kf_bucket_reduce_batch(sets[i][0], 1, sets[i][0], sets[i][1],
+                                                        len(qs), KF_FLOAT, KF_SUM, world, sp),
+                   nsets)
+        report(name, per_set, us, ok, what % (len(qs), qs[0] * 4 / 2**20), len(qs))
+        del sets, ref
+        torch.cuda.empty_cache()
+
+    rn = GradBuckets(models["resnet50-imagenet"], torch.float32, dev, world, n_buckets=16)
+    shard_div("c4_shard_div_n8_f32", [b.numel() for b in rn.buckets],
+              "C4 at N=8: kf_bucket_reduce_batch k=1, in-place /8 of each bucket's shard "
+              "after the reduce-scatter (%d shards of %.2f MiB)")
+    del rn
+    shard_div("c3_shard_div_n8_f32", [1 << 20] * 64,
+              "C3 at N=8: kf_bucket_reduce_batch k=1, in-place /8 of each 4 MiB bucket's "
+              "shard after the reduce-scatter (%d shards of %.2f MiB)")
     return out
 
 
@@ -700,9 +802,10 @@ def main():
         gb.views[0].copy_(x)
         step_s = _timed(lambda: prim_ex.all_reduce_(pieces, average=True, coalesce=coalesce),
                         args.steps, args.warmup, dev, world)
-        value = world * s_bytes / step_s / 2**30
+        value = s_bytes / step_s / 2**30  # per GPU, as the metric says
         busbw = 2 * (world - 1) / world * s_bytes / step_s / 1e9
         _progress(rank, "C3 %.3f ms per step" % (step_s * 1e3))
+        out["value_aggregate"] = round(world * value, 3)
         out["collective"] = {
             "busbw_GBps": round(busbw, 2),
             "algbw_GiBps_per_gpu": round(s_bytes / step_s / 2**30, 3),
@@ -840,9 +943,10 @@ def _result(args, world, sets, s_bytes, n, hot_s, prim):
         },
         "note": ("BASELINE configs: N = 1 times the local two-input reduce (C2, HBM-bound); "
                  "N > 1 times the S-SGD all-reduce of 64 x 4 MiB buckets over xGMI (C3, "
-                 "link-bound), value = N x bucket bytes / step; the two are different steps, so "
-                 "value(N) / (N x value(1)) is the exchange's cost relative to one local "
-                 "reduce, not a scaling efficiency of one kernel (DESIGN.md section 7); "
+                 "link-bound). value is per GPU at every N (the metric's unit): bucket bytes "
+                 "/ step; value_aggregate = N x value is the whole job. The two steps differ, "
+                 "so value(N) / value(1) is the exchange's cost relative to one local reduce, "
+                 "not a scaling efficiency of one kernel (DESIGN.md section 7); "
                  "collective.frac_of_xgmi grades the N > 1 step against its own bound"),
         "roofline": {
             "bound": "hbm",

@@ -503,19 +503,76 @@ int kf_exchange_info(kf_exchange_t *ex, int *rank, int *world, int *device);
 void kf_exchange_destroy(kf_exchange_t *ex);
 const char *kf_exchange_last_error(void);
 
-/* Loopback transport, for testing the exchange on ONE device: a group of
- * `world` ranks that are threads of one process (RCCL refuses two ranks on
- * one GPU). Each rank's exchange runs the same code as over RCCL — shards,
- * tails, workspace, batched folds, scheduler — with every collective a
- * rendezvous of the ranks' threads that moves the bytes with hipMemcpy (the
- * reduce-scatter folds in rank order on the host; no f16/bf16 reduce-scatter).
- * Every rank's calls must come from its own thread. */
-#pragma GCC visibility pop
-typedef struct kf_loopback kf_loopback_t; /* opaque */
-#pragma GCC visibility push(default)
-kf_loopback_t *kf_loopback_create(int world);
-void kf_loopback_destroy(kf_loopback_t *g);
-kf_exchange_t *kf_exchange_create_loopback(kf_loopback_t *g, int rank, int device);
+/* Name-keyed all-reduce: GoKungfuAllReduce(send, recv, count, dtype, op,
+ * name, done) (srcs/go/libkungfu-comm/collective.go:34-45) on the exchange.
+ * Each rank may start its names in ANY order, from any thread: tensors pair
+ * by name across ranks, as the reference's per-name mailbox pairs messages
+ * (srcs/go/rchannel/handler/collective.go:48-64), not by call order. An
+ * exchange thread agrees the issue order with the peers in negotiation
+ * cycles (one all-gather of the newly started names per cycle over a second
+ * communicator split off at the first call, so negotiating never waits
+ * behind queued data collectives); a name is issued once every rank started
+ * it, in rank 0's start order, and names that become ready in one cycle with
+ * the same dtype / op / average / algo go out as ONE batched call (grouped
+ * RCCL phases, one HIP launch). The data moves on the exchange's own stream
+ * after the work queued on `stream` before this call; done(status, arg)
+ * runs once the all-reduce finished on the device (kf_exchange_last_error
+ * inside done gives a failure's message). A name may be outstanding once per
+ * rank; count, dtype, op and average must agree across ranks (a mismatch
+ * fails that name with KF_ERR_ARG on every rank). Do not interleave these
+ * with the ordered calls above on one exchange. */
+int kf_exchange_all_reduce_named(kf_exchange_t *ex, const char *name, const void *send, void *recv,
+                                 size_t count, KungFu_Datatype dt, KungFu_Op op, int average,
+                                 int algo, void *stream, kf_done_fn done, void *arg);
+/* Block until every name started so far on this rank has completed; the
+ * first failure since the previous wait (message in kf_exchange_last_error),
+ * else KF_OK. Destroy an exchange only after this returned. */
+int kf_exchange_wait_named(kf_exchange_t *ex);
+
+/* ---- exchange transports ---------------------------------------------------
+ * The exchange issues five collectives and moves every byte through them; a
+ * transport is the table of those collectives bound to one communicator.
+ * kf_exchange_create binds the built-in librccl transport (RCCL over xGMI).
+ * kf_exchange_create_transport binds any other one — a host's own collective
+ * library, or a stand-in that lets the exchange's multi-rank logic run where
+ * RCCL cannot (several ranks on one device; tests/c/kf_testing.cpp). Every
+ * function queues its work on `stream` (a hipStream_t) in call order and
+ * returns 0, or a transport code that error_string explains. The calls
+ * between group_start and group_end belong to one phase and may be fused.
+ * reduce_scatter sums count elements per rank (op, dt as the exchange's own
+ * kernels define them) and may refuse a dtype with a non-zero code; the
+ * AUTO algo never asks for an f16 / bf16 / u16 / i16 reduce-scatter. split
+ * (ncclCommSplit's contract: collective over comm; ranks of one color form a
+ * communicator ordered by key) is needed by kf_exchange_split and the named
+ * all-reduce. The table must outlive every exchange bound to it; the
+ * exchange owns `comm` and releases it with destroy. */
+typedef struct kf_transport_ops {
+    int (*group_start)(void *comm);
+    int (*group_end)(void *comm);
+    int (*reduce_scatter)(const void *send, void *recv, size_t count, KungFu_Datatype dt,
+                          KungFu_Op op, void *comm, void *stream);
+    int (*all_gather)(const void *send, void *recv, size_t bytes, void *comm, void *stream);
+    int (*all_to_all)(const void *send, void *recv, size_t bytes, void *comm, void *stream);
+    int (*broadcast)(const void *send, void *recv, size_t bytes, int root, void *comm,
+                     void *stream);
+    int (*split)(void *comm, int color, int key, void **newcomm);
+    int (*async_error)(void *comm);
+    void (*destroy)(void *comm);
+    const char *(*error_string)(int code);
+} kf_transport_ops;
+/* An exchange of rank `rank` of `world` on HIP device `device` over `ops`
+ * bound to `comm` (ownership passes to the exchange; on failure the caller
+ * keeps it). A one-rank exchange over a transport still calls it (only the
+ * built-in RCCL transport short-cuts world 1 to a copy). */
+kf_exchange_t *kf_exchange_create_transport(const kf_transport_ops *ops, void *comm, int rank,
+                                            int world, int device);
+/* gpu_collective::new_local / new_group (srcs/cpp/src/nccl/gpu_collective.cpp:
+ * 202-243): a new exchange over the ranks of `ex` that pass the same color,
+ * ranked by key (ties by rank), on the same device. Collective over `ex`:
+ * every rank calls it at the same point of its call sequence. color < 0:
+ * this rank joins none (returns NULL with KF_OK in *status). The local scope
+ * is color = host index, key = rank (kf_exchange_create_local). */
+kf_exchange_t *kf_exchange_split(kf_exchange_t *ex, int color, int key, int *status);
 
 #pragma GCC visibility pop
 

@@ -81,9 +81,10 @@ EXPORTED = (
     "kf_exchange_info",
     "kf_exchange_destroy",
     "kf_exchange_last_error",
-    "kf_loopback_create",
-    "kf_loopback_destroy",
-    "kf_exchange_create_loopback",
+    "kf_exchange_all_reduce_named",
+    "kf_exchange_wait_named",
+    "kf_exchange_create_transport",
+    "kf_exchange_split",
 )
 
 STATUS = {
@@ -297,12 +298,16 @@ def load():
     lib.kf_exchange_destroy.restype = None
     lib.kf_exchange_last_error.argtypes = []
     lib.kf_exchange_last_error.restype = ctypes.c_char_p
-    lib.kf_loopback_create.argtypes = [c_int]
-    lib.kf_loopback_create.restype = c_void_p
-    lib.kf_loopback_destroy.argtypes = [c_void_p]
-    lib.kf_loopback_destroy.restype = None
-    lib.kf_exchange_create_loopback.argtypes = [c_void_p, c_int, c_int]
-    lib.kf_exchange_create_loopback.restype = c_void_p
+    lib.kf_exchange_all_reduce_named.argtypes = [c_void_p, ctypes.c_char_p, c_void_p, c_void_p,
+                                                 c_size_t, c_int, c_int, c_int, c_int, c_void_p,
+                                                 DONE_FN, c_void_p]
+    lib.kf_exchange_all_reduce_named.restype = c_int
+    lib.kf_exchange_wait_named.argtypes = [c_void_p]
+    lib.kf_exchange_wait_named.restype = c_int
+    lib.kf_exchange_create_transport.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int]
+    lib.kf_exchange_create_transport.restype = c_void_p
+    lib.kf_exchange_split.argtypes = [c_void_p, c_int, c_int, P(c_int)]
+    lib.kf_exchange_split.restype = c_void_p
     _lib = lib
     return lib
 

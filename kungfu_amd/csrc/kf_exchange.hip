@@ -1,4 +1,4 @@
-// kf_exchange.hip — the multi-GPU bucket exchange over RCCL behind the C ABI
+// kf_exchange.hip — the multi-GPU bucket exchange behind the C ABI
 // (include/kungfu_amd.h, "multi-GPU exchange").
 //
 // Reference: srcs/cpp/src/nccl/gpu_collective.cpp. There, one communicator per
@@ -10,28 +10,43 @@
 // Here a bucket's all-reduce is split so that the element-wise sum is the
 // build's HIP kernel where the semantics call for it (north_star: RCCL
 // reduce-scatter + all-gather over xGMI):
-//   reduce-scatter algo: ncclReduceScatter -> kf_bucket_div on the shard ->
-//                        in-place ncclAllGather;
-//   all-to-all algo:     ncclAllToAll of the shards -> HIP k-input fold of
-//                        the received shards in rank order (/np fused) ->
-//                        in-place ncclAllGather. Same xGMI bytes as the
+//   reduce-scatter algo: reduce-scatter -> kf_bucket_div on the shard ->
+//                        in-place all-gather;
+//   all-to-all algo:     all-to-all of the shards -> HIP k-input fold of the
+//                        received shards in rank order (/np fused) ->
+//                        in-place all-gather. Same xGMI bytes as the
 //                        reduce-scatter ((w-1)/w of the bucket out and in per
 //                        rank), one extra HBM pass over the received shards,
 //                        and the result is the oracle's rank-order fold for
 //                        every dtype (bf16: fp32 accumulation, one rounding).
-// Many buckets go in ONE call: every phase is one ncclGroupStart/End (RCCL
-// fuses the group into one launch) and all shard epilogues are one batched
-// HIP launch (kf_bucket_reduce_batch), so 64 x 4 MiB buckets cost 3 launches.
+// Many buckets go in ONE call: every phase is one group (RCCL fuses the group
+// into one launch) and all shard epilogues are one batched HIP launch
+// (kf_bucket_reduce_batch), so 64 x 4 MiB buckets cost 3 launches.
 //
-// librccl is opened at run time (dlopen "librccl.so.1"): the B1 drop-in does
-// not need it, and in a process where torch already loaded its RCCL (same
-// soname) both use that one library.
+// The bytes move through a transport (kf_transport_ops): the built-in one is
+// librccl, opened at run time (dlopen "librccl.so.1": the B1 drop-in does not
+// need it, and in a process where torch already loaded its RCCL, same soname,
+// both use that one library). Hosts may bind another (kf_exchange_create_
+// transport); the test library's in-process loopback is one.
+//
+// Three ways to issue:
+//   direct        kf_exchange_all_reduce(_batch) / _sma_batch: every rank calls
+//                 in the same order (RCCL's rule);
+//   ordered       kf_exchange_begin_step / start: NCCLScheduler's fixed name
+//                 list per step (scheduler.cpp:37-119);
+//   name-keyed    kf_exchange_all_reduce_named: ranks start names in any
+//                 order and tensors pair by name, as KungFu's own all-reduce
+//                 pairs messages by name (rchannel/handler/collective.go:
+//                 48-64). A negotiation thread agrees the issue order with
+//                 the peers in cycles over a split-off control communicator.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
@@ -77,8 +92,8 @@ struct Rccl {
     decltype(&::ncclGetUniqueId) GetUniqueId             = nullptr;
     decltype(&::ncclCommInitRank) CommInitRank           = nullptr;
     decltype(&::ncclCommDestroy) CommDestroy             = nullptr;
-    decltype(&::ncclCommAbort) CommAbort                 = nullptr;
     decltype(&::ncclCommGetAsyncError) CommGetAsyncError = nullptr;
+    decltype(&::ncclCommSplit) CommSplit                 = nullptr;
     decltype(&::ncclReduceScatter) ReduceScatter         = nullptr;
     decltype(&::ncclAllGather) AllGather                 = nullptr;
     decltype(&::ncclAllToAll) AllToAll                   = nullptr;
@@ -108,8 +123,8 @@ const Rccl &rccl()
         KF_LOAD(GetUniqueId, ncclGetUniqueId)
         KF_LOAD(CommInitRank, ncclCommInitRank)
         KF_LOAD(CommDestroy, ncclCommDestroy)
-        KF_LOAD(CommAbort, ncclCommAbort)
         KF_LOAD(CommGetAsyncError, ncclCommGetAsyncError)
+        KF_LOAD(CommSplit, ncclCommSplit)
         KF_LOAD(ReduceScatter, ncclReduceScatter)
         KF_LOAD(AllGather, ncclAllGather)
         KF_LOAD(AllToAll, ncclAllToAll)
@@ -203,219 +218,83 @@ ncclRedOp_t nccl_op(KungFu_Op op)
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-// Testing only: KUNGFU_AMD_EXCHANGE_W1_COLLECTIVES=1 sends a one-rank
-// exchange through the RCCL calls and the batched epilogue instead of the
-// identity copy, so a one-GPU box exercises librccl's own entry points with
-// the exchange's exact arguments (RCCL refuses two ranks on one device).
-bool w1_collectives()
-{
-    static const bool on = [] {
-        const char *e = std::getenv("KUNGFU_AMD_EXCHANGE_W1_COLLECTIVES");
-        return e && e[0] == '1';
-    }();
-    return on;
-}
-
 // ---------------------------------------------------------------------------
-// Loopback transport (testing): the RCCL entry points the exchange uses,
-// re-implemented for `world` ranks that are threads of ONE process on ONE
-// device, so the sharding, tails, workspace and fold logic of every world
-// size runs on a single GPU (RCCL itself refuses two ranks on one device).
-// Every collective is a rendezvous: each rank synchronises its stream and
-// posts its buffers; the last to arrive moves the bytes (hipMemcpy, and for
-// the reduce-scatter a host fold in rank order) and releases the others.
+// the built-in transport: librccl
 // ---------------------------------------------------------------------------
-struct LoopSlot {
-    int arrived = 0, left = 0;
-    bool done   = false;
-    std::vector<const void *> send;
-    std::vector<void *> recv;
-};
+ncclComm_t C(void *comm) { return static_cast<ncclComm_t>(comm); }
+hipStream_t S(void *stream) { return static_cast<hipStream_t>(stream); }
 
-struct LoopGroup {
-    int world;
-    std::mutex mu;
-    std::condition_variable cv;
-    std::map<uint64_t, LoopSlot> slots;
-    explicit LoopGroup(int w) : world(w) {}
-};
-
-struct LoopComm {
-    LoopGroup *g;
-    int rank;
-    uint64_t seq = 0;
-};
-
-size_t nccl_size(ncclDataType_t t)
+int rccl_group_start(void *) { return rccl().GroupStart(); }
+int rccl_group_end(void *) { return rccl().GroupEnd(); }
+int rccl_reduce_scatter(const void *send, void *recv, size_t count, KungFu_Datatype dt,
+                        KungFu_Op op, void *comm, void *stream)
 {
-    switch (t) {
-    case ncclInt8: case ncclUint8: return 1;
-    case ncclFloat16: case ncclBfloat16: return 2;
-    case ncclInt32: case ncclUint32: case ncclFloat32: return 4;
-    case ncclInt64: case ncclUint64: case ncclFloat64: return 8;
-    default: return 0;
-    }
+    ncclDataType_t t;
+    if (!nccl_type(dt, &t)) return ncclInvalidArgument;
+    return rccl().ReduceScatter(send, recv, count, t, nccl_op(op), C(comm), S(stream));
 }
-
-template <typename T>
-void host_fold(const std::vector<std::vector<char>> &in, size_t off, size_t n, ncclRedOp_t op,
-               char *out)
+int rccl_all_gather(const void *send, void *recv, size_t bytes, void *comm, void *stream)
 {
-    for (size_t i = 0; i < n; ++i) {
-        T a = reinterpret_cast<const T *>(in[0].data() + off)[i];
-        for (size_t j = 1; j < in.size(); ++j) {
-            const T b = reinterpret_cast<const T *>(in[j].data() + off)[i];
-            if (op == ncclSum) a = static_cast<T>(a + b);
-            else if (op == ncclProd) a = static_cast<T>(a * b);
-            else if (op == ncclMin) a = (b < a) ? b : a;
-            else a = (a < b) ? b : a;
-        }
-        reinterpret_cast<T *>(out)[i] = a;
-    }
+    return rccl().AllGather(send, recv, bytes, ncclUint8, C(comm), S(stream));
 }
-
-// rendezvous; `move` runs once, on the last rank to arrive, with every
-// rank's posted buffers
-template <typename F>
-ncclResult_t loop_collective(ncclComm_t comm, const void *send, void *recv, hipStream_t s, F move)
+int rccl_all_to_all(const void *send, void *recv, size_t bytes, void *comm, void *stream)
 {
-    auto *c = reinterpret_cast<LoopComm *>(comm);
-    if (hipStreamSynchronize(s) != hipSuccess) return ncclUnhandledCudaError;
-    LoopGroup *g = c->g;
-    std::unique_lock<std::mutex> lk(g->mu);
-    LoopSlot &sl = g->slots[c->seq];
-    const uint64_t seq = c->seq++;
-    if (sl.send.empty()) {
-        sl.send.assign(g->world, nullptr);
-        sl.recv.assign(g->world, nullptr);
-    }
-    sl.send[c->rank] = send;
-    sl.recv[c->rank] = recv;
-    ncclResult_t rc = ncclSuccess;
-    if (++sl.arrived == g->world) {
-        rc      = move(sl.send, sl.recv);
-        sl.done = true;
-        g->cv.notify_all();
-    } else {
-        g->cv.wait(lk, [&] { return sl.done; });
-    }
-    if (++sl.left == g->world) g->slots.erase(seq);
-    return rc;
+    return rccl().AllToAll(send, recv, bytes, ncclUint8, C(comm), S(stream));
 }
-
-ncclResult_t loop_reduce_scatter(const void *send, void *recv, size_t count, ncclDataType_t t,
-                                 ncclRedOp_t op, ncclComm_t comm, hipStream_t s)
+int rccl_broadcast(const void *send, void *recv, size_t bytes, int root, void *comm, void *stream)
 {
-    return loop_collective(comm, send, recv, s, [&](const std::vector<const void *> &sd,
-                                                     const std::vector<void *> &rv) {
-        const size_t sz = nccl_size(t), W = sd.size();
-        if (sz == 0 || t == ncclFloat16 || t == ncclBfloat16) return ncclInvalidArgument;
-        std::vector<std::vector<char>> in(W, std::vector<char>(count * W * sz));
-        for (size_t j = 0; j < W; ++j) {
-            if (hipMemcpy(in[j].data(), sd[j], count * W * sz, hipMemcpyDeviceToHost) != hipSuccess)
-                return ncclUnhandledCudaError;
-        }
-        std::vector<char> out(count * sz);
-        for (size_t r = 0; r < W; ++r) {
-            const size_t off = r * count * sz;
-            switch (t) {
-            case ncclInt8: host_fold<int8_t>(in, off, count, op, out.data()); break;
-            case ncclUint8: host_fold<uint8_t>(in, off, count, op, out.data()); break;
-            case ncclInt32: host_fold<int32_t>(in, off, count, op, out.data()); break;
-            case ncclUint32: host_fold<uint32_t>(in, off, count, op, out.data()); break;
-            case ncclInt64: host_fold<int64_t>(in, off, count, op, out.data()); break;
-            case ncclUint64: host_fold<uint64_t>(in, off, count, op, out.data()); break;
-            case ncclFloat32: host_fold<float>(in, off, count, op, out.data()); break;
-            default: host_fold<double>(in, off, count, op, out.data()); break;
-            }
-            if (hipMemcpy(rv[r], out.data(), count * sz, hipMemcpyHostToDevice) != hipSuccess)
-                return ncclUnhandledCudaError;
-        }
-        return ncclSuccess;
-    });
+    return rccl().Broadcast(send, recv, bytes, ncclUint8, root, C(comm), S(stream));
 }
-
-ncclResult_t loop_all_gather(const void *send, void *recv, size_t count, ncclDataType_t t,
-                             ncclComm_t comm, hipStream_t s)
+int rccl_split(void *comm, int color, int key, void **newcomm)
 {
-    return loop_collective(comm, send, recv, s, [&](const std::vector<const void *> &sd,
-                                                     const std::vector<void *> &rv) {
-        const size_t b = count * nccl_size(t), W = sd.size();
-        for (size_t r = 0; r < W; ++r) {
-            for (size_t j = 0; j < W; ++j) {
-                char *dst = static_cast<char *>(rv[r]) + j * b;
-                if (dst == sd[j]) continue;  // in place
-                if (hipMemcpy(dst, sd[j], b, hipMemcpyDeviceToDevice) != hipSuccess)
-                    return ncclUnhandledCudaError;
-            }
-        }
-        return ncclSuccess;
-    });
-}
-
-ncclResult_t loop_all_to_all(const void *send, void *recv, size_t count, ncclDataType_t t,
-                             ncclComm_t comm, hipStream_t s)
-{
-    return loop_collective(comm, send, recv, s, [&](const std::vector<const void *> &sd,
-                                                     const std::vector<void *> &rv) {
-        const size_t b = count * nccl_size(t), W = sd.size();
-        for (size_t r = 0; r < W; ++r) {
-            for (size_t j = 0; j < W; ++j) {
-                if (hipMemcpy(static_cast<char *>(rv[r]) + j * b,
-                              static_cast<const char *>(sd[j]) + r * b, b,
-                              hipMemcpyDeviceToDevice) != hipSuccess)
-                    return ncclUnhandledCudaError;
-            }
-        }
-        return ncclSuccess;
-    });
-}
-
-ncclResult_t loop_broadcast(const void *send, void *recv, size_t count, ncclDataType_t t, int root,
-                            ncclComm_t comm, hipStream_t s)
-{
-    return loop_collective(comm, send, recv, s, [&](const std::vector<const void *> &sd,
-                                                     const std::vector<void *> &rv) {
-        const size_t b = count * nccl_size(t);
-        for (size_t r = 0; r < rv.size(); ++r) {
-            if (rv[r] == sd[root]) continue;
-            if (hipMemcpy(rv[r], sd[root], b, hipMemcpyDeviceToDevice) != hipSuccess)
-                return ncclUnhandledCudaError;
-        }
-        return ncclSuccess;
-    });
-}
-
-ncclResult_t loop_nop() { return ncclSuccess; }
-ncclResult_t loop_async_error(ncclComm_t, ncclResult_t *e)
-{
-    *e = ncclSuccess;
-    return ncclSuccess;
-}
-ncclResult_t loop_destroy(ncclComm_t comm)
-{
-    delete reinterpret_cast<LoopComm *>(comm);
-    return ncclSuccess;
-}
-const char *loop_error_string(ncclResult_t) { return "loopback transport error"; }
-
-const Rccl &loop_rccl()
-{
-    static const Rccl r = [] {
-        Rccl x;
-        x.CommDestroy       = loop_destroy;
-        x.CommGetAsyncError = loop_async_error;
-        x.ReduceScatter     = loop_reduce_scatter;
-        x.AllGather         = loop_all_gather;
-        x.AllToAll          = loop_all_to_all;
-        x.Broadcast         = loop_broadcast;
-        x.GroupStart        = loop_nop;
-        x.GroupEnd          = loop_nop;
-        x.GetErrorString    = loop_error_string;
-        x.ok                = true;
-        return x;
-    }();
+    ncclComm_t n = nullptr;
+    const ncclResult_t r =
+        rccl().CommSplit(C(comm), color < 0 ? NCCL_SPLIT_NOCOLOR : color, key, &n, nullptr);
+    *newcomm = n;
     return r;
+}
+int rccl_async_error(void *comm)
+{
+    ncclResult_t ae = ncclSuccess;
+    const ncclResult_t r = rccl().CommGetAsyncError(C(comm), &ae);
+    return r != ncclSuccess ? r : ae;
+}
+void rccl_destroy(void *comm) { (void)rccl().CommDestroy(C(comm)); }
+const char *rccl_error_string(int code)
+{
+    return rccl().ok ? rccl().GetErrorString(static_cast<ncclResult_t>(code)) : "RCCL unavailable";
+}
+
+const kf_transport_ops kRcclOps = {
+    rccl_group_start, rccl_group_end, rccl_reduce_scatter, rccl_all_gather, rccl_all_to_all,
+    rccl_broadcast,   rccl_split,     rccl_async_error,    rccl_destroy,    rccl_error_string,
+};
+
+// ---------------------------------------------------------------------------
+// name-keyed negotiation: one control-row per rank per cycle
+// ---------------------------------------------------------------------------
+struct CtrlEntry {
+    uint64_t h1, h2, count;
+    uint32_t sig, pad;
+};
+static_assert(sizeof(CtrlEntry) == 32, "control entry");
+constexpr size_t kCtrlRow = 4096;                        // bytes per rank per cycle
+constexpr int kCtrlMax    = kCtrlRow / sizeof(CtrlEntry) - 1;  // entry 0 is the header
+
+uint64_t fnv1a(const char *s, uint64_t basis)
+{
+    uint64_t h = basis;
+    for (; *s; ++s) {
+        h ^= static_cast<unsigned char>(*s);
+        h *= 0x100000001b3ull;
+    }
+    return h;
+}
+
+uint32_t task_sig(KungFu_Datatype dt, KungFu_Op op, int average, int algo)
+{
+    return (static_cast<uint32_t>(dt) << 8) ^ (static_cast<uint32_t>(op) << 4) ^
+           (static_cast<uint32_t>(average != 0) << 3) ^ static_cast<uint32_t>(algo);
 }
 
 }  // namespace
@@ -441,11 +320,28 @@ struct Done {
     kf_done_fn done;
     void *arg;
     int status;
+    hipEvent_t ready = nullptr;  // named tasks: the start event, destroyed here
+    std::string why;             // named tasks: the failure's message
+};
+
+struct NamedTask {
+    std::string name;
+    uint64_t h1 = 0, h2 = 0;
+    const void *send = nullptr;
+    void *recv       = nullptr;
+    size_t count     = 0;
+    KungFu_Datatype dt;
+    KungFu_Op op;
+    int average = 0, algo = 0;
+    hipEvent_t ready = nullptr;
+    kf_done_fn done  = nullptr;
+    void *arg        = nullptr;
 };
 
 struct kf_exchange {
-    const Rccl *R   = nullptr;  // librccl, or the loopback transport
-    ncclComm_t comm = nullptr;
+    const kf_transport_ops *T = nullptr;  // librccl, or a host's transport
+    void *comm                = nullptr;
+    bool builtin              = false;    // the RCCL transport (world-1 shortcut)
     int rank = 0, world = 1, device = 0;
     std::mutex mu;  // one collective sequence at a time
 
@@ -455,10 +351,10 @@ struct kf_exchange {
     hipEvent_t ws_ev    = nullptr;
     hipStream_t ws_last = nullptr;
     bool ws_used        = false;
-    hipStream_t own     = nullptr;  // internal (order broadcast)
+    hipStream_t own     = nullptr;  // internal (order broadcast, split)
 
     // pipelined schedule (kf_exchange_set_pipeline): the buckets of a call in
-    // `groups` groups; RCCL phases on the caller's stream, the element-wise
+    // `groups` groups; collectives on the caller's stream, the element-wise
     // work (folds, /np, SMA blends) on `comp`, so group g's HIP work runs
     // while group g+1's collectives move bytes
     int groups         = 1;
@@ -479,6 +375,30 @@ struct kf_exchange {
     std::deque<Done> cq;
     std::thread issuer, completer;
 
+    // name-keyed all-reduce (kf_exchange_all_reduce_named)
+    std::mutex nmu;
+    std::condition_variable ncv;
+    std::map<std::string, NamedTask> nwait;  // started here, not yet issued
+    std::deque<std::string> nfresh;          // started, not yet reported to the peers
+    std::map<std::pair<uint64_t, uint64_t>, std::string> nhash;  // outstanding names
+    size_t nstarted = 0, nfinished = 0;
+    int nstatus      = KF_OK;
+    std::string nerr;
+    bool nstop = false, nbroken = false, nready = false;
+    std::deque<Done> ndq;
+    std::thread negotiator, nfinisher;
+    kf_exchange *ctrl   = nullptr;  // the control communicator (split off)
+    hipStream_t nstream = nullptr;  // the named tasks' data stream
+    hipStream_t cstream = nullptr;  // the control all-gathers
+    bool ntrace         = false;    // KUNGFU_AMD_TRACE_NAMED=1: every issued batch to stderr
+    void *cdev = nullptr, *chost = nullptr;  // [row | W rows], device and page-locked
+
+    int tfail(int code, const std::string &what) const
+    {
+        const char *why = T && T->error_string ? T->error_string(code) : nullptr;
+        return fail(KF_ERR_RCCL, what + ": " + (why ? why : "transport error") + " (" +
+                                     std::to_string(code) + ")");
+    }
     int ensure_ws(size_t bytes, hipStream_t s);
     void release_ws(hipStream_t s);
     // sma_alpha != nullptr: SMA, sends = the variables, recvs = the sum workspaces,
@@ -486,10 +406,38 @@ struct kf_exchange {
     int batch(const void *const *sends, void *const *recvs, const size_t *counts, int nb,
               KungFu_Datatype dt, KungFu_Op op, int average, int algo, hipStream_t s,
               const double *sma_alpha = nullptr);
+    kf_exchange *split(int color, int key, int *status);  // caller holds mu
+    int start_named();                                     // caller holds mu
     void issue_loop();
     void complete_loop();
+    void negotiate_loop();
+    void finish_loop();
+    void fail_outstanding(int rc, const std::string &why);
     ~kf_exchange();
 };
+
+namespace
+{
+kf_exchange *new_exchange(const kf_transport_ops *T, void *comm, bool builtin, int rank, int world,
+                          int device)
+{
+    auto *ex    = new kf_exchange;
+    ex->T       = T;
+    ex->comm    = comm;
+    ex->builtin = builtin;
+    ex->rank    = rank;
+    ex->world   = world;
+    ex->device  = device;
+    if (hipEventCreateWithFlags(&ex->ws_ev, hipEventDisableTiming) != hipSuccess ||
+        hipStreamCreateWithFlags(&ex->own, hipStreamNonBlocking) != hipSuccess) {
+        fail(KF_ERR_HIP, "exchange: event/stream");
+        ex->comm = nullptr;  // the caller keeps it
+        delete ex;
+        return nullptr;
+    }
+    return ex;
+}
+}  // namespace
 
 int kf_exchange::ensure_ws(size_t bytes, hipStream_t s)
 {
@@ -522,7 +470,7 @@ static int resolve_algo(int algo, KungFu_Datatype dt, KungFu_Op op, int world, i
     ncclDataType_t t;
     const bool rs_ok = nccl_type(dt, &t);
     if (algo == KF_ALGO_REDUCE_SCATTER) {
-        if (!rs_ok) return fail(KF_ERR_DTYPE, "no RCCL reduction type for this dtype");
+        if (!rs_ok) return fail(KF_ERR_DTYPE, "no reduce-scatter type for this dtype");
         *out = algo;
         return KF_OK;
     }
@@ -550,11 +498,10 @@ int kf_exchange::batch(const void *const *sends, void *const *recvs, const size_
                        int nb, KungFu_Datatype dt, KungFu_Op op, int average, int algo,
                        hipStream_t s, const double *sma_alpha)
 {
-    const Rccl &R = *this->R;
-    const int sz  = tsize(dt);
+    const int sz = tsize(dt);
     const int W = world, r = rank;
     const bool sma = sma_alpha != nullptr;
-    if (W == 1 && !w1_collectives()) {  // a single peer: the sum is the bucket, x / 1 == x
+    if (W == 1 && builtin) {  // a single peer: the sum is the bucket, x / 1 == x
         for (int b = 0; b < nb; ++b) {
             if (counts[b] && sends[b] != recvs[b]) {
                 KF_HIP(hipMemcpyAsync(recvs[b], sends[b], counts[b] * sz, hipMemcpyDeviceToDevice, s));
@@ -572,8 +519,6 @@ int kf_exchange::batch(const void *const *sends, void *const *recvs, const size_
     int a  = 0;
     int rc = resolve_algo(algo, dt, op, W, &a);
     if (rc != KF_OK) return rc;
-    ncclDataType_t nt = ncclUint8;
-    nccl_type(dt, &nt);
 
     // workspace: received shards (all-to-all) and gathered tails
     std::vector<size_t> wsoff(nb, 0), toff(nb, 0);
@@ -596,30 +541,31 @@ int kf_exchange::batch(const void *const *sends, void *const *recvs, const size_
     char *wsp = static_cast<char *>(ws);
 
     auto group_end = [&](int status) -> int {
-        ncclResult_t e = R.GroupEnd();
+        const int e = T->group_end(comm);
         if (status != KF_OK) return status;
-        if (e != ncclSuccess) return nccl_fail(e, "ncclGroupEnd");
+        if (e != 0) return tfail(e, "group_end");
         return KF_OK;
     };
 
     // phase 1: every bucket's reduce-scatter (or all-to-all) and tail gather
     auto phase1 = [&](int b0, int b1) -> int {
-        KF_NCCL(R.GroupStart());
+        const int e0 = T->group_start(comm);
+        if (e0 != 0) return tfail(e0, "group_start");
         int rc1 = KF_OK;
         for (int b = b0; b < b1 && rc1 == KF_OK; ++b) {
             const size_t q = counts[b] / W, t = counts[b] % W;
             const char *snd = static_cast<const char *>(sends[b]);
             char *rcv       = static_cast<char *>(recvs[b]);
-            ncclResult_t e  = ncclSuccess;
+            int e           = 0;
             if (q && a == KF_ALGO_REDUCE_SCATTER) {
-                e = R.ReduceScatter(snd, rcv + r * q * sz, q, nt, nccl_op(op), comm, s);
+                e = T->reduce_scatter(snd, rcv + r * q * sz, q, dt, op, comm, s);
             } else if (q) {
-                e = R.AllToAll(snd, wsp + wsoff[b], q * sz, ncclUint8, comm, s);
+                e = T->all_to_all(snd, wsp + wsoff[b], q * sz, comm, s);
             }
-            if (e == ncclSuccess && t) {
-                e = R.AllGather(snd + q * W * sz, wsp + toff[b], t * sz, ncclUint8, comm, s);
+            if (e == 0 && t) {
+                e = T->all_gather(snd + q * W * sz, wsp + toff[b], t * sz, comm, s);
             }
-            if (e != ncclSuccess) rc1 = nccl_fail(e, "phase-1 collective");
+            if (e != 0) rc1 = tfail(e, "phase-1 collective");
         }
         return group_end(rc1);
     };
@@ -673,14 +619,15 @@ int kf_exchange::batch(const void *const *sends, void *const *recvs, const size_
 
     // phase 3: in-place all-gather of every reduced shard
     auto phase3 = [&](int b0, int b1) -> int {
-        KF_NCCL(R.GroupStart());
+        const int e0 = T->group_start(comm);
+        if (e0 != 0) return tfail(e0, "group_start");
         int rc3 = KF_OK;
         for (int b = b0; b < b1 && rc3 == KF_OK; ++b) {
             const size_t q = counts[b] / W;
             if (!q) continue;
-            char *rcv      = static_cast<char *>(recvs[b]);
-            ncclResult_t e = R.AllGather(rcv + r * q * sz, rcv, q * sz, ncclUint8, comm, s);
-            if (e != ncclSuccess) rc3 = nccl_fail(e, "ncclAllGather");
+            char *rcv   = static_cast<char *>(recvs[b]);
+            const int e = T->all_gather(rcv + r * q * sz, rcv, q * sz, comm, s);
+            if (e != 0) rc3 = tfail(e, "all_gather");
         }
         return group_end(rc3);
     };
@@ -703,17 +650,16 @@ int kf_exchange::batch(const void *const *sends, void *const *recvs, const size_
         if (rc == KF_OK) rc = phase2(0, nb, s);
         if (rc == KF_OK) rc = phase3(0, nb);
         if (rc == KF_OK) rc = blend(0, nb, s);
-        if (rc != KF_OK) return rc;
-        if (need) release_ws(s);
-        return KF_OK;
+        if (need) release_ws(s);  // whatever ran reads the workspace in stream order
+        return rc;
     }
 
     // pipelined: groups of consecutive buckets with about equal bytes;
     //   caller stream s: p1(0) p1(1) [wait p2(0)] p3(0) p1(2) [wait p2(1)] p3(1) ...
     //   comp stream:     [wait p1(0)] p2(0) [wait p1(1)] p2(1) [wait p3(0)] blend(0) ...
     // every wait is on an event recorded earlier on the other stream, so
-    // neither stream can wait on the other in a cycle; the RCCL calls keep the
-    // same order on every rank
+    // neither stream can wait on the other in a cycle; the collectives keep
+    // the same order on every rank
     std::vector<int> gb(1, 0);  // group g = buckets [gb[g], gb[g+1])
     {
         size_t total = 0, acc = 0;
@@ -736,6 +682,7 @@ int kf_exchange::batch(const void *const *sends, void *const *recvs, const size_
     auto e2 = [&](int g) { return pev[3 * g + 1]; };
     auto e3 = [&](int g) { return pev[3 * g + 2]; };
     hipEvent_t e_end = pev[3 * ng];
+    bool comp_used   = false;
     auto finish = [&](int g) -> int {  // gather group g, then blend it
         KF_HIP(hipStreamWaitEvent(s, e2(g), 0));
         int f = phase3(gb[g], gb[g + 1]);
@@ -749,19 +696,82 @@ int kf_exchange::batch(const void *const *sends, void *const *recvs, const size_
         if (rc != KF_OK) break;
         KF_HIP(hipEventRecord(e1(g), s));
         KF_HIP(hipStreamWaitEvent(comp, e1(g), 0));
+        comp_used = true;
         rc = phase2(gb[g], gb[g + 1], comp);
         if (rc != KF_OK) break;
         KF_HIP(hipEventRecord(e2(g), comp));
         if (g > 0) rc = finish(g - 1);
     }
     if (rc == KF_OK) rc = finish(ng - 1);
-    if (rc == KF_OK && sma) {  // the caller's stream ends after the last blend
-        KF_HIP(hipEventRecord(e_end, comp));
-        KF_HIP(hipStreamWaitEvent(s, e_end, 0));
+    // the caller's stream ends after everything queued on comp (the last
+    // blend; after a failure, the folds already queued), so neither the
+    // workspace nor the buckets are reused under them
+    if (comp_used && (sma || rc != KF_OK)) {
+        if (hipEventRecord(e_end, comp) == hipSuccess) (void)hipStreamWaitEvent(s, e_end, 0);
     }
-    if (rc != KF_OK) return rc;
     if (need) release_ws(s);
-    return KF_OK;
+    return rc;
+}
+
+// A sub-communicator of the ranks that pass `color` (gpu_collective.cpp:
+// 202-243): the (color, key) of every rank are all-gathered first, so each
+// rank knows its place and the group's size without asking the transport.
+kf_exchange *kf_exchange::split(int color, int key, int *status)
+{
+    auto bad = [&](int rc) -> kf_exchange * {
+        *status = rc;
+        return nullptr;
+    };
+    if (!T->split) return bad(fail(KF_ERR_ARG, "the transport cannot split"));
+    const int W = world;
+    std::vector<int32_t> ck(2 * W, 0);
+    if (W > 1) {
+        int32_t *d = nullptr;
+        hipError_t e = hipMalloc(&d, sizeof(int32_t) * 2 * (W + 1));
+        if (e != hipSuccess) return bad(hip_fail(e, "split: hipMalloc"));
+        const int32_t mine[2] = {color, key};
+        int rc = KF_OK;
+        e = hipMemcpyAsync(d, mine, sizeof(mine), hipMemcpyHostToDevice, own);
+        if (e != hipSuccess) rc = hip_fail(e, "split: hipMemcpyAsync");
+        if (rc == KF_OK) {
+            const int t = T->all_gather(d, d + 2, sizeof(mine), comm, own);
+            if (t != 0) rc = tfail(t, "split: all_gather");
+        }
+        if (rc == KF_OK) {
+            e = hipMemcpyAsync(ck.data(), d + 2, sizeof(int32_t) * 2 * W, hipMemcpyDeviceToHost, own);
+            if (e == hipSuccess) e = hipStreamSynchronize(own);
+            if (e != hipSuccess) rc = hip_fail(e, "split: hipMemcpyAsync");
+        }
+        (void)hipFree(d);
+        if (rc != KF_OK) return bad(rc);
+    } else {
+        ck = {color, key};
+    }
+    // ranks of my color, ordered by (key, rank): ncclCommSplit's order
+    std::vector<std::pair<int32_t, int>> mem;
+    for (int j = 0; j < W; ++j) {
+        if (ck[2 * j] == color && color >= 0) mem.emplace_back(ck[2 * j + 1], j);
+    }
+    std::sort(mem.begin(), mem.end());
+    void *nc   = nullptr;
+    const int t = T->split(comm, color, key, &nc);
+    if (t != 0) return bad(tfail(t, "split"));
+    if (color < 0) {
+        *status = KF_OK;
+        return nullptr;
+    }
+    int nr = 0;
+    for (size_t i = 0; i < mem.size(); ++i) {
+        if (mem[i].second == rank) nr = static_cast<int>(i);
+    }
+    kf_exchange *ex = new_exchange(T, nc, builtin, nr, static_cast<int>(mem.size()), device);
+    if (!ex) {
+        T->destroy(nc);
+        return bad(KF_ERR_HIP);
+    }
+    ex->groups = groups;
+    *status    = KF_OK;
+    return ex;
 }
 
 // Issue thread: the tasks of the step, strictly in `order`
@@ -819,20 +829,279 @@ void kf_exchange::complete_loop()
             if (hipEventSynchronize(d.ev) != hipSuccess) rc = KF_ERR_HIP;
             (void)hipEventDestroy(d.ev);
         }
-        if (rc == KF_OK) {
-            ncclResult_t ae = ncclSuccess;
-            if (R->CommGetAsyncError(comm, &ae) != ncclSuccess || ae != ncclSuccess) {
-                rc = KF_ERR_RCCL;
-            }
-        }
+        if (rc == KF_OK && T->async_error(comm) != 0) rc = KF_ERR_RCCL;
         if (d.done) d.done(rc, d.arg);
         lk.lock();
         if (rc != KF_OK && sstatus == KF_OK) {
             sstatus = rc;
-            if (serr.empty()) serr = "an issued all-reduce failed on the device or in RCCL";
+            if (serr.empty()) serr = "an issued all-reduce failed on the device or in the transport";
         }
         ++completed;
         scv.notify_all();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// name-keyed all-reduce
+//
+// Every cycle, each rank that has work (names started and not yet issued)
+// all-gathers one control row over the control communicator: the names it
+// started since its last row (hash pair, count, dtype/op signature). Every
+// rank sees the same rows, so every rank counts the same reporters per name
+// and finds the same names complete (reported by all ranks) in the same
+// cycle; those are issued in rank 0's start order. A rank with nothing to do
+// does not enter a cycle: its peers wait in the all-gather until it starts a
+// name, which it must (same name set on every rank). Cycles that carry no
+// news back off (50 us doubling to 1 ms) until a local start arrives.
+// ---------------------------------------------------------------------------
+int kf_exchange::start_named()
+{
+    if (nready) return KF_OK;
+    if (world > 1) {
+        int st = KF_OK;
+        ctrl   = split(0, rank, &st);
+        if (!ctrl) return st != KF_OK ? st : fail(KF_ERR_RCCL, "control communicator");
+        KF_HIP(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
+        KF_HIP(hipMalloc(&cdev, kCtrlRow * (world + 1)));
+        KF_HIP(hipHostMalloc(&chost, kCtrlRow * (world + 1), hipHostMallocDefault));
+    }
+    KF_HIP(hipStreamCreateWithFlags(&nstream, hipStreamNonBlocking));
+    const char *tr = std::getenv("KUNGFU_AMD_TRACE_NAMED");
+    ntrace         = tr && tr[0] == '1';
+    nready     = true;
+    negotiator = std::thread([this] { negotiate_loop(); });
+    nfinisher  = std::thread([this] { finish_loop(); });
+    return KF_OK;
+}
+
+// every task still waiting fails (a broken control channel, or shutdown)
+void kf_exchange::fail_outstanding(int rc, const std::string &why)
+{
+    std::lock_guard<std::mutex> lk(nmu);
+    nbroken = true;
+    for (auto &kv : nwait) {
+        ndq.push_back(Done{nullptr, kv.second.done, kv.second.arg, rc, kv.second.ready, why});
+    }
+    nwait.clear();
+    nfresh.clear();
+    nhash.clear();
+    ncv.notify_all();
+}
+
+void kf_exchange::negotiate_loop()
+{
+    (void)hipSetDevice(device);
+    const int W = world;
+    struct Seen {
+        int n        = 0;
+        uint32_t sig = 0;
+        uint64_t count = 0, key0 = 0;
+        bool bad = false;
+    };
+    std::map<std::pair<uint64_t, uint64_t>, Seen> seen;
+    uint64_t cycle = 0;
+    int idle       = 0;
+    char *row      = static_cast<char *>(chost);
+    char *all      = row ? row + kCtrlRow : nullptr;
+    for (;;) {
+        std::vector<std::pair<uint64_t, uint64_t>> complete;
+        int sent = 0;
+        {
+            std::unique_lock<std::mutex> lk(nmu);
+            ncv.wait(lk, [&] { return nstop || !nfresh.empty() || !nwait.empty(); });
+            if (nstop) return;
+            if (idle > 0 && nfresh.empty()) {
+                const auto us = std::chrono::microseconds(std::min(1000, 50 << std::min(idle - 1, 5)));
+                ncv.wait_for(lk, us, [&] { return nstop || !nfresh.empty(); });
+                if (nstop) return;
+            }
+            if (W == 1) {  // nothing to agree: issue in start order
+                for (; !nfresh.empty(); nfresh.pop_front()) {
+                    const NamedTask &t = nwait.at(nfresh.front());
+                    complete.emplace_back(t.h1, t.h2);
+                }
+            } else {
+                auto *ent = reinterpret_cast<CtrlEntry *>(row);
+                for (; !nfresh.empty() && sent < kCtrlMax; nfresh.pop_front()) {
+                    const NamedTask &t = nwait.at(nfresh.front());
+                    ent[1 + sent++]    = CtrlEntry{t.h1, t.h2, t.count,
+                                                task_sig(t.dt, t.op, t.average, t.algo), 0};
+                }
+                ent[0] = CtrlEntry{static_cast<uint64_t>(sent), 0, 0, 0, 0};
+            }
+        }
+        bool news = !complete.empty();
+        if (W > 1) {
+            int rc        = KF_OK;
+            char *d       = static_cast<char *>(cdev);
+            hipError_t e  = hipMemcpyAsync(d, row, kCtrlRow, hipMemcpyHostToDevice, cstream);
+            if (e != hipSuccess) rc = hip_fail(e, "control row H2D");
+            if (rc == KF_OK) {
+                const int t = T->all_gather(d, d + kCtrlRow, kCtrlRow, ctrl->comm, cstream);
+                if (t != 0) rc = tfail(t, "control all_gather");
+            }
+            if (rc == KF_OK) {
+                e = hipMemcpyAsync(all, d + kCtrlRow, kCtrlRow * W, hipMemcpyDeviceToHost, cstream);
+                if (e == hipSuccess) e = hipStreamSynchronize(cstream);
+                if (e != hipSuccess) rc = hip_fail(e, "control rows D2H");
+            }
+            if (rc != KF_OK) {
+                fail_outstanding(rc, "name negotiation failed: " + t_ex_error);
+                return;
+            }
+            for (int j = 0; j < W; ++j) {
+                const auto *ent = reinterpret_cast<const CtrlEntry *>(all + j * kCtrlRow);
+                const int n     = static_cast<int>(std::min<uint64_t>(ent[0].h1, kCtrlMax));
+                news            = news || n > 0;
+                for (int i = 0; i < n; ++i) {
+                    const CtrlEntry &c = ent[1 + i];
+                    Seen &s            = seen[{c.h1, c.h2}];
+                    if (s.n == 0) {
+                        s.sig   = c.sig;
+                        s.count = c.count;
+                    } else if (s.sig != c.sig || s.count != c.count) {
+                        s.bad = true;
+                    }
+                    if (j == 0) s.key0 = cycle * (kCtrlMax + 1) + i;
+                    if (++s.n == W) complete.emplace_back(c.h1, c.h2);
+                }
+            }
+            if (ntrace) {
+                std::string line = "[kf named] rank " + std::to_string(rank) + " cycle " +
+                                   std::to_string(cycle) + " rows:";
+                for (int j = 0; j < W; ++j) {
+                    const auto *ent = reinterpret_cast<const CtrlEntry *>(all + j * kCtrlRow);
+                    line += " " + std::to_string(ent[0].h1);
+                    for (uint64_t i = 0; i < std::min<uint64_t>(ent[0].h1, kCtrlMax); ++i) {
+                        line += ":" + std::to_string(ent[1 + i].h1 % 1000);
+                    }
+                }
+                line += " complete " + std::to_string(complete.size()) + " seen " +
+                        std::to_string(seen.size());
+                std::fprintf(stderr, "%s\n", line.c_str());
+            }
+            // rank 0's start order (NCCLScheduler::Reset adopts rank 0's
+            // arrival order the same way, scheduler.cpp:96-118)
+            std::sort(complete.begin(), complete.end(), [&](const auto &x, const auto &y) {
+                return seen[x].key0 < seen[y].key0;
+            });
+            ++cycle;
+        }
+        idle = news ? 0 : idle + 1;
+        if (complete.empty()) continue;
+
+        // the completed tasks, in issue order
+        std::vector<NamedTask> ts;
+        std::vector<bool> bad;
+        {
+            std::lock_guard<std::mutex> lk(nmu);
+            for (const auto &h : complete) {
+                auto hn = nhash.find(h);
+                if (hn == nhash.end()) {  // cannot happen: this rank reported it
+                    std::fprintf(stderr, "[kf named] rank %d: completed name not outstanding\n",
+                                 rank);
+                    continue;
+                }
+                auto it = nwait.find(hn->second);
+                ts.push_back(it->second);
+                nwait.erase(it);
+                nhash.erase(hn);
+                auto sn = seen.find(h);
+                bad.push_back(sn != seen.end() && sn->second.bad);
+                if (sn != seen.end()) seen.erase(sn);
+            }
+        }
+        // runs of one dtype / op / average / algo go out as one batched call
+        for (size_t i = 0; i < ts.size();) {
+            if (bad[i]) {
+                std::lock_guard<std::mutex> lk(nmu);
+                ndq.push_back(Done{nullptr, ts[i].done, ts[i].arg, KF_ERR_ARG, ts[i].ready,
+                                   "named all-reduce '" + ts[i].name +
+                                       "': count, dtype, op or average differ across ranks"});
+                ncv.notify_all();
+                ++i;
+                continue;
+            }
+            size_t j = i + 1;
+            while (j < ts.size() && !bad[j] && ts[j].dt == ts[i].dt && ts[j].op == ts[i].op &&
+                   ts[j].average == ts[i].average && ts[j].algo == ts[i].algo) {
+                ++j;
+            }
+            std::vector<const void *> snd;
+            std::vector<void *> rcv;
+            std::vector<size_t> cnt;
+            int rc = KF_OK;
+            for (size_t k = i; k < j; ++k) {
+                if (hipStreamWaitEvent(nstream, ts[k].ready, 0) != hipSuccess && rc == KF_OK) {
+                    rc = fail(KF_ERR_HIP, "hipStreamWaitEvent(start)");
+                }
+                snd.push_back(ts[k].send);
+                rcv.push_back(ts[k].recv);
+                cnt.push_back(ts[k].count);
+            }
+            if (ntrace) {
+                std::string line = "[kf named] rank " + std::to_string(rank) + " cycle " +
+                                   std::to_string(cycle) + " batch:";
+                for (size_t k = i; k < j; ++k) line += " " + ts[k].name;
+                std::fprintf(stderr, "%s\n", line.c_str());
+            }
+            if (rc == KF_OK) {
+                std::lock_guard<std::mutex> g(mu);
+                rc = batch(snd.data(), rcv.data(), cnt.data(), static_cast<int>(j - i), ts[i].dt,
+                           ts[i].op, ts[i].average, ts[i].algo, nstream);
+            }
+            const std::string why = rc == KF_OK ? std::string() : t_ex_error;
+            std::lock_guard<std::mutex> lk(nmu);
+            for (size_t k = i; k < j; ++k) {
+                hipEvent_t ev = nullptr;
+                int st        = rc;
+                if (st == KF_OK &&
+                    (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess ||
+                     hipEventRecord(ev, nstream) != hipSuccess)) {
+                    st = KF_ERR_HIP;
+                }
+                ndq.push_back(Done{ev, ts[k].done, ts[k].arg, st, ts[k].ready,
+                                   st == KF_OK ? std::string() : (why.empty() ? "hipEventRecord" : why)});
+            }
+            ncv.notify_all();
+            i = j;
+        }
+    }
+}
+
+// done(status, arg) once each issued named all-reduce finished on the device
+void kf_exchange::finish_loop()
+{
+    (void)hipSetDevice(device);
+    std::unique_lock<std::mutex> lk(nmu);
+    for (;;) {
+        ncv.wait(lk, [&] { return nstop || !ndq.empty(); });
+        if (ndq.empty() && nstop) return;
+        Done d = ndq.front();
+        ndq.pop_front();
+        lk.unlock();
+        int rc = d.status;
+        if (d.ev) {
+            if (hipEventSynchronize(d.ev) != hipSuccess) {
+                rc    = KF_ERR_HIP;
+                d.why = "the all-reduce failed on the device";
+            }
+            (void)hipEventDestroy(d.ev);
+        }
+        if (rc == KF_OK && T->async_error(comm) != 0) {
+            rc    = KF_ERR_RCCL;
+            d.why = "asynchronous transport error";
+        }
+        if (d.ready) (void)hipEventDestroy(d.ready);
+        t_ex_error = d.why;
+        if (d.done) d.done(rc, d.arg);
+        lk.lock();
+        if (rc != KF_OK && nstatus == KF_OK) {
+            nstatus = rc;
+            nerr    = d.why;
+        }
+        ++nfinished;
+        ncv.notify_all();
     }
 }
 
@@ -845,12 +1114,24 @@ kf_exchange::~kf_exchange()
     scv.notify_all();
     if (issuer.joinable()) issuer.join();
     if (completer.joinable()) completer.join();
+    {
+        std::lock_guard<std::mutex> lk(nmu);
+        nstop = true;
+    }
+    ncv.notify_all();
+    if (negotiator.joinable()) negotiator.join();
+    if (nfinisher.joinable()) nfinisher.join();
     DeviceGuard g(device);
-    if (comm) (void)R->CommDestroy(comm);
+    delete ctrl;
+    if (comm) T->destroy(comm);
     if (ws) (void)hipFree(ws);
     if (ws_ev) (void)hipEventDestroy(ws_ev);
     if (own) (void)hipStreamDestroy(own);
     if (comp) (void)hipStreamDestroy(comp);
+    if (nstream) (void)hipStreamDestroy(nstream);
+    if (cstream) (void)hipStreamDestroy(cstream);
+    if (cdev) (void)hipFree(cdev);
+    if (chost) (void)hipHostFree(chost);
     for (auto e : pev) (void)hipEventDestroy(e);
 }
 
@@ -891,40 +1172,49 @@ int kf_exchange_share_id(kf_session_t *s, void *id)
     return rc;
 }
 
+static bool device_ok(int device)
+{
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device >= ndev) {
+        fail(KF_ERR_NO_DEVICE, "no HIP device " + std::to_string(device));
+        return false;
+    }
+    return true;
+}
+
 kf_exchange_t *kf_exchange_create(const void *id, int rank, int world, int device)
 {
     if (!id || world < 1 || rank < 0 || rank >= world || device < 0) {
         fail(KF_ERR_ARG, "kf_exchange_create: bad arguments");
         return nullptr;
     }
-    if (need_rccl() != KF_OK) return nullptr;
-    int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || device >= ndev) {
-        fail(KF_ERR_NO_DEVICE, "kf_exchange_create: no HIP device " + std::to_string(device));
-        return nullptr;
-    }
+    if (need_rccl() != KF_OK || !device_ok(device)) return nullptr;
     DeviceGuard g(device);
-    auto *ex   = new kf_exchange;
-    ex->R      = &rccl();
-    ex->rank   = rank;
-    ex->world  = world;
-    ex->device = device;
     ncclUniqueId u;
     std::memcpy(&u, id, sizeof(u));
-    ncclResult_t e = rccl().CommInitRank(&ex->comm, world, u, rank);
+    ncclComm_t comm = nullptr;
+    ncclResult_t e  = rccl().CommInitRank(&comm, world, u, rank);
     if (e != ncclSuccess) {
         nccl_fail(e, "ncclCommInitRank");
-        ex->comm = nullptr;
-        delete ex;
         return nullptr;
     }
-    if (hipEventCreateWithFlags(&ex->ws_ev, hipEventDisableTiming) != hipSuccess ||
-        hipStreamCreateWithFlags(&ex->own, hipStreamNonBlocking) != hipSuccess) {
-        fail(KF_ERR_HIP, "kf_exchange_create: event/stream");
-        delete ex;
-        return nullptr;
-    }
+    kf_exchange *ex = new_exchange(&kRcclOps, comm, true, rank, world, device);
+    if (!ex) (void)rccl().CommDestroy(comm);
     return ex;
+}
+
+kf_exchange_t *kf_exchange_create_transport(const kf_transport_ops *ops, void *comm, int rank,
+                                            int world, int device)
+{
+    if (!ops || !ops->group_start || !ops->group_end || !ops->reduce_scatter ||
+        !ops->all_gather || !ops->all_to_all || !ops->broadcast || !ops->async_error ||
+        !ops->destroy || world < 1 || rank < 0 || rank >= world || device < 0) {
+        fail(KF_ERR_ARG, "kf_exchange_create_transport: bad arguments");
+        return nullptr;
+    }
+    if (!device_ok(device)) return nullptr;
+    DeviceGuard g(device);
+    return new_exchange(ops, comm, false, rank, world, device);
 }
 
 kf_exchange_t *kf_exchange_create_session(kf_session_t *s, int rank, int world, int device)
@@ -943,6 +1233,19 @@ kf_exchange_t *kf_exchange_create_session(kf_session_t *s, int rank, int world, 
         return nullptr;
     }
     return kf_exchange_create(id, rank, world, device);
+}
+
+kf_exchange_t *kf_exchange_split(kf_exchange_t *ex, int color, int key, int *status)
+{
+    int st = KF_OK;
+    if (!status) status = &st;
+    if (!ex) {
+        *status = fail(KF_ERR_ARG, "kf_exchange_split: no exchange");
+        return nullptr;
+    }
+    DeviceGuard g(ex->device);
+    std::lock_guard<std::mutex> lk(ex->mu);
+    return ex->split(color, key, status);
 }
 
 static int check_bucket_args(kf_exchange_t *ex, const void *const *sends, void *const *recvs,
@@ -1029,8 +1332,8 @@ int kf_exchange_begin_step(kf_exchange_t *ex, const char *const *names, int n, i
         if (e != hipSuccess) rc = hip_fail(e, "order broadcast buffer");
         if (rc == KF_OK) {
             std::lock_guard<std::mutex> g2(ex->mu);
-            ncclResult_t r = ex->R->Broadcast(d, d, n, ncclInt32, 0, ex->comm, ex->own);
-            if (r != ncclSuccess) rc = nccl_fail(r, "ncclBroadcast(order)");
+            const int t = ex->T->broadcast(d, d, bytes, 0, ex->comm, ex->own);
+            if (t != 0) rc = ex->tfail(t, "broadcast(order)");
         }
         if (rc == KF_OK) {
             e = hipMemcpyAsync(ord.data(), d, bytes, hipMemcpyDeviceToHost, ex->own);
@@ -1094,12 +1397,82 @@ int kf_exchange_wait_all(kf_exchange_t *ex, int32_t *order)
     return ex->sstatus;
 }
 
+int kf_exchange_all_reduce_named(kf_exchange_t *ex, const char *name, const void *send, void *recv,
+                                 size_t count, KungFu_Datatype dt, KungFu_Op op, int average,
+                                 int algo, void *stream, kf_done_fn done, void *arg)
+{
+    if (!ex || !name) return fail(KF_ERR_ARG, "bad arguments");
+    size_t c = count;
+    int rc   = check_bucket_args(ex, &send, &recv, &c, 1, dt, op, average);
+    if (rc != KF_OK) return rc;
+    if (algo < KF_ALGO_AUTO || algo > KF_ALGO_ALL_TO_ALL) return fail(KF_ERR_ARG, "unknown algo");
+    DeviceGuard g(ex->device);
+    {
+        std::lock_guard<std::mutex> lk(ex->mu);
+        rc = ex->start_named();
+        if (rc != KF_OK) return rc;
+    }
+    NamedTask t;
+    t.name    = name;
+    t.h1      = fnv1a(name, 0xcbf29ce484222325ull);
+    t.h2      = fnv1a(name, 0x6c62272e07bb0142ull) ^ (t.name.size() * 0x9e3779b97f4a7c15ull);
+    t.send    = send;
+    t.recv    = recv;
+    t.count   = count;
+    t.dt      = dt;
+    t.op      = op;
+    t.average = average ? 1 : 0;
+    t.algo    = algo;
+    t.done    = done;
+    t.arg     = arg;
+    KF_HIP(hipEventCreateWithFlags(&t.ready, hipEventDisableTiming));
+    hipError_t e = hipEventRecord(t.ready, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) {
+        (void)hipEventDestroy(t.ready);
+        return hip_fail(e, "hipEventRecord(start)");
+    }
+    std::lock_guard<std::mutex> lk(ex->nmu);
+    rc = KF_OK;
+    if (ex->nbroken) {
+        rc = fail(KF_ERR_RCCL, "the name negotiation has failed on this exchange");
+    } else if (ex->nwait.count(t.name)) {
+        rc = fail(KF_ERR_ARG, std::string("name already outstanding: ") + name);
+    } else if (ex->nhash.count({t.h1, t.h2})) {
+        rc = fail(KF_ERR_ARG, std::string("name hash collides with an outstanding name: ") + name);
+    }
+    if (rc != KF_OK) {
+        (void)hipEventDestroy(t.ready);
+        return rc;
+    }
+    const std::string key   = t.name;
+    ex->nhash[{t.h1, t.h2}] = key;
+    ex->nfresh.push_back(key);
+    ex->nwait.emplace(key, std::move(t));
+    ex->nstarted++;
+    ex->ncv.notify_all();
+    return KF_OK;
+}
+
+int kf_exchange_wait_named(kf_exchange_t *ex)
+{
+    if (!ex) return KF_ERR_ARG;
+    if (std::this_thread::get_id() == ex->nfinisher.get_id()) {
+        return fail(KF_ERR_ARG, "kf_exchange_wait_named from a done callback");
+    }
+    std::unique_lock<std::mutex> lk(ex->nmu);
+    ex->ncv.wait(lk, [&] { return ex->nfinished == ex->nstarted; });
+    const int rc = ex->nstatus;
+    if (rc != KF_OK) t_ex_error = ex->nerr;
+    ex->nstatus = KF_OK;
+    ex->nerr.clear();
+    return rc;
+}
+
 int kf_exchange_check(kf_exchange_t *ex)
 {
     if (!ex) return KF_ERR_ARG;
-    ncclResult_t ae = ncclSuccess;
-    KF_NCCL(ex->R->CommGetAsyncError(ex->comm, &ae));
-    if (ae != ncclSuccess) return nccl_fail(ae, "RCCL asynchronous error");
+    const int e = ex->T->async_error(ex->comm);
+    if (e != 0) return ex->tfail(e, "asynchronous transport error");
     return KF_OK;
 }
 
@@ -1113,37 +1486,6 @@ int kf_exchange_info(kf_exchange_t *ex, int *rank, int *world, int *device)
 }
 
 void kf_exchange_destroy(kf_exchange_t *ex) { delete ex; }
-
-kf_loopback_t *kf_loopback_create(int world)
-{
-    if (world < 1) return nullptr;
-    return reinterpret_cast<kf_loopback_t *>(new LoopGroup(world));
-}
-
-void kf_loopback_destroy(kf_loopback_t *g) { delete reinterpret_cast<LoopGroup *>(g); }
-
-kf_exchange_t *kf_exchange_create_loopback(kf_loopback_t *g, int rank, int device)
-{
-    auto *lg = reinterpret_cast<LoopGroup *>(g);
-    if (!lg || rank < 0 || rank >= lg->world || device < 0) {
-        fail(KF_ERR_ARG, "kf_exchange_create_loopback: bad arguments");
-        return nullptr;
-    }
-    DeviceGuard dg(device);
-    auto *ex   = new kf_exchange;
-    ex->R      = &loop_rccl();
-    ex->rank   = rank;
-    ex->world  = lg->world;
-    ex->device = device;
-    ex->comm   = reinterpret_cast<ncclComm_t>(new LoopComm{lg, rank});
-    if (hipEventCreateWithFlags(&ex->ws_ev, hipEventDisableTiming) != hipSuccess ||
-        hipStreamCreateWithFlags(&ex->own, hipStreamNonBlocking) != hipSuccess) {
-        fail(KF_ERR_HIP, "kf_exchange_create_loopback: event/stream");
-        delete ex;
-        return nullptr;
-    }
-    return ex;
-}
 
 const char *kf_exchange_last_error(void) { return t_ex_error.c_str(); }
 

@@ -338,8 +338,12 @@ __device__ __forceinline__ Vec<S> ld_vec_serial(const void *base, size_t vi)
 {
     const u32x4 *p = reinterpret_cast<const u32x4 *>(base) + vi;
     u32x4 raw;
-    asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(raw) : "v"(p));
-    asm volatile("s_waitcnt vmcnt(0)" : "+v"(raw));
+    // ONE statement: no compiler-placed read or copy of `raw` can fall
+    // between the load and its wait (early-clobber: raw never shares the
+    // address registers)
+    asm volatile("global_load_dwordx4 %0, %1, off nt\n\ts_waitcnt vmcnt(0)"
+                 : "=&v"(raw)
+                 : "v"(p));
     Vec<S> v;
     __builtin_memcpy(&v, &raw, 16);
     return v;

@@ -3,16 +3,26 @@
 // srcs/cpp/src/torch/ops/cuda/collective.cpp:20-55), over the C ABI of
 // libkungfu_amd.so instead of a host round trip.
 //
-// The reference copies a CUDA tensor into a std::vector, all-reduces it on the
-// host through Peer::GetDefault()->AllReduce, and copies it back
-// (collective.cpp:24-29). Here the process's exchange (kf_exchange_*, RCCL
-// over xGMI for the bytes, the HIP kernels for the sum) reduces it in HBM,
-// queued on torch's current HIP stream:
+// The reference copies a CUDA tensor into a host buffer, all-reduces it there
+// through Peer::GetDefault()->AllReduce keyed by the tensor's name, and copies
+// it back (collective.cpp:24-29, 41-53). Here the process's exchange
+// (kf_exchange_*: RCCL over xGMI for the bytes, the HIP kernels for the sum)
+// reduces it in HBM, and the pairing across ranks is the reference's: by
+// NAME, through kf_exchange_all_reduce_named, so ranks may start their
+// tensors in different orders (the torch optimizer starts them in parameter
+// or hook order, sync_sgd.py:12-22):
 //
 //   all_reduce_cuda(input, output, type, op)             collective.cpp:20-30
+//       blocking; the reference names it "" and relies on call order, so
+//       here every rank's k-th synchronous call is the name "::sync::k"
 //   all_reduce_cuda_async(input, output, type, op, name) collective.cpp:32-55
 //       -> int handle; wait_handle(h) / wait_all_handles(hs) block until done
-//          (the reference's HandleManager, handler_manager.hpp:6-84)
+//          (the reference's HandleManager, handler_manager.hpp:6-84) and
+//          raise the failure if there was one
+//
+// The data moves after the work queued on torch's current stream before the
+// call (an event recorded there), on the exchange's own stream, so it
+// overlaps whatever the caller queues next.
 //
 // `type` is the tensor's x.type() string (torch/ops/clib.py maps
 // 'torch.cuda.FloatTensor'; the reference converts only Float,
@@ -22,11 +32,16 @@
 // Peer::GetDefault() is init_exchange(id, rank, size, device): the id is
 // rank 0's kf_exchange_unique_id() bytes, shared by the caller (torch.distributed
 // in kungfu_amd/torch/ops.py), as gpu_collective.cpp:190-200 shares it.
+// bind_exchange(handle) makes an exchange built elsewhere (a C++ host's
+// kf_exchange_create_session, kf_exchange_split, a host transport) the one
+// this thread's ops use.
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime_api.h>
 #include <torch/extension.h>
 
+#include <condition_variable>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -36,9 +51,20 @@
 
 namespace
 {
-kf_exchange_t *g_ex = nullptr;
+kf_exchange_t *g_ex = nullptr;              // init_exchange's (Peer::GetDefault)
+thread_local kf_exchange_t *t_ex = nullptr; // bind_exchange's, this thread only
 std::mutex g_mu;
-std::map<int, hipEvent_t> g_handles;
+std::map<kf_exchange_t *, uint64_t> g_sync_seq;
+
+struct Pending {
+    std::mutex m;
+    std::condition_variable cv;
+    bool done  = false;
+    int status = KF_OK;
+    std::string why;
+    torch::Tensor input, output;  // alive until waited for (released with the GIL held)
+};
+std::map<int, std::shared_ptr<Pending>> g_handles;
 int g_next = 0;
 
 void check(int rc, const char *what)
@@ -49,9 +75,11 @@ void check(int rc, const char *what)
     }
 }
 
-void check_hip(hipError_t e, const char *what)
+kf_exchange_t *current()
 {
-    if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+    kf_exchange_t *ex = t_ex ? t_ex : g_ex;
+    if (!ex) throw std::runtime_error("kungfu_amd: init_exchange() first");
+    return ex;
 }
 
 // x.type() strings of CUDA tensors -> KungFu dtype codes (dtype.h:21-39)
@@ -78,10 +106,25 @@ KungFu_Op from_op(const std::string &op)
     return it->second;
 }
 
-hipStream_t issue(const torch::Tensor &input, torch::Tensor &output, const std::string &type,
-                  const std::string &op_name)
+void on_done(int status, void *arg)
 {
-    if (!g_ex) throw std::runtime_error("kungfu_amd: init_exchange() first");
+    auto *ref = static_cast<std::shared_ptr<Pending> *>(arg);
+    std::shared_ptr<Pending> p = *ref;
+    delete ref;
+    {
+        std::lock_guard<std::mutex> lk(p->m);
+        p->status = status;
+        if (status != KF_OK) p->why = kf_exchange_last_error();  // set for done()
+        p->done = true;
+    }
+    p->cv.notify_all();
+}
+
+std::shared_ptr<Pending> start(const torch::Tensor &input, torch::Tensor &output,
+                               const std::string &type, const std::string &op_name,
+                               const std::string &name)
+{
+    kf_exchange_t *ex = current();
     if (!input.is_cuda() || !output.is_cuda()) {
         throw std::runtime_error("kungfu_amd: all_reduce_cuda needs CUDA tensors");
     }
@@ -93,17 +136,45 @@ hipStream_t issue(const torch::Tensor &input, torch::Tensor &output, const std::
     if (kungfu_type_size(dt) != static_cast<uint32_t>(input.element_size())) {
         throw std::runtime_error("kungfu_amd: type string does not match the tensor");
     }
+    const KungFu_Op op = from_op(op_name);
     int dev = -1;
-    check(kf_exchange_info(g_ex, nullptr, nullptr, &dev), "kf_exchange_info");
-    if (input.get_device() != dev) {
+    check(kf_exchange_info(ex, nullptr, nullptr, &dev), "kf_exchange_info");
+    if (input.get_device() != dev || output.get_device() != dev) {
         throw std::runtime_error("kungfu_amd: tensor not on the exchange's device");
     }
     hipStream_t s = c10::hip::getCurrentHIPStream(dev).stream();
-    check(kf_exchange_all_reduce(g_ex, input.data_ptr(), output.data_ptr(),
-                                 static_cast<size_t>(input.numel()), dt, from_op(op_name), 0,
-                                 KF_ALGO_AUTO, s),
-          "kf_exchange_all_reduce");
-    return s;
+    auto p        = std::make_shared<Pending>();
+    p->input      = input;
+    p->output     = output;
+    auto *ref     = new std::shared_ptr<Pending>(p);
+    const int rc  = kf_exchange_all_reduce_named(ex, name.c_str(), input.data_ptr(),
+                                                output.data_ptr(),
+                                                static_cast<size_t>(input.numel()), dt, op, 0,
+                                                KF_ALGO_AUTO, s, on_done, ref);
+    if (rc != KF_OK) {
+        delete ref;
+        check(rc, "kf_exchange_all_reduce_named");
+    }
+    return p;
+}
+
+void wait(const std::shared_ptr<Pending> &p)
+{
+    std::string why;
+    int status;
+    {
+        py::gil_scoped_release nogil;
+        std::unique_lock<std::mutex> lk(p->m);
+        p->cv.wait(lk, [&] { return p->done; });
+        status = p->status;
+        why    = p->why;
+    }
+    p->input.reset();
+    p->output.reset();
+    if (status != KF_OK) {
+        throw std::runtime_error("kungfu_amd: all-reduce failed (status " +
+                                 std::to_string(status) + "): " + why);
+    }
 }
 }  // namespace
 
@@ -112,7 +183,10 @@ void init_exchange(py::bytes uid, int rank, int size, int device)
     std::string id = uid;
     if (id.size() != KF_UNIQUE_ID_BYTES) throw std::runtime_error("kungfu_amd: id must be 128 bytes");
     std::lock_guard<std::mutex> lk(g_mu);
-    if (g_ex) kf_exchange_destroy(g_ex);
+    if (g_ex) {
+        (void)kf_exchange_wait_named(g_ex);
+        kf_exchange_destroy(g_ex);
+    }
     g_ex = kf_exchange_create(id.data(), rank, size, device);
     if (!g_ex) throw std::runtime_error(std::string("kf_exchange_create: ") + kf_exchange_last_error());
 }
@@ -126,55 +200,67 @@ py::bytes unique_id()
 
 bool initialized() { return g_ex != nullptr; }
 
+// this thread's ops use `handle` (a kf_exchange_t* as an integer; 0 = back to
+// the process exchange); the caller keeps it alive while bound
+void bind_exchange(uintptr_t handle) { t_ex = reinterpret_cast<kf_exchange_t *>(handle); }
+
 void finalize()
 {
     std::lock_guard<std::mutex> lk(g_mu);
-    for (auto &kv : g_handles) (void)hipEventDestroy(kv.second);
-    g_handles.clear();
-    if (g_ex) kf_exchange_destroy(g_ex);
+    if (g_ex) {
+        py::gil_scoped_release nogil;
+        (void)kf_exchange_wait_named(g_ex);
+        kf_exchange_destroy(g_ex);
+    }
+    g_sync_seq.erase(g_ex);
     g_ex = nullptr;
 }
 
 void all_reduce_cuda(torch::Tensor input, torch::Tensor output, const std::string &type,
                      const std::string &op_name)
 {
-    issue(input, output, type, op_name);
+    std::string name;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        name = "::sync::" + std::to_string(g_sync_seq[current()]++);
+    }
+    wait(start(input, output, type, op_name, name));
 }
 
 int all_reduce_cuda_async(torch::Tensor input, torch::Tensor output, const std::string &type,
-                          const std::string &op_name, const std::string & /*tensor_name*/)
+                          const std::string &op_name, const std::string &tensor_name)
 {
-    // every rank issues its all-reduces in one order (RCCL's rule; the
-    // reference keys them by name instead), the name is kept for the API
-    hipStream_t s = issue(input, output, type, op_name);
-    hipEvent_t ev;
-    check_hip(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
-    check_hip(hipEventRecord(ev, s), "hipEventRecord");
+    auto p = start(input, output, type, op_name, tensor_name);
     std::lock_guard<std::mutex> lk(g_mu);
     const int h  = g_next++;
-    g_handles[h] = ev;
+    g_handles[h] = p;
     return h;
 }
 
 void wait_handle(int handle)
 {
-    hipEvent_t ev;
+    std::shared_ptr<Pending> p;
     {
         std::lock_guard<std::mutex> lk(g_mu);
         auto it = g_handles.find(handle);
         if (it == g_handles.end()) throw std::runtime_error("kungfu_amd: unknown handle");
-        ev = it->second;
+        p = it->second;
         g_handles.erase(it);
     }
-    hipError_t e = hipEventSynchronize(ev);
-    (void)hipEventDestroy(ev);
-    check_hip(e, "hipEventSynchronize");
-    check(kf_exchange_check(g_ex), "kf_exchange_check");
+    wait(p);
 }
 
 void wait_all_handles(const std::vector<int> &handles)
 {
-    for (int h : handles) wait_handle(h);
+    std::string first;
+    for (int h : handles) {
+        try {
+            wait_handle(h);
+        } catch (const std::runtime_error &e) {
+            if (first.empty()) first = e.what();
+        }
+    }
+    if (!first.empty()) throw std::runtime_error(first);
 }
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m)
@@ -182,6 +268,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m)
     m.def("unique_id", &unique_id);
     m.def("init_exchange", &init_exchange);
     m.def("initialized", &initialized);
+    m.def("bind_exchange", &bind_exchange);
     m.def("finalize", &finalize);
     m.def("all_reduce_cuda", &all_reduce_cuda);
     m.def("all_reduce_cuda_async", &all_reduce_cuda_async);

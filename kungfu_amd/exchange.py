@@ -78,21 +78,33 @@ class NativeExchange:
         self._sums = {}
 
     @classmethod
-    def loopback(cls, group, rank, algo="auto", device=None):
-        """Rank `rank` of a LoopbackGroup: the same exchange over the loopback
-        transport (ranks are threads of this process on one device; testing)."""
-        self = cls.__new__(cls)
+    def from_handle(cls, h, algo="auto", device=None):
+        """Wrap a kf_exchange_t* made elsewhere — kf_exchange_create_session by
+        a C++/Go host, kf_exchange_split, kf_exchange_create_transport over a
+        host's own transport; this object owns (destroys) it."""
+        if not h:
+            raise _lib.KungFuAMDError("no exchange handle")
         if algo not in ALGOS:
             raise ValueError("algo must be one of %s" % sorted(ALGOS))
-        self.algo, self.group, self.world, self.rank = algo, None, group.world, rank
+        self = cls.__new__(cls)
         self.lib = _lib.load()
-        self.device = torch.device(device if device is not None else "cuda:0")
-        h = self.lib.kf_exchange_create_loopback(group._h, rank, self.device.index)
-        if not h:
-            raise _lib.KungFuAMDError("kf_exchange_create_loopback: " +
-                                      self.lib.kf_exchange_last_error().decode())
+        r, w, d = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        _lib.check(self.lib.kf_exchange_info(h, ctypes.byref(r), ctypes.byref(w),
+                                             ctypes.byref(d)), "kf_exchange_info")
+        self.algo, self.group, self.rank, self.world = algo, None, r.value, w.value
+        self.device = torch.device("cuda", d.value) if device is None else torch.device(device)
         self._h, self._side, self._sums = h, None, {}
         return self
+
+    def split(self, color, key=None):
+        """kf_exchange_split (gpu_collective::new_local / new_group,
+        gpu_collective.cpp:202-243): the ranks passing the same color form a
+        new exchange, ordered by key; color < 0 joins none (None)."""
+        st = ctypes.c_int(0)
+        h = self.lib.kf_exchange_split(self._h, int(color), int(self.rank if key is None else key),
+                                       ctypes.byref(st))
+        _lib.check(st.value, "kf_exchange_split")
+        return NativeExchange.from_handle(h, self.algo, self.device) if h else None
 
     def set_pipeline(self, groups):
         """kf_exchange_set_pipeline: split every batch call into `groups`
@@ -175,6 +187,33 @@ class NativeExchange:
         _lib.check(rc, "kf_exchange_sma_batch")
         return buckets
 
+    def all_reduce_named(self, name, buf, op="sum", average=False, stream=None, callback=None):
+        """kf_exchange_all_reduce_named: in place, paired with the peers' calls
+        of the same name whatever order each rank starts its names in
+        (GoKungfuAllReduce with a done callback). callback(name, status) runs
+        on the exchange's completion thread; wait_named() blocks for all."""
+        red = OP_NAMES[op] if isinstance(op, str) else OP(op)
+        s = stream if stream is not None else torch.cuda.current_stream(buf.device)
+
+        def done(status, _arg):
+            if callback is not None:
+                callback(name, status)
+
+        cfn = _lib.DONE_FN(done)
+        self._named_keep = getattr(self, "_named_keep", [])
+        self._named_keep.append((cfn, buf))
+        rc = self.lib.kf_exchange_all_reduce_named(
+            self._h, name.encode(), buf.data_ptr(), buf.data_ptr(), buf.numel(),
+            int(kungfu_dtype(buf)), int(red), 1 if average else 0, ALGOS[self.algo],
+            s.cuda_stream, cfn, None)
+        _lib.check(rc, "kf_exchange_all_reduce_named")
+
+    def wait_named(self):
+        """Block until every name started so far completed; raise on failure."""
+        rc = self.lib.kf_exchange_wait_named(self._h)
+        self._named_keep = []
+        _lib.check(rc, "kf_exchange_wait_named")
+
     def check(self):
         """Raise if RCCL reported an asynchronous error."""
         _lib.check(self.lib.kf_exchange_check(self._h), "kf_exchange_check")
@@ -196,23 +235,6 @@ class NativeExchange:
             self.close()
         except Exception:
             pass
-
-
-class LoopbackGroup:
-    """kf_loopback_create: `world` ranks as threads of one process on one GPU
-    (include/kungfu_amd.h, "Loopback transport")."""
-
-    def __init__(self, world):
-        self.world = world
-        self.lib = _lib.load()
-        self._h = self.lib.kf_loopback_create(world)
-        if not self._h:
-            raise _lib.KungFuAMDError("kf_loopback_create(%d)" % world)
-
-    def close(self):
-        if self._h:
-            self.lib.kf_loopback_destroy(self._h)
-            self._h = None
 
 
 class _Handle:

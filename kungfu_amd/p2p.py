@@ -377,15 +377,27 @@ class AutoExchange:
     (integer dtypes; two ranks summing f32/f64). So the result never depends
     on which transport won on a given box.
 
+    "Same bits" is checked, not assumed: every candidate's warm-up starts from
+    the same snapshot of the buckets, and its result is compared bit for bit
+    with the first candidate's (rank-agreed: a mismatch on any rank drops the
+    candidate on every rank, and the rank, the candidate, the bucket and the
+    first differing element are printed to stderr). So a transport that
+    returns a stale or wrong shard on some node (the P2P push
+    mode's cross-device coherence) is never adopted, however fast it is.
+
     The trial runs `trials` exchanges with each candidate on the buckets, then
-    restores their contents from a snapshot, so the first call returns the
+    restores their contents from the snapshot, so the first call returns the
     same values as any later one. The choice is rank-agreed (the slowest
     rank's time decides), so every rank keeps issuing the same collectives.
     P2P is a candidate only for GPU buckets with every rank on one host; if
-    its setup fails on any rank, RCCL is used. ``picked`` maps each bucket
-    list (by address) to "rccl" or "p2p"."""
+    its setup fails on any rank, RCCL is used. Past KF_MAX_INPUTS (16) ranks
+    the rank-order fold cannot run, and RCCL's reduce-scatter is the only
+    candidate. `extra` adds (name, exchange) candidates a host offers (its own
+    transport, say); they are held to the same check. ``picked`` maps each
+    bucket list (by address) to the winner's name; ``dropped`` lists
+    (candidate, reason) of those that failed or differed."""
 
-    def __init__(self, group=None, trials=3, mode="pull", epilogue=None):
+    def __init__(self, group=None, trials=3, mode="pull", epilogue=None, extra=()):
         from .collective import Exchange, HipEpilogue
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -399,6 +411,8 @@ class AutoExchange:
         self._host_ok = None
         self._native, self._native_tried = None, False
         self.picked = {}
+        self.dropped = []
+        self.extra = list(extra)
         self._choice = {}
 
     def _p2p_candidate(self, buckets):
@@ -451,12 +465,10 @@ class AutoExchange:
         return (self.world == 2 and op == "sum" and
                 all(b.dtype in (torch.float32, torch.float64) for b in buckets))
 
-    def _pick(self, buckets, step, op="sum"):
-        import time
-        key = tuple((b.data_ptr(), b.numel(), b.dtype) for b in buckets)
-        ex = self._choice.get(key)
-        if ex is not None:
-            return ex
+    def _candidates(self, buckets, op):
+        from ._lib import MAX_INPUTS
+        if self.world > MAX_INPUTS:  # no rank-order fold of more than 16 inputs
+            return [("rccl_rs", self.rccl_rs)] + self.extra
         cands = [("rccl", self.rccl)]
         if self._rs_exact(buckets, op):
             cands.append(("rccl_rs", self.rccl_rs))
@@ -466,29 +478,72 @@ class AutoExchange:
         p2p = self._p2p_candidate(buckets)
         if p2p is not None:
             cands.append(("p2p", p2p))
+        return cands + self.extra
+
+    def _drop(self, name, why):
+        import sys
+        self.dropped.append((name, why))
+        print("kungfu_amd AutoExchange: rank %d drops candidate %s: %s" % (self.rank, name, why),
+              file=sys.stderr)
+
+    @staticmethod
+    def _first_difference(ref, res):
+        """None if every bucket holds the same bytes, else (bucket, element)."""
+        for j, (a, b) in enumerate(zip(ref, res)):
+            x, y = a.reshape(-1).view(torch.uint8), b.reshape(-1).view(torch.uint8)
+            if not torch.equal(x, y):
+                byte = int((x != y).nonzero()[0])
+                return j, byte // a.element_size()
+        return None
+
+    def _pick(self, buckets, step, op="sum"):
+        import time
+        key = tuple((b.data_ptr(), b.numel(), b.dtype) for b in buckets)
+        ex = self._choice.get(key)
+        if ex is not None:
+            return ex
+        cands = self._candidates(buckets, op)
+        on_gpu = any(b.is_cuda for b in buckets)
+
+        def sync():
+            if on_gpu:
+                torch.cuda.synchronize()
+
         if len(cands) > 1:
             snap = [b.clone() for b in buckets]
-            times = []
+            times, ref = [], None
             for name, cand in cands:
+                for b, s in zip(buckets, snap):  # every warm-up from the same inputs
+                    b.copy_(s)
                 ok = True
                 try:
                     step(cand)  # warm-up; maps the buckets for P2P
-                    torch.cuda.synchronize()
+                    sync()
                     if hasattr(cand, "finish"):
                         cand.finish()
                 except Exception as e:  # say why; the other candidates still run
-                    import sys
-                    print("kungfu_amd AutoExchange: candidate %s failed on rank %d: %r"
-                          % (name, self.rank, e), file=sys.stderr)
+                    self._drop(name, "failed: %r" % (e,))
                     ok = False
                 if not self._agree_all(ok):
                     times.append(float("inf"))
                     continue
+                if ref is None:  # the first candidate that ran everywhere is the reference
+                    ref, ref_name = [b.clone() for b in buckets], name
+                else:
+                    diff = self._first_difference(ref, buckets)
+                    if diff is not None:
+                        self._drop(name, "result differs from %s's in bucket %d at element %d"
+                                   % (ref_name, diff[0], diff[1]))
+                    if not self._agree_all(diff is None):
+                        if diff is None:
+                            self.dropped.append((name, "differs on another rank"))
+                        times.append(float("inf"))
+                        continue
                 dist.barrier(group=self.group)
                 t0 = time.perf_counter()
                 for _ in range(self.trials):
                     step(cand)
-                torch.cuda.synchronize()
+                sync()
                 times.append(time.perf_counter() - t0)
                 if hasattr(cand, "finish"):
                     cand.finish()
@@ -498,7 +553,11 @@ class AutoExchange:
             best = min(range(len(cands)), key=lambda i: worst[i])
             for b, s in zip(buckets, snap):
                 b.copy_(s)
-            del snap
+            del snap, ref
+            if worst[best] == float("inf"):
+                from ._lib import KungFuAMDError
+                raise KungFuAMDError("AutoExchange: no candidate ran on every rank (%s)"
+                                     % self.dropped)
         else:
             best = 0
         self.picked[key] = cands[best][0]

@@ -6,6 +6,8 @@ Peer::AllReduce and copies it back (srcs/cpp/src/torch/ops/cuda/collective.cpp:
 reduced by RCCL reduce-scatter + all-gather over xGMI (op 'sum' / 'min' /
 'max' / 'prod'); the handle API is kept for the async variants.
 """
+import threading
+
 import torch
 import torch.distributed as dist
 
@@ -13,6 +15,7 @@ from ..collective import Exchange, padded_count
 
 _exchange = None
 _native = [None, False]  # the C++ op module once its exchange is up; tried?
+_native_lock = threading.Lock()
 
 
 def native_ops():
@@ -20,21 +23,54 @@ def native_ops():
     (kungfu_amd/csrc/torch_ops.cpp: all_reduce_cuda(input, output, type, op),
     all_reduce_cuda_async(..., name) -> handle, wait_handle), its exchange
     initialised from the process group: RCCL needs one GPU per rank, so only
-    with the nccl backend (or a single process). None where it cannot run."""
-    if _native[1]:
+    with the nccl backend (or a single process). None where it cannot run —
+    decided the same way on every rank: a rank whose import or exchange setup
+    fails says why, every rank agrees on the outcome (all_gather_object), and
+    all of them take the torch.distributed path from then on."""
+    with _native_lock:
+        if not _native[1]:
+            _native[0] = _init_native()
+            _native[1] = True
         return _native[0]
-    _native[1] = True
+
+
+def _init_native():
     if not torch.cuda.is_available():
         return None
     if dist.is_initialized() and dist.get_backend() != "nccl":
         return None
-    from .. import kungfu_amd_torch_ops as m
-    from ..exchange import NativeExchange
-    uid = NativeExchange.shared_id()
-    rank = dist.get_rank() if dist.is_initialized() else 0
-    m.init_exchange(uid, rank, _world(), torch.cuda.current_device())
-    _native[0] = m
+    import sys
+    m, ok = None, True
+    try:
+        from .. import kungfu_amd_torch_ops as m
+    except ImportError as e:
+        print("kungfu_amd.torch.ops: C++ op module unavailable: %r" % (e,), file=sys.stderr)
+        ok = False
+    if not _agree(ok):
+        return None
+    try:
+        from ..exchange import NativeExchange
+        uid = NativeExchange.shared_id()
+        rank = dist.get_rank() if dist.is_initialized() else 0
+        m.init_exchange(uid, rank, _world(), torch.cuda.current_device())
+    except RuntimeError as e:  # KungFuAMDError is one
+        print("kungfu_amd.torch.ops: exchange setup failed on rank %d: %r"
+              % (dist.get_rank() if dist.is_initialized() else 0, e), file=sys.stderr)
+        ok = False
+    if not _agree(ok):
+        if m.initialized():
+            m.finalize()
+        return None
     return m
+
+
+def _agree(flag):
+    """True iff `flag` holds on every rank."""
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return bool(flag)
+    flags = [None] * dist.get_world_size()
+    dist.all_gather_object(flags, bool(flag))
+    return all(flags)
 
 
 def _op_maps():
@@ -102,8 +138,11 @@ def inplace_all_reduce_op(x, op=None):
 
 def inplace_all_reduce_async_op(x, name, op=None):
     """Starts x <- all-reduce(x); returns a handle for wait_handle
-    (collective.py:22-25). Reduce-scatter and all-gather are queued on the
-    RCCL stream at once; the copy back happens in wait_handle."""
+    (collective.py:22-25). CUDA tensors go through the C++ op, which pairs
+    them across ranks by `name` (any start order per rank, as the
+    reference). The torch.distributed stand-in (no C++ op: CPU tensors, gloo)
+    queues reduce-scatter and all-gather at once and pairs by call order, so
+    there every rank must start its names in one order."""
     op = op or "sum"
     h = _next[0]
     _next[0] += 1

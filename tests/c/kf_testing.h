@@ -1,0 +1,36 @@
+/*
+ * kf_testing.h — test-only transports for the exchange (tests/c/libkf_testing.so,
+ * built by tests/c/Makefile). NOT part of the product library: they plug into
+ * libkungfu_amd.so through kf_exchange_create_transport (include/kungfu_amd.h).
+ *
+ *  loopback   `world` ranks that are threads of ONE process on ONE device
+ *             (RCCL refuses two ranks on one GPU). Each rank's exchange runs
+ *             the product's code — shards, tails, workspace, batched folds,
+ *             the ordered scheduler, the name-keyed negotiation, splits —
+ *             with every collective a rendezvous of the ranks' threads that
+ *             moves the bytes with hipMemcpy (the reduce-scatter folds in rank
+ *             order on the host; no f16/bf16/u16/i16 reduce-scatter). Every
+ *             rank's calls must come from its own thread.
+ *  rccl1      a one-rank librccl communicator bound through the transport
+ *             table, so the exchange calls librccl's own entry points with
+ *             its exact arguments instead of the built-in world-1 copy.
+ */
+#pragma once
+#include "kungfu_amd.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct kf_loopback kf_loopback_t;
+kf_loopback_t *kf_loopback_create(int world);
+/* after every exchange of the group (and of its splits) was destroyed */
+void kf_loopback_destroy(kf_loopback_t *g);
+kf_exchange_t *kf_exchange_create_loopback(kf_loopback_t *g, int rank, int device);
+/* NULL on failure (kf_testing_last_error) */
+kf_exchange_t *kf_exchange_create_rccl1(int device);
+const char *kf_testing_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif

@@ -3,11 +3,13 @@
 // kf_exchange_unique_id, communicator, a batch of buckets all-reduced with the
 // S-SGD epilogue, the ordered scheduler with done callbacks, the SMA batch.
 // One rank (world 1): every all-reduce is the identity, the order is checked;
-// then three ranks as threads over the loopback transport.
+// then three ranks as threads over the test library's loopback transport
+// (tests/c/kf_testing.h, plugged in through kf_exchange_create_transport):
+// batches, and name-keyed all-reduces started in a different order per rank.
 // Exit 0 = pass, 77 = no device (build checked only).
-//   g++ -std=c++17 -D__HIP_PLATFORM_AMD__ -I include -I /opt/rocm/include
-//       tests/c/test_exchange.cpp -L kungfu_amd -lkungfu_amd -L /opt/rocm/lib
-//       -lamdhip64 -o /tmp/test_exchange
+//   g++ -std=c++17 -D__HIP_PLATFORM_AMD__ -I include -I tests/c -I /opt/rocm/include
+//       tests/c/test_exchange.cpp -L kungfu_amd -lkungfu_amd -L tests/c -lkf_testing
+//       -L /opt/rocm/lib -lamdhip64 -o /tmp/test_exchange
 #include <hip/hip_runtime_api.h>
 
 #include <atomic>
@@ -18,6 +20,7 @@
 #include <thread>
 #include <vector>
 
+#include "kf_testing.h"
 #include "kungfu_amd.h"
 
 #define CHECK(c)                                                                \
@@ -109,6 +112,66 @@ int multi_rank_loopback(int world)
     return 0;
 }
 
+// name-keyed: rank r starts the names rotated by r (and reversed on odd
+// ranks); every bucket must still be the sum over ranks of ITS name
+int multi_rank_named(int world)
+{
+    kf_loopback_t *g = kf_loopback_create(world);
+    CHECK(g != nullptr);
+    const int nn = 9;
+    std::vector<int> rc(world, 0);
+    std::vector<std::thread> ts;
+    for (int r = 0; r < world; ++r) {
+        ts.emplace_back([&, r] {
+            rc[r] = [&]() -> int {
+                CHECK(hipSetDevice(0) == hipSuccess);
+                kf_exchange_t *ex = kf_exchange_create_loopback(g, r, 0);
+                CHECK(ex != nullptr);
+                hipStream_t s;
+                CHECK(hipStreamCreate(&s) == hipSuccess);
+                std::vector<void *> bufs(nn);
+                std::vector<size_t> counts(nn);
+                for (int b = 0; b < nn; ++b) {
+                    counts[b] = 1 + 1000 * b + b % 3;
+                    std::vector<int32_t> h(counts[b]);
+                    for (size_t i = 0; i < counts[b]; ++i) h[i] = (r + 1) * (b + 1) + int(i % 11);
+                    CHECK(hipMalloc(&bufs[b], counts[b] * 4) == hipSuccess);
+                    CHECK(hipMemcpy(bufs[b], h.data(), counts[b] * 4, hipMemcpyHostToDevice) ==
+                          hipSuccess);
+                }
+                for (int k = 0; k < nn; ++k) {
+                    int b = (k + 2 * r) % nn;
+                    if (r % 2) b = nn - 1 - b;
+                    const std::string name = "grad/" + std::to_string(b);
+                    CHECK(kf_exchange_all_reduce_named(ex, name.c_str(), bufs[b], bufs[b],
+                                                       counts[b], KungFu_INT32, KungFu_SUM, 0,
+                                                       KF_ALGO_AUTO, s, nullptr,
+                                                       nullptr) == KF_OK);
+                }
+                CHECK(kf_exchange_wait_named(ex) == KF_OK);
+                for (int b = 0; b < nn; ++b) {
+                    std::vector<int32_t> got(counts[b]);
+                    CHECK(hipMemcpy(got.data(), bufs[b], counts[b] * 4, hipMemcpyDeviceToHost) ==
+                          hipSuccess);
+                    for (size_t i = 0; i < counts[b]; ++i) {
+                        int32_t want = 0;
+                        for (int q = 0; q < world; ++q) want += (q + 1) * (b + 1) + int(i % 11);
+                        CHECK(got[i] == want);
+                    }
+                    CHECK(hipFree(bufs[b]) == hipSuccess);
+                }
+                CHECK(hipStreamDestroy(s) == hipSuccess);
+                kf_exchange_destroy(ex);
+                return 0;
+            }();
+        });
+    }
+    for (auto &t : ts) t.join();
+    kf_loopback_destroy(g);
+    for (int r = 0; r < world; ++r) CHECK(rc[r] == 0);
+    return 0;
+}
+
 int main()
 {
     if (kf_device_count() < 1) {
@@ -187,6 +250,7 @@ int main()
     kf_exchange_destroy(ex);
     CHECK(hipStreamDestroy(s) == hipSuccess);
     CHECK(multi_rank_loopback(3) == 0);
+    CHECK(multi_rank_named(3) == 0);
     std::printf("exchange ok\n");
     return 0;
 }

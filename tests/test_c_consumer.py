@@ -39,10 +39,14 @@ def exchange_binary(tmp_path_factory):
     ABI alone (the reference's C++ side, gpu_collective.cpp / scheduler.cpp)."""
     out = str(tmp_path_factory.mktemp("cx") / "test_exchange")
     lib = os.path.join(ROOT, "kungfu_amd")
+    tl = os.path.join(ROOT, "tests", "c")
+    if not os.path.exists(os.path.join(tl, "libkf_testing.so")):
+        subprocess.run(["make", "-s", "-C", tl], check=True)
     subprocess.run(["g++", "-std=c++17", "-Wall", "-Wextra", "-Werror", "-D__HIP_PLATFORM_AMD__",
-                    "-I", os.path.join(ROOT, "include"), "-I", "/opt/rocm/include",
+                    "-I", os.path.join(ROOT, "include"), "-I", tl, "-I", "/opt/rocm/include",
                     os.path.join(ROOT, "tests", "c", "test_exchange.cpp"),
                     "-L", lib, "-lkungfu_amd", "-Wl,-rpath," + lib,
+                    "-L", tl, "-lkf_testing", "-Wl,-rpath," + tl,
                     "-L", "/opt/rocm/lib", "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib",
                     "-lpthread", "-o", out], check=True)
     return out

@@ -194,3 +194,30 @@ def test_tf_dtype_map_is_the_reference_one():
     for bad in ("float16", "uint8", "complex64"):  # ops.h: no DT_HALF, throws
         with pytest.raises(ValueError, match="unsupported dtype"):
             ops.to_kungfu_type(bad)
+
+
+def test_no_test_transport_in_the_product(lib):
+    """The loopback transport and its host fold live in the TEST library
+    (tests/c/libkf_testing.so), plugged in through the product's
+    kf_exchange_create_transport; the shipped library exports none of it and
+    has no switch that changes what a one-rank exchange does."""
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True,
+                         text=True, check=True).stdout
+    names = [l.split()[-1] for l in out.splitlines()]
+    assert not [n for n in names if "loopback" in n or "rccl1" in n or "kf_testing" in n]
+    strings = subprocess.run(["strings", LIB], capture_output=True, text=True,
+                             check=True).stdout
+    assert "KUNGFU_AMD_EXCHANGE_W1_COLLECTIVES" not in strings
+    assert "loopback" not in strings
+    tl = os.path.join(ROOT, "tests", "c")
+    subprocess.run(["make", "-s", "-C", tl], check=True)
+    out = subprocess.run(["nm", "-D", "--defined-only", os.path.join(tl, "libkf_testing.so")],
+                         capture_output=True, text=True, check=True).stdout
+    exported = set(l.split()[-1] for l in out.splitlines() if " T " in l)
+    assert {"kf_loopback_create", "kf_loopback_destroy", "kf_exchange_create_loopback",
+            "kf_exchange_create_rccl1"} <= exported
+    # no kernel and no copy of the product in the test library: it calls it
+    undefined = subprocess.run(["nm", "-D", "--undefined-only",
+                                os.path.join(tl, "libkf_testing.so")],
+                               capture_output=True, text=True, check=True).stdout
+    assert "kf_exchange_create_transport" in undefined

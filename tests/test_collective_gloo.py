@@ -554,3 +554,79 @@ def body_a2a_rank_order(rank, world, use_gpu):
 @pytest.mark.parametrize("world", [2, 3, 4])
 def test_a2a_rank_order_bit_exact(world):
     run_world("body_a2a_rank_order", world)
+
+
+class _Perturbing:
+    """A candidate that runs the real exchange and then flips the low bit of
+    one element on rank 1 only — a stand-in for a transport that serves a
+    stale shard on one node. It is the fastest (it IS the reference's path,
+    minus nothing); the pick must still drop it."""
+
+    def __init__(self, inner):
+        self.inner = inner
+
+    def all_reduce_(self, buckets, op="sum", average=False, coalesce=True):
+        self.inner.all_reduce_(buckets, op=op, average=average)
+        if dist.get_rank() == 1:
+            v = buckets[1].view(torch.int32) if buckets[1].dtype == torch.float32 else buckets[1]
+            v[17] ^= 1
+        return buckets
+
+    def sma_(self, buckets, alpha):
+        self.inner.sma_(buckets, alpha)
+        if dist.get_rank() == 1:
+            buckets[0].view(torch.int32)[3] ^= 1
+        return buckets
+
+
+def body_auto_exchange_drops_wrong_bits(rank, world, use_gpu):
+    import contextlib
+    import io
+    from kungfu_amd.collective import Exchange
+    from kungfu_amd.p2p import AutoExchange
+    from oracle import oracle
+    ep = _epilogue(use_gpu)
+    bad = _Perturbing(Exchange(epilogue=ep, algo="a2a"))
+    ex = AutoExchange(epilogue=ep, extra=[("bad", bad)], trials=1)
+    sizes = [1000 * world, 4096 * world, 111 * world]
+    xs = [[_inputs(10 * r + j, n) for j, n in enumerate(sizes)] for r in range(world)]
+    buckets = [torch.from_numpy(xs[rank][j].copy()) for j in range(len(sizes))]
+    err = io.StringIO()
+    with contextlib.redirect_stderr(err):
+        ex.all_reduce_(buckets, average=True)
+    assert ex.picked[tuple((b.data_ptr(), b.numel(), b.dtype) for b in buckets)] != "bad"
+    assert [n for n, _ in ex.dropped] == ["bad"], ex.dropped
+    if rank == 1:
+        assert "rank 1 drops candidate bad" in err.getvalue(), err.getvalue()
+        assert "bucket 1 at element 17" in err.getvalue(), err.getvalue()
+    for j in range(len(sizes)):
+        want = oracle.reduce_avg([xs[r][j] for r in range(world)], "f32", world)
+        assert np.array_equal(buckets[j].numpy(), want), j
+    # SMA picks separately, with the same check
+    vs = [torch.from_numpy(xs[rank][j].copy()) for j in range(len(sizes))]
+    with contextlib.redirect_stderr(io.StringIO()):
+        ex.sma_(vs, 0.1)
+    assert "bad" not in [ex.picked[k] for k in ex.picked]
+    for j in range(len(sizes)):
+        s = oracle.reduce_k([xs[r][j] for r in range(world)], "f32", "sum")
+        assert np.array_equal(vs[j].numpy(), oracle.sma_blend(xs[rank][j], s, "f32", world, 0.1))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_auto_exchange_drops_a_candidate_with_other_bits(world):
+    run_world("body_auto_exchange_drops_wrong_bits", world)
+
+
+def body_auto_exchange_past_16_ranks(rank, world, use_gpu):
+    # past KF_MAX_INPUTS ranks the rank-order fold cannot run: RCCL's
+    # reduce-scatter is the base candidate and the call goes through
+    from kungfu_amd.p2p import AutoExchange
+    ex = AutoExchange(epilogue=_epilogue(use_gpu))
+    b = torch.full((world * 64,), float(rank + 1))
+    ex.all_reduce_([b])
+    assert torch.equal(b, torch.full_like(b, world * (world + 1) / 2))
+    assert list(ex.picked.values()) == ["rccl_rs"]
+
+
+def test_auto_exchange_past_16_ranks():
+    run_world("body_auto_exchange_past_16_ranks", 17)

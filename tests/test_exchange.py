@@ -89,12 +89,14 @@ def _rand(name, n, seed):
     if name == "bf16":
         from oracle import oracle
         return oracle.f32_to_bf16_bits(rng.standard_normal(n).astype(np.float32))
-    info = np.iinfo({"i32": np.int32, "i8": np.int8, "u8": np.uint8}[name])
+    info = np.iinfo({"i32": np.int32, "i8": np.int8, "u8": np.uint8, "u16": np.uint16}[name])
     return rng.integers(info.min, info.max, n, endpoint=True).astype(info.dtype)
 
 
 def _to_dev(a, name, dev):
     import torch
+    if name == "u16":
+        return torch.from_numpy(np.ascontiguousarray(a).view(np.int16)).to(dev)
     t = torch.from_numpy(np.ascontiguousarray(a))
     if name == "bf16":
         t = t.view(torch.int16).view(torch.bfloat16)
@@ -104,7 +106,7 @@ def _to_dev(a, name, dev):
 def _to_np(t, name):
     import torch
     t = t.cpu()
-    if name == "bf16":
+    if name in ("bf16", "u16"):
         return t.view(torch.int16).numpy().view(np.uint16)
     return t.numpy()
 
@@ -113,7 +115,7 @@ def _to_np(t, name):
 @pytest.mark.parametrize("name,k,avg", [("f32", 2, False), ("f32", 1, True), ("f32", 5, True),
                                         ("bf16", 4, True), ("bf16", 2, False), ("f16", 3, False),
                                         ("i32", 3, False), ("i8", 2, False), ("u8", 8, False),
-                                        ("f64", 2, True)])
+                                        ("f64", 2, True), ("u16", 4, False), ("u16", 8, False)])
 def test_batch_kernel_matches_oracle(name, k, avg):
     """20 buckets (more than one launch of 16), ragged sizes incl. 0, 1 and a
     misaligned bucket, against the oracle's fold / reduce_avg per bucket."""
@@ -220,32 +222,10 @@ def test_world1_native_exchange():
 # ---- the exchange's multi-rank logic over the loopback transport ------------
 
 def _loop_ranks(world, body):
-    """Run body(rank, ex) on `world` threads, each with its own exchange of
-    one loopback group; re-raise the first failure."""
-    import threading
-    import torch
-    from kungfu_amd.exchange import LoopbackGroup, NativeExchange
-    g = LoopbackGroup(world)
-    errs = []
-
-    def run(r):
-        try:
-            torch.cuda.set_device(0)
-            ex = NativeExchange.loopback(g, r)
-            body(r, ex)
-            torch.cuda.synchronize()
-            ex.close()
-        except Exception:
-            errs.append("rank %d: %s" % (r, traceback.format_exc()))
-
-    ts = [threading.Thread(target=run, args=(r,)) for r in range(world)]
-    for t in ts:
-        t.start()
-    for t in ts:
-        t.join(timeout=300)
-    g.close()
-    assert not errs, "\n".join(errs)
-    assert not any(t.is_alive() for t in ts), "a rank did not finish"
+    """body(rank, ex) on `world` threads over the test library's loopback
+    transport (tests/loopback.py, tests/c/kf_testing.cpp)."""
+    from loopback import loop_ranks
+    loop_ranks(world, body)
 
 
 @pytest.mark.gpu
@@ -576,8 +556,9 @@ _W1_CHILD = r"""
 import ctypes, sys
 import numpy as np
 import torch
-sys.path.insert(0, %r)
+sys.path[:0] = [%r, %r]
 from kungfu_amd import _lib
+from loopback import rccl1_exchange
 from kungfu_amd.collective import GradBuckets
 from kungfu_amd.exchange import NativeExchange, Scheduler
 from oracle import oracle
@@ -592,7 +573,7 @@ def rnd(n, dt):
     return torch.randint(max(info.min, -2**31), min(info.max, 2**31 - 1), (n,), device=dev,
                          generator=g).to(dt)
 for algo in ("rs", "a2a", "auto"):
-    ex = NativeExchange(algo=algo, device=dev)
+    ex = rccl1_exchange(algo)
     # C3's shape: 64 grouped 4 MiB buckets, S-SGD average (x / 1 == x)
     gb = GradBuckets([64 << 20], torch.float32, dev, 1, n_buckets=64)
     gb.views[0].copy_(rnd(64 << 20, torch.float32))
@@ -671,8 +652,8 @@ print("W1_RCCL_OK")
 
 @pytest.mark.gpu
 def test_world1_rccl_entry_points():
-    """A one-rank exchange forced through librccl's own entry points
-    (KUNGFU_AMD_EXCHANGE_W1_COLLECTIVES=1: reduce-scatter / all-to-all /
+    """A one-rank exchange through librccl's own entry points (the test
+    library's rccl1 transport, which has no world-1 copy: reduce-scatter / all-to-all /
     all-gather groups, the batched epilogue, the order broadcast) with the
     exchange's exact arguments — C3's 64 grouped buckets, every RCCL dtype
     and the all-to-all-only int16, in and out of place, SMA, the scheduler —
@@ -681,8 +662,7 @@ def test_world1_rccl_entry_points():
     import subprocess
     import sys
     _gpu()
-    env = dict(os.environ, KUNGFU_AMD_EXCHANGE_W1_COLLECTIVES="1")
-    r = subprocess.run([sys.executable, "-c", _W1_CHILD % os.path.dirname(HERE)], env=env,
+    r = subprocess.run([sys.executable, "-c", _W1_CHILD % (os.path.dirname(HERE), HERE)],
                        capture_output=True, text=True, timeout=240)
     assert r.returncode == 0 and "W1_RCCL_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
 
@@ -716,3 +696,145 @@ def test_sma_blend_batch_matches_single(name, np_):
         if name in ("f32", "bf16"):
             want = oracle.sma_blend(vs0[j], ss[j], name, np_, 0.1)
             assert np.array_equal(_to_np(a[j], name), want), j
+
+
+# ---- name-keyed all-reduce and splits ----------------------------------------
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_named_all_reduce_any_order(world):
+    """kf_exchange_all_reduce_named: every rank starts the step's names in its
+    own random order, with random gaps, from its own thread; tensors pair by
+    name (the reference's per-name mailbox, handler/collective.go:48-64), so
+    each result is the oracle's rank-order fold of that name's buffers on
+    every rank. Three steps reuse the names; f32 /np, bf16, i32 MAX and a u16
+    SUM (all-to-all fold) are mixed, so one cycle can complete names of
+    different kinds (one batched call per kind)."""
+    import time
+    import torch
+    from oracle import oracle
+    dev = _gpu()
+    kinds = [("f32", "sum", True), ("bf16", "sum", False), ("i32", "max", False),
+             ("u16", "sum", False)]
+    names = ["t%02d/%s" % (i, kinds[i % 4][0]) for i in range(14)]
+    sizes = [1, 7, 4099, 100003, world * 1000 + 1, 65536, 3, 262147, 5, 777, 1 << 16, 9, 31,
+             4096]
+
+    def data(r, step, i):
+        name = kinds[i % 4][0]
+        if name == "u16":
+            return np.random.default_rng(7 * r + 1000 * step + i).integers(
+                0, 65535, sizes[i]).astype(np.uint16)
+        return _rand(name, sizes[i], 10000 * step + 100 * r + i)
+
+    def body(rank, ex):
+        import torch
+        s = torch.cuda.Stream()
+        for step in range(3):
+            rng = np.random.default_rng(31 * rank + step)
+            hs = [data(rank, step, i) for i in range(len(names))]
+            bufs = []
+            for i, h in enumerate(hs):
+                if kinds[i % 4][0] == "u16":
+                    bufs.append(torch.from_numpy(h.view(np.int16)).to(dev))
+                else:
+                    bufs.append(_to_dev(h, kinds[i % 4][0], dev))
+            torch.cuda.synchronize()
+            seen = []
+            with torch.cuda.stream(s):
+                for i in rng.permutation(len(names)):
+                    time.sleep(float(rng.random()) * 0.002)
+                    name, op, avg = kinds[i % 4]
+                    if name == "u16":
+                        from kungfu_amd import _lib
+                        cb = _lib.DONE_FN(lambda st, a: seen.append(st))
+                        ex._named_keep = getattr(ex, "_named_keep", []) + [cb]
+                        _lib.check(ex.lib.kf_exchange_all_reduce_named(
+                            ex._h, names[i].encode(), bufs[i].data_ptr(), bufs[i].data_ptr(),
+                            bufs[i].numel(), 0x00208, 0, 0, 0, s.cuda_stream, cb, None), "u16")
+                    else:
+                        ex.all_reduce_named(names[i], bufs[i], op=op, average=avg,
+                                            callback=lambda n, st: seen.append(st))
+            ex.wait_named()
+            assert len(seen) == len(names) and all(st == 0 for st in seen), seen
+            for i in range(len(names)):
+                name, op, avg = kinds[i % 4]
+                ins = [data(r, step, i) for r in range(world)]
+                if avg:
+                    want = oracle.reduce_avg(ins, name, world)
+                else:
+                    want = oracle.reduce_k(ins, name, op)
+                got = (bufs[i].cpu().numpy().view(np.uint16) if name == "u16"
+                       else _to_np(bufs[i], name))
+                assert np.array_equal(got, want), (step, names[i])
+
+    _loop_ranks(world, body)
+
+
+@pytest.mark.gpu
+def test_named_all_reduce_mismatch_fails_on_every_rank():
+    """A name whose count differs across ranks fails with KF_ERR_ARG on every
+    rank (no collective is issued for it); the other names still complete."""
+    import torch
+    from kungfu_amd import _lib
+    from oracle import oracle
+    dev = _gpu()
+    world = 2
+
+    def body(rank, ex):
+        import torch
+        ok = torch.full((1000,), float(rank + 1), device=dev)
+        bad = torch.ones(100 + rank, device=dev)
+        st = {}
+        ex.all_reduce_named("bad", bad, callback=lambda n, s: st.__setitem__(n, s))
+        ex.all_reduce_named("ok", ok, callback=lambda n, s: st.__setitem__(n, s))
+        with pytest.raises(_lib.KungFuAMDError, match="differ across ranks"):
+            ex.wait_named()
+        assert st == {"bad": 3, "ok": 0}, st
+        assert torch.all(ok == 3.0)
+        # the exchange keeps working, and a name may be reused
+        ex.all_reduce_named("bad", torch.ones(5, device=dev))
+        ex.wait_named()
+        # one name outstanding twice is refused at once
+        x = torch.ones(8, device=dev)
+        ex.all_reduce_named("twice", x)
+        with pytest.raises(_lib.KungFuAMDError, match="outstanding"):
+            ex.all_reduce_named("twice", x)
+        ex.wait_named()
+        del oracle
+
+    _loop_ranks(world, body)
+
+
+@pytest.mark.gpu
+def test_split_local_scope():
+    """kf_exchange_split (gpu_collective::new_local / new_group): world 4 as 2
+    emulated hosts of 2 ranks (color = rank // 2); each sub-exchange
+    all-reduces within its host only, ranks ordered by key (here reversed), and
+    color -1 joins none. A second split of the sub-exchange still works."""
+    import torch
+    from oracle import oracle
+    dev = _gpu()
+    world = 4
+    xs = [_rand("f32", 30011, 50 + r) for r in range(world)]
+
+    def body(rank, ex):
+        import torch
+        loc = ex.split(rank // 2, key=-rank)
+        assert (loc.world, loc.rank) == (2, 1 - rank % 2), (loc.world, loc.rank)
+        x = _to_dev(xs[rank], "f32", dev)
+        loc.all_reduce_([x], average=True)
+        torch.cuda.synchronize()
+        host = [xs[2 * (rank // 2) + 1], xs[2 * (rank // 2)]]  # the sub-exchange's rank order
+        assert np.array_equal(_to_np(x, "f32"), oracle.reduce_avg(host, "f32", 2))
+        none = ex.split(-1 if rank == 3 else 0)
+        assert (none is None) == (rank == 3)
+        if none is not None:
+            assert none.world == 3
+            none.close()
+        solo = loc.split(loc.rank)
+        assert solo.world == 1
+        solo.close()
+        loc.close()
+
+    _loop_ranks(world, body)

@@ -252,3 +252,66 @@ def test_auto_exchange_gpu(world):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     _run(_auto_body, world)
+
+
+def _auto_guard_body(rank, world, port, errq):
+    """AutoExchange's same-bits guard on GPU buckets: an extra candidate that
+    runs the P2P pull exchange and then flips one bit on the last rank (a
+    stand-in for a shard served stale over xGMI) is dropped on EVERY rank,
+    the rank that saw the difference says where, and the result is the
+    oracle's rank-order average."""
+    sys.path[:0] = [ROOT, HERE]
+    import contextlib
+    import io
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from kungfu_amd.collective import GradBuckets
+        from kungfu_amd.p2p import AutoExchange, PeerExchange
+        from oracle import oracle
+        dev = torch.device("cuda:0")
+
+        class Perturbing:
+            def __init__(self):
+                self.inner = PeerExchange()
+
+            def all_reduce_(self, buckets, op="sum", average=False, coalesce=True):
+                self.inner.all_reduce_(buckets, op=op, average=average)
+                if rank == world - 1:
+                    buckets[2].view(torch.int32)[4097] ^= 1
+                return buckets
+
+            def finish(self):
+                self.inner.finish()
+
+        sizes = [70001, 333, 120000]
+        gb = GradBuckets(sizes, torch.float32, dev, world, n_buckets=3)
+        ex = AutoExchange(trials=1, extra=[("p2p_stale", Perturbing())])
+        xs = [[np.random.default_rng(100 * r + i).standard_normal(n).astype(np.float32)
+               for i, n in enumerate(sizes)] for r in range(world)]
+        for v, x in zip(gb.views, xs[rank]):
+            v.copy_(torch.from_numpy(x))
+        err = io.StringIO()
+        with contextlib.redirect_stderr(err):
+            ex.all_reduce_(gb.buckets, average=True)
+        assert "p2p_stale" not in ex.picked.values(), ex.picked
+        assert "p2p_stale" in [n for n, _ in ex.dropped], ex.dropped
+        if rank == world - 1:
+            assert "drops candidate p2p_stale" in err.getvalue(), err.getvalue()
+            assert "bucket 2 at element 4097" in err.getvalue(), err.getvalue()
+        for i, v in enumerate(gb.views):
+            want = oracle.reduce_avg([xs[r][i] for r in range(world)], "f32", world)
+            assert np.array_equal(v.cpu().numpy(), want), i
+        ex.close()
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:
+        errq.put("rank %d: %s" % (rank, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_auto_exchange_drops_wrong_bits_gpu(world):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _run(_auto_guard_body, world)

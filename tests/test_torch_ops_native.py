@@ -69,3 +69,90 @@ def test_cuda_ops_world1():
     assert torch.equal(x0, torch.arange(10, dtype=torch.float32, device=dev).reshape(2, 5))
     ar, ara = ops._op_maps()
     assert ar["torch.cuda.FloatTensor"] is m.all_reduce_cuda
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_cuda_ops_multi_rank_by_name(world):
+    """all_reduce_cuda_async pairs tensors by NAME across ranks, as the
+    reference's does (collective.cpp:32-55 hands tensor_name to
+    Peer::AllReduce, whose messages pair by name): `world` ranks (threads,
+    each with its own exchange over the test library's loopback transport,
+    bound with bind_exchange) start the same named tensors in different
+    random orders with random gaps; every result equals the oracle's
+    rank-order fold of that name's tensors — f32 sum, i32 max, bf16 sum. Then
+    the blocking all_reduce_cuda in one order, and the kungfu.torch.ops mirror
+    (inplace_all_reduce_async_op) over the same binding."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import time
+    import numpy as np
+    from loopback import loop_ranks
+    from oracle import oracle
+    from kungfu_amd.torch import ops
+    m = _mod()
+    dev = torch.device("cuda:0")
+    kinds = [("f32", "sum"), ("i32", "max"), ("bf16", "sum")]
+    sizes = [1, 1000, 65537, 7, 300001, 4096, 33, 2 * 4096 + 3, 5]
+    names = ["layer%d.%s" % (i, kinds[i % 3][0]) for i in range(len(sizes))]
+
+    def host(r, step, i):
+        name = kinds[i % 3][0]
+        rng = np.random.default_rng(1000 * step + 10 * r + i)
+        if name == "i32":
+            return rng.integers(-2 ** 31, 2 ** 31 - 1, sizes[i]).astype(np.int32)
+        x = rng.standard_normal(sizes[i]).astype(np.float32)
+        return oracle.f32_to_bf16_bits(x) if name == "bf16" else x
+
+    def dev_t(a, name):
+        t = torch.from_numpy(np.ascontiguousarray(a))
+        if name == "bf16":
+            t = t.view(torch.int16).view(torch.bfloat16)
+        return t.to(dev)
+
+    def back(t, name):
+        t = t.cpu()
+        return t.view(torch.int16).numpy().view(np.uint16) if name == "bf16" else t.numpy()
+
+    def want(step, i):
+        name, op = kinds[i % 3]
+        return oracle.reduce_k([host(r, step, i) for r in range(world)], name, op)
+
+    def body(rank, ex):
+        m.bind_exchange(ex._h)
+        try:
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                for step in range(2):
+                    rng = np.random.default_rng(77 * rank + step)
+                    xs = [dev_t(host(rank, step, i), kinds[i % 3][0]) for i in range(len(sizes))]
+                    outs = [torch.empty_like(x) for x in xs]
+                    hs = []
+                    for i in rng.permutation(len(sizes)):
+                        time.sleep(float(rng.random()) * 0.003)
+                        x = xs[i]
+                        hs.append(m.all_reduce_cuda_async(x, outs[i], x.type(), kinds[i % 3][1],
+                                                          names[i]))
+                    m.wait_all_handles(hs)
+                    for i in range(len(sizes)):
+                        assert np.array_equal(back(outs[i], kinds[i % 3][0]), want(step, i)), \
+                            (rank, step, names[i])
+                # the blocking op: same order on every rank (the reference's "" name)
+                for i in range(len(sizes)):
+                    x = dev_t(host(rank, 5, i), kinds[i % 3][0])
+                    m.all_reduce_cuda(x, x, x.type(), kinds[i % 3][1])
+                    assert np.array_equal(back(x, kinds[i % 3][0]), want(5, i)), (rank, i)
+                # the Python mirror, in place, any order
+                rng = np.random.default_rng(5 + rank)
+                xs = [dev_t(host(rank, 9, i), kinds[i % 3][0]) for i in range(len(sizes))]
+                hs = {}
+                for i in rng.permutation(len(sizes)):
+                    hs[i] = ops.inplace_all_reduce_async_op(xs[i], names[i], kinds[i % 3][1])
+                ops.wait_all_handles([hs[i] for i in range(len(sizes))])
+                for i in range(len(sizes)):
+                    assert np.array_equal(back(xs[i], kinds[i % 3][0]), want(9, i)), (rank, i)
+            torch.cuda.synchronize()
+        finally:
+            m.bind_exchange(0)
+
+    loop_ranks(world, body)
