@@ -356,6 +356,11 @@ int kf_session_all_reduce_async(kf_session_t *s, const void *send, void *recv,
  * device-mode sessions use a workspace of their own in HBM. */
 int kf_session_barrier(kf_session_t *s);
 int kf_session_wait_all(kf_session_t *s);
+/* Peer::Rank / Size / LocalRank / LocalSize / HostCount (include/kungfu/
+ * peer.hpp): peers with the same IPv4 share a host; local ranks follow the
+ * peer list's order. Any pointer may be NULL. */
+int kf_session_info(kf_session_t *s, int *rank, int *size, int *local_rank, int *local_size,
+                    int *host_count);
 void kf_session_destroy(kf_session_t *s);
 const char *kf_session_last_error(void);
 
@@ -573,6 +578,34 @@ kf_exchange_t *kf_exchange_create_transport(const kf_transport_ops *ops, void *c
  * this rank joins none (returns NULL with KF_OK in *status). The local scope
  * is color = host index, key = rank (kf_exchange_create_local). */
 kf_exchange_t *kf_exchange_split(kf_exchange_t *ex, int color, int key, int *status);
+
+/* ---- hierarchical all-reduce (several hosts, several GPUs each) -----------
+ * gpu_collective::new_local (srcs/cpp/src/nccl/gpu_collective.cpp:202-212):
+ * an exchange over this host's ranks of the session `s` (same IPv4), ranked
+ * in the session's order. Each host's first rank creates the RCCL id; every
+ * host's id travels in ONE session all-reduce of hosts x 128 bytes (one
+ * contributor per slot, so the sum is the id). Collective over `s`. */
+kf_exchange_t *kf_exchange_create_local(kf_session_t *s, int device);
+/* ScheduledHierarchicalNcclAllReduce (srcs/cpp/src/tensorflow/ops/gpu/
+ * collective.cpp:108-162: ncclReduce in the host -> CrossAllReduceGpu over
+ * the hosts, nccl/controller.cpp:7-39 -> ncclBroadcast in the host), with the
+ * bucket sharded across the host's GPUs when every host has as many:
+ *   1. local reduce-scatter (algo: RCCL's, or the all-to-all + HIP rank-order
+ *      fold) — local rank j holds shard j of its host's sum;
+ *   2. the shard all-reduced across hosts by the device-mode session `cross`
+ *      among the ranks with the same local rank (kf_session_subset_all_reduce,
+ *      one tree per local rank), so every link carries 1/local_size of it;
+ *   3. average: / size() on the shard (kf_bucket_div);
+ *   4. local in-place all-gather.
+ * Hosts of different sizes take the reference's path: local all-reduce, the
+ * hosts' first ranks all-reduce across hosts, local broadcast. `local` must
+ * hold exactly this host's ranks in session order (kf_exchange_create_local,
+ * or any transport with that layout); every rank calls with the same name,
+ * count, dtype and op, in the same order. Buffers are HBM; queued on
+ * `stream`, blocking on the host while the cross-host step runs. */
+int kf_hier_all_reduce(kf_exchange_t *local, kf_session_t *cross, const void *send, void *recv,
+                       size_t count, KungFu_Datatype dt, KungFu_Op op, int average, int algo,
+                       const char *name, void *stream);
 
 #pragma GCC visibility pop
 

@@ -85,6 +85,9 @@ EXPORTED = (
     "kf_exchange_wait_named",
     "kf_exchange_create_transport",
     "kf_exchange_split",
+    "kf_session_info",
+    "kf_exchange_create_local",
+    "kf_hier_all_reduce",
 )
 
 STATUS = {
@@ -308,6 +311,13 @@ def load():
     lib.kf_exchange_create_transport.restype = c_void_p
     lib.kf_exchange_split.argtypes = [c_void_p, c_int, c_int, P(c_int)]
     lib.kf_exchange_split.restype = c_void_p
+    lib.kf_session_info.argtypes = [c_void_p, P(c_int), P(c_int), P(c_int), P(c_int), P(c_int)]
+    lib.kf_session_info.restype = c_int
+    lib.kf_exchange_create_local.argtypes = [c_void_p, c_int]
+    lib.kf_exchange_create_local.restype = c_void_p
+    lib.kf_hier_all_reduce.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_int,
+                                       c_int, c_int, c_int, ctypes.c_char_p, c_void_p]
+    lib.kf_hier_all_reduce.restype = c_int
     _lib = lib
     return lib
 

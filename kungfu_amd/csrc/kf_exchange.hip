@@ -61,6 +61,7 @@
 
 // kf_session.hip (library-internal)
 int kf_session_device_mode_internal(const kf_session_t *s);
+int kf_session_hosts_internal(const kf_session_t *s, int *host_of);
 
 namespace
 {
@@ -403,9 +404,13 @@ struct kf_exchange {
     void release_ws(hipStream_t s);
     // sma_alpha != nullptr: SMA, sends = the variables, recvs = the sum workspaces,
     // each variable blended once its sum is gathered
+    // phases: which of the three to run (kAll; the hierarchical all-reduce
+    // runs 1+2, its cross-host step, then 3)
     int batch(const void *const *sends, void *const *recvs, const size_t *counts, int nb,
               KungFu_Datatype dt, KungFu_Op op, int average, int algo, hipStream_t s,
-              const double *sma_alpha = nullptr);
+              const double *sma_alpha = nullptr, int phases = 7);
+    int hier(kf_session_t *cross, const void *send, void *recv, size_t count, KungFu_Datatype dt,
+             KungFu_Op op, int average, int algo, const std::string &name, hipStream_t s);
     kf_exchange *split(int color, int key, int *status);  // caller holds mu
     int start_named();                                     // caller holds mu
     void issue_loop();
@@ -496,13 +501,13 @@ static int resolve_algo(int algo, KungFu_Datatype dt, KungFu_Op op, int world, i
 
 int kf_exchange::batch(const void *const *sends, void *const *recvs, const size_t *counts,
                        int nb, KungFu_Datatype dt, KungFu_Op op, int average, int algo,
-                       hipStream_t s, const double *sma_alpha)
+                       hipStream_t s, const double *sma_alpha, int phases)
 {
     const int sz = tsize(dt);
     const int W = world, r = rank;
     const bool sma = sma_alpha != nullptr;
     if (W == 1 && builtin) {  // a single peer: the sum is the bucket, x / 1 == x
-        for (int b = 0; b < nb; ++b) {
+        for (int b = 0; b < nb && (phases & 1); ++b) {
             if (counts[b] && sends[b] != recvs[b]) {
                 KF_HIP(hipMemcpyAsync(recvs[b], sends[b], counts[b] * sz, hipMemcpyDeviceToDevice, s));
             }
@@ -523,7 +528,7 @@ int kf_exchange::batch(const void *const *sends, void *const *recvs, const size_
     // workspace: received shards (all-to-all) and gathered tails
     std::vector<size_t> wsoff(nb, 0), toff(nb, 0);
     size_t need = 0;
-    for (int b = 0; b < nb; ++b) {
+    for (int b = 0; b < nb && (phases & 3); ++b) {
         const size_t q = counts[b] / W, t = counts[b] % W;
         if (a == KF_ALGO_ALL_TO_ALL && q) {
             wsoff[b] = need;
@@ -644,12 +649,12 @@ int kf_exchange::batch(const void *const *sends, void *const *recvs, const size_
         return KF_OK;
     };
 
-    const int G = std::min(groups, nb);
+    const int G = phases == 7 ? std::min(groups, nb) : 1;
     if (G <= 1) {
-        rc = phase1(0, nb);
-        if (rc == KF_OK) rc = phase2(0, nb, s);
-        if (rc == KF_OK) rc = phase3(0, nb);
-        if (rc == KF_OK) rc = blend(0, nb, s);
+        if (phases & 1) rc = phase1(0, nb);
+        if (rc == KF_OK && (phases & 2)) rc = phase2(0, nb, s);
+        if (rc == KF_OK && (phases & 4)) rc = phase3(0, nb);
+        if (rc == KF_OK && phases == 7) rc = blend(0, nb, s);
         if (need) release_ws(s);  // whatever ran reads the workspace in stream order
         return rc;
     }
@@ -772,6 +777,83 @@ kf_exchange *kf_exchange::split(int color, int key, int *status)
     ex->groups = groups;
     *status    = KF_OK;
     return ex;
+}
+
+// The hierarchical all-reduce (kf_hier_all_reduce); caller holds mu.
+int kf_exchange::hier(kf_session_t *cross, const void *send, void *recv, size_t count,
+                      KungFu_Datatype dt, KungFu_Op op, int average, int algo,
+                      const std::string &name, hipStream_t s)
+{
+    if (kf_session_device_mode_internal(cross) != 1) {
+        return fail(KF_ERR_ARG, "kf_hier_all_reduce: the cross-host session must be device-mode");
+    }
+    int grank = 0, gsize = 0;
+    (void)kf_session_info(cross, &grank, &gsize, nullptr, nullptr, nullptr);
+    std::vector<int> host(gsize);
+    (void)kf_session_hosts_internal(cross, host.data());
+    const int H = *std::max_element(host.begin(), host.end()) + 1;
+    std::vector<std::vector<int>> members(H);  // global ranks per host, in order
+    std::vector<int> lrank(gsize);
+    for (int g = 0; g < gsize; ++g) {
+        lrank[g] = static_cast<int>(members[host[g]].size());
+        members[host[g]].push_back(g);
+    }
+    if (lrank[grank] != rank || static_cast<int>(members[host[grank]].size()) != world) {
+        return fail(KF_ERR_ARG, "kf_hier_all_reduce: the local exchange must hold this host's "
+                                "ranks of the session, in its order");
+    }
+    bool equal = true;
+    for (auto &m : members) equal = equal && m.size() == members[0].size();
+    const int W = world;
+    const int sz = tsize(dt);
+    char *out    = static_cast<char *>(recv);
+    std::vector<int32_t> forest(gsize);
+    int rc = KF_OK;
+    auto scale = [&](char *p, size_t n) -> int {
+        if (!average || !n) return KF_OK;
+        const int e = kf_bucket_div(p, n, dt, gsize, s);
+        return e == KF_OK ? KF_OK : fail(e, "kf_hier_all_reduce: / np");
+    };
+    if (equal) {
+        // one tree per local rank: the ranks holding the same shard, rooted
+        // at host 0's (graph.go:46-62's forest array)
+        for (int g = 0; g < gsize; ++g) forest[g] = members[0][lrank[g]];
+        const size_t q = count / W, t = count % W;
+        rc = batch(&send, &recv, &count, 1, dt, op, 0, algo, s, nullptr, 3);
+        if (rc == KF_OK && q) {
+            char *sh = out + rank * q * sz;
+            rc = kf_session_subset_all_reduce(cross, sh, sh, q, dt, op, forest.data(),
+                                              (name + "/shard").c_str(), s);
+            if (rc != KF_OK) rc = fail(rc, std::string("cross-host shard all-reduce: ") +
+                                               kf_session_last_error());
+            if (rc == KF_OK) rc = scale(sh, q);
+        }
+        if (rc == KF_OK && t) {  // every local rank holds its host's tail sum
+            char *tl = out + q * W * sz;
+            rc = kf_session_subset_all_reduce(cross, tl, tl, t, dt, op, forest.data(),
+                                              (name + "/tail").c_str(), s);
+            if (rc != KF_OK) rc = fail(rc, std::string("cross-host tail all-reduce: ") +
+                                               kf_session_last_error());
+            if (rc == KF_OK) rc = scale(tl, t);
+        }
+        if (rc == KF_OK) rc = batch(&recv, &recv, &count, 1, dt, op, 0, algo, s, nullptr, 4);
+        return rc;
+    }
+    // hosts of different sizes: the reference's structure (collective.cpp:
+    // 144-160) — host all-reduce, the hosts' first ranks across, host broadcast
+    for (int g = 0; g < gsize; ++g) forest[g] = lrank[g] == 0 ? members[0][0] : g;
+    rc = batch(&send, &recv, &count, 1, dt, op, 0, algo, s);
+    if (rc == KF_OK) {
+        rc = kf_session_subset_all_reduce(cross, recv, recv, count, dt, op, forest.data(),
+                                          name.c_str(), s);
+        if (rc != KF_OK) rc = fail(rc, std::string("cross-host all-reduce: ") + kf_session_last_error());
+    }
+    if (rc == KF_OK && rank == 0) rc = scale(out, count);
+    if (rc == KF_OK && W > 1 && !(builtin && W == 1) && count) {
+        const int e = T->broadcast(recv, recv, count * sz, 0, comm, s);
+        if (e != 0) rc = tfail(e, "host broadcast");
+    }
+    return rc;
 }
 
 // Issue thread: the tasks of the step, strictly in `order`
@@ -1246,6 +1328,73 @@ kf_exchange_t *kf_exchange_split(kf_exchange_t *ex, int color, int key, int *sta
     DeviceGuard g(ex->device);
     std::lock_guard<std::mutex> lk(ex->mu);
     return ex->split(color, key, status);
+}
+
+static int check_bucket_args(kf_exchange_t *ex, const void *const *sends, void *const *recvs,
+                             const size_t *counts, int nb, KungFu_Datatype dt, KungFu_Op op,
+                             int average);
+
+kf_exchange_t *kf_exchange_create_local(kf_session_t *s, int device)
+{
+    int rank = 0, size = 0, lr = 0, ls = 0, hosts = 0;
+    if (!s || kf_session_info(s, &rank, &size, &lr, &ls, &hosts) != KF_OK) {
+        fail(KF_ERR_ARG, "kf_exchange_create_local: no session");
+        return nullptr;
+    }
+    std::vector<int> host(size);
+    (void)kf_session_hosts_internal(s, host.data());
+    const size_t bytes = static_cast<size_t>(hosts) * KF_UNIQUE_ID_BYTES;
+    std::vector<unsigned char> ids(bytes, 0);
+    int rc = KF_OK;
+    std::string why;
+    if (lr == 0 && kf_exchange_unique_id(ids.data() + host[rank] * KF_UNIQUE_ID_BYTES) != KF_OK) {
+        why = t_ex_error;  // the host's peers still take part: they get zeros and fail in init
+        rc  = KF_ERR_RCCL;
+    }
+    // every host's id in one all-reduce: one contributor per slot, so the sum is the id
+    int e = KF_OK;
+    if (kf_session_device_mode_internal(s) == 0) {
+        e = kf_session_all_reduce(s, ids.data(), ids.data(), bytes, KungFu_UINT8, KungFu_SUM,
+                                  "local nccl ids", nullptr);
+    } else {
+        DeviceGuard g(device);
+        void *d = nullptr;
+        if (hipMalloc(&d, bytes) != hipSuccess) {
+            fail(KF_ERR_HIP, "kf_exchange_create_local: hipMalloc");
+            return nullptr;
+        }
+        e = hipMemcpy(d, ids.data(), bytes, hipMemcpyHostToDevice) == hipSuccess ? KF_OK : KF_ERR_HIP;
+        if (e == KF_OK) {
+            e = kf_session_all_reduce(s, d, d, bytes, KungFu_UINT8, KungFu_SUM, "local nccl ids",
+                                      nullptr);
+        }
+        if (e == KF_OK && hipMemcpy(ids.data(), d, bytes, hipMemcpyDeviceToHost) != hipSuccess) {
+            e = KF_ERR_HIP;
+        }
+        (void)hipFree(d);
+    }
+    if (e != KF_OK) {
+        fail(e, std::string("kf_exchange_create_local: sharing the ids: ") + kf_session_last_error());
+        return nullptr;
+    }
+    if (rc != KF_OK) {
+        fail(rc, why);
+        return nullptr;
+    }
+    return kf_exchange_create(ids.data() + host[rank] * KF_UNIQUE_ID_BYTES, lr, ls, device);
+}
+
+int kf_hier_all_reduce(kf_exchange_t *local, kf_session_t *cross, const void *send, void *recv,
+                       size_t count, KungFu_Datatype dt, KungFu_Op op, int average, int algo,
+                       const char *name, void *stream)
+{
+    if (!cross || !name) return fail(KF_ERR_ARG, "kf_hier_all_reduce: bad arguments");
+    int rc = check_bucket_args(local, &send, &recv, &count, 1, dt, op, average);
+    if (rc != KF_OK || count == 0) return rc;
+    DeviceGuard g(local->device);
+    std::lock_guard<std::mutex> lk(local->mu);
+    return local->hier(cross, send, recv, count, dt, op, average, algo, name,
+                       static_cast<hipStream_t>(stream));
 }
 
 static int check_bucket_args(kf_exchange_t *ex, const void *const *sends, void *const *recvs,

@@ -1373,6 +1373,28 @@ int kf_session_wait_all(kf_session_t *s)
     return s->wait_all();
 }
 
+int kf_session_info(kf_session_t *s, int *rank, int *size, int *local_rank, int *local_size,
+                    int *host_count)
+{
+    if (!s) return KF_ERR_ARG;
+    int lr = 0, ls = 0;
+    std::vector<uint32_t> ips;
+    for (int r = 0; r < s->size; ++r) {
+        const uint32_t ip = s->peers[r].ip;
+        if (std::find(ips.begin(), ips.end(), ip) == ips.end()) ips.push_back(ip);
+        if (ip == s->peers[s->rank].ip) {
+            if (r < s->rank) ++lr;
+            ++ls;
+        }
+    }
+    if (rank) *rank = s->rank;
+    if (size) *size = s->size;
+    if (local_rank) *local_rank = lr;
+    if (local_size) *local_size = ls;
+    if (host_count) *host_count = static_cast<int>(ips.size());
+    return KF_OK;
+}
+
 void kf_session_destroy(kf_session_t *s) { delete s; }
 
 const char *kf_session_last_error(void) { return t_sess_error.c_str(); }
@@ -1382,3 +1404,18 @@ const char *kf_session_last_error(void) { return t_sess_error.c_str(); }
 // library-internal (hidden): whether a session moves device or host buffers
 // (kf_exchange.hip broadcasts the RCCL id through it)
 int kf_session_device_mode_internal(const kf_session_t *s) { return s ? s->device_mode : -1; }
+
+// library-internal: the host index of every rank (distinct IPv4 addresses in
+// order of first appearance, the reference's host list, plan/peerlist.go)
+int kf_session_hosts_internal(const kf_session_t *s, int *host_of)
+{
+    if (!s || !host_of) return KF_ERR_ARG;
+    std::vector<uint32_t> ips;
+    for (int r = 0; r < s->size; ++r) {
+        const uint32_t ip = s->peers[r].ip;
+        auto it           = std::find(ips.begin(), ips.end(), ip);
+        host_of[r]        = static_cast<int>(it - ips.begin());
+        if (it == ips.end()) ips.push_back(ip);
+    }
+    return KF_OK;
+}

@@ -147,10 +147,17 @@ std::shared_ptr<Pending> start(const torch::Tensor &input, torch::Tensor &output
     p->input      = input;
     p->output     = output;
     auto *ref     = new std::shared_ptr<Pending>(p);
-    const int rc  = kf_exchange_all_reduce_named(ex, name.c_str(), input.data_ptr(),
-                                                output.data_ptr(),
-                                                static_cast<size_t>(input.numel()), dt, op, 0,
-                                                KF_ALGO_AUTO, s, on_done, ref);
+    void *in_ptr = input.data_ptr(), *out_ptr = output.data_ptr();
+    const size_t n = static_cast<size_t>(input.numel());
+    int rc;
+    {
+        // the exchange may wait for its negotiation thread (which runs the
+        // collectives): never with the GIL held, so other Python threads
+        // (other ranks in a test, the training loop) keep running
+        py::gil_scoped_release nogil;
+        rc = kf_exchange_all_reduce_named(ex, name.c_str(), in_ptr, out_ptr, n, dt, op, 0,
+                                          KF_ALGO_AUTO, s, on_done, ref);
+    }
     if (rc != KF_OK) {
         delete ref;
         check(rc, "kf_exchange_all_reduce_named");

@@ -110,3 +110,51 @@ def test_cpp_peer_fake_agent(peer_binary, np_, mode):
     # fake_agent.cpp:15-44: iota summed over np peers == i * np, host buffers
     # (the drop-in's HIP fold) and HBM buffers (the device session)
     _peers(peer_binary, np_, mode)
+
+
+@pytest.fixture(scope="module")
+def hier_binary(tmp_path_factory):
+    """tests/c/test_hier.cpp: the hierarchical all-reduce (kf_hier_all_reduce,
+    kf_exchange_create_local, kf_session_info) from a C++ host, the C ABI
+    alone: device-mode sessions across emulated hosts, the test library's
+    loopback inside a host."""
+    out = str(tmp_path_factory.mktemp("ch") / "test_hier")
+    lib = os.path.join(ROOT, "kungfu_amd")
+    tl = os.path.join(ROOT, "tests", "c")
+    if not os.path.exists(os.path.join(tl, "libkf_testing.so")):
+        subprocess.run(["make", "-s", "-C", tl], check=True)
+    subprocess.run(["g++", "-std=c++17", "-Wall", "-Wextra", "-Werror", "-D__HIP_PLATFORM_AMD__",
+                    "-I", os.path.join(ROOT, "include"), "-I", tl, "-I", "/opt/rocm/include",
+                    os.path.join(tl, "test_hier.cpp"),
+                    "-L", lib, "-lkungfu_amd", "-Wl,-rpath," + lib,
+                    "-L", tl, "-lkf_testing", "-Wl,-rpath," + tl,
+                    "-L", "/opt/rocm/lib", "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib",
+                    "-lpthread", "-o", out], check=True)
+    return out
+
+
+def _hier_args():
+    import socket
+    import tempfile
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return [str(20000 + port % 20000), tempfile.mkdtemp(prefix="kfh")]
+
+
+def test_cpp_hier_host_builds(hier_binary):
+    r = subprocess.run([hier_binary] + _hier_args(), capture_output=True, text=True, timeout=300)
+    assert r.returncode in (0, 77), r.stdout + r.stderr
+
+
+@pytest.mark.gpu
+def test_cpp_hier_all_reduce_on_gpu(hier_binary):
+    """2 emulated hosts x 2 ranks (sharded: local reduce-scatter or all-to-all
+    fold -> cross-host session all-reduce of the shard -> / np -> local
+    all-gather), 2 + 1 ranks (the reference's masters path) and 2 x 1 with
+    kf_exchange_create_local: bit-exact against each host's rank-order fold
+    combined across the hosts, / np."""
+    r = subprocess.run([hier_binary] + _hier_args(), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "hier ok" in r.stdout
