@@ -184,3 +184,83 @@ class HierarchicalExchange:
                 self.epilogue.div_(b, self.np)
         if self.local_size > 1:
             dist.broadcast(b, src=master, group=self.local_group)
+
+
+class NativeHierarchicalExchange:
+    """The hierarchical all-reduce behind the C ABI (kf_hier_all_reduce,
+    include/kungfu_amd.h): one native call per bucket does the host's
+    reduce-scatter (RCCL, or the all-to-all + HIP rank-order fold), the
+    cross-host all-reduce of the shard over the device-mode session (one tree
+    of ranks per local rank, kf_session_subset_all_reduce), / np and the host's
+    all-gather; hosts of different sizes take the reference's masters path.
+    The same code a C++ or Go host runs.
+
+    session   a device-mode kungfu_amd.session.Session over ALL peers
+    local     the host's exchange (kungfu_amd.exchange.NativeExchange);
+              default kf_exchange_create_local(session) — gpu_collective::
+              new_local, its RCCL id shared over the session."""
+
+    def __init__(self, session, local=None, device=None, algo="auto"):
+        import ctypes
+        from . import _lib
+        from .exchange import ALGOS, NativeExchange
+        self.lib = _lib.load()
+        self.session = session
+        r, n, lr, ls, hc = (ctypes.c_int() for _ in range(5))
+        _lib.check(self.lib.kf_session_info(session._h, ctypes.byref(r), ctypes.byref(n),
+                                            ctypes.byref(lr), ctypes.byref(ls),
+                                            ctypes.byref(hc)), "kf_session_info")
+        self.rank, self.np, self.world = r.value, n.value, n.value
+        self.local_rank, self.local_size, self.host_count = lr.value, ls.value, hc.value
+        if local is None:
+            dev = torch.device(device if device is not None else
+                               ("cuda:%d" % torch.cuda.current_device()))
+            h = self.lib.kf_exchange_create_local(session._h, dev.index)
+            if not h:
+                raise _lib.KungFuAMDError("kf_exchange_create_local: " +
+                                          self.lib.kf_exchange_last_error().decode())
+            local = NativeExchange.from_handle(h, algo)
+        self.local = local
+        self.algo = ALGOS[algo]
+        self._sums = {}
+
+    def padded_count(self, count, itemsize):
+        return hier_padded_count(count, self.local_size, itemsize)
+
+    def all_reduce_(self, buckets, op="sum", average=False, name="hier"):
+        """In place, queued on the current stream; every rank passes the same
+        buckets (counts), op and name, in the same order."""
+        from . import _lib
+        from .ops import kungfu_dtype
+        red = OP_NAMES[op] if isinstance(op, str) else OP(op)
+        if average and red != OP.SUM:
+            raise ValueError("average requires op='sum'")
+        for i, b in enumerate(buckets):
+            if not b.is_cuda or b.dim() != 1 or not b.is_contiguous():
+                raise ValueError("buckets must be flat contiguous GPU tensors")
+            rc = self.lib.kf_hier_all_reduce(
+                self.local._h, self.session._h, b.data_ptr(), b.data_ptr(), b.numel(),
+                int(kungfu_dtype(b)), int(red), 1 if average else 0, self.algo,
+                ("%s/%d" % (name, i)).encode(), torch.cuda.current_stream(b.device).cuda_stream)
+            _lib.check(rc, "kf_hier_all_reduce")
+        return buckets
+
+    def sma_(self, buckets, alpha, name="hier-sma"):
+        from . import ops
+        sums = []
+        for i, b in enumerate(buckets):
+            key = (i, b.numel(), b.dtype)
+            s = self._sums.get(key)
+            if s is None:
+                s = self._sums[key] = torch.empty_like(b)
+            s.copy_(b)
+            sums.append(s)
+        self.all_reduce_(sums, name=name)
+        for b, s in zip(buckets, sums):
+            ops.sma_blend_(b, s, self.np, alpha)
+        return buckets
+
+    def close(self):
+        if self.local is not None:
+            self.local.close()
+            self.local = None

@@ -8,6 +8,8 @@ import subprocess
 import threading
 import traceback
 
+from kungfu_amd.exchange import NativeExchange  # bound now: a test may stub the module's name
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "c", "libkf_testing.so")
 _lib = None
@@ -45,7 +47,6 @@ class LoopbackGroup:
         assert self._h, "kf_loopback_create(%d)" % world
 
     def exchange(self, rank, algo="auto", device=0):
-        from kungfu_amd.exchange import NativeExchange
         h = self.lib.kf_exchange_create_loopback(self._h, rank, device)
         assert h, self.lib.kf_testing_last_error().decode()
         return NativeExchange.from_handle(h, algo)
@@ -59,7 +60,6 @@ class LoopbackGroup:
 def rccl1_exchange(algo="auto", device=0):
     """A one-rank librccl communicator bound through the transport table: the
     exchange calls librccl's own entry points instead of the world-1 copy."""
-    from kungfu_amd.exchange import NativeExchange
     lib = load()
     h = lib.kf_exchange_create_rccl1(device)
     assert h, lib.kf_testing_last_error().decode()
@@ -80,7 +80,7 @@ def loop_ranks(world, body, timeout=300):
             body(r, ex)
             torch.cuda.synchronize()
             ex.close()
-        except Exception:
+        except BaseException:  # pytest.raises failures are BaseException
             errs.append("rank %d: %s" % (r, traceback.format_exc()))
 
     ts = [threading.Thread(target=run, args=(r,)) for r in range(world)]

@@ -47,15 +47,15 @@ def test_bench_n2_rehearsal_with_p2p_children():
 
 _NATIVE_CHILD = r"""
 import os, sys
-sys.path.insert(0, %r)
+sys.path[:0] = [%r, %r]
 import torch
 import torch.distributed as dist
 import bench
-from kungfu_amd.exchange import NativeExchange
+from loopback import rccl1_exchange
 dev = torch.device("cuda:0")
 torch.cuda.set_device(0)
 dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
-bench._NATIVE["ex"] = NativeExchange(algo="rs", device=dev)
+bench._NATIVE["ex"] = rccl1_exchange("rs")
 n = 16 << 20
 x = torch.randn(n, device=dev, generator=torch.Generator(device=dev).manual_seed(0))
 res = {
@@ -77,40 +77,58 @@ print("NATIVE_SUB_OK" if not bad else "NATIVE_SUB_BAD %%r" %% bad)
 def test_bench_native_subbenchmarks_world1_rccl():
     """bench.py's native sub-benchmark bodies (c4, c5, c3_a2a, c3_fused and the
     pipelined c3/c4/c5) run end to end — parity check, timed loop — over a
-    one-rank RCCL communicator forced through librccl's collectives
-    (KUNGFU_AMD_EXCHANGE_W1_COLLECTIVES=1), so the code the driver's multi-GPU
-    node runs first has run on real RCCL here."""
+    one-rank RCCL communicator bound through the test library's rccl1
+    transport (librccl's collectives, no world-1 copy), so the code the
+    driver's multi-GPU node runs first has run on real RCCL here."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    env = dict(os.environ, KUNGFU_AMD_EXCHANGE_W1_COLLECTIVES="1", MASTER_ADDR="127.0.0.1",
-               MASTER_PORT=str(_port()))
-    r = subprocess.run([sys.executable, "-c", _NATIVE_CHILD % ROOT], env=env, capture_output=True,
-                       text=True, timeout=240, cwd=ROOT)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()))
+    r = subprocess.run([sys.executable, "-c", _NATIVE_CHILD % (ROOT, os.path.join(ROOT, "tests"))],
+                       env=env, capture_output=True, text=True, timeout=240, cwd=ROOT)
     assert r.returncode == 0 and "NATIVE_SUB_OK" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]
 
 
+_BRANCH_CHILD = r"""
+import sys
+sys.path[:0] = [%r, %r]
+import bench
+from kungfu_amd import exchange
+from loopback import rccl1_exchange
+# the primary exchange over librccl's own collectives (one rank, no world-1 copy)
+exchange.NativeExchange = lambda *a, **kw: rccl1_exchange(kw.get("algo", "auto"))
+exchange.NativeExchange.shared_id = staticmethod(lambda group=None: b"\0" * 128)
+sys.argv = ["bench.py"] + %r
+bench.main()
+"""
+
+
 def test_bench_exchange_branch_single_rank_rccl():
-    """bench.py's whole N > 1 branch — shared id, the native exchange as the
-    primary (RCCL), its parity check, the timed C3 step, the agreed
-    sub-benchmark loop and the JSON line — run by one rank on real RCCL
-    (--rehearse-exchange, the one-rank communicator forced through librccl's
-    collectives): the primary must be the native exchange, not the fallback."""
+    """bench.py's whole N > 1 branch — the native exchange as the primary,
+    its parity check, the timed C3 step, the agreed sub-benchmark loop and the
+    JSON line — run by one rank on real RCCL (--rehearse-exchange, the
+    primary's communicator bound through the test library's rccl1 transport,
+    so librccl's collectives run): the primary must be the native exchange,
+    not the fallback, and value is per GPU with value_aggregate beside it."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    env = dict(os.environ, KUNGFU_AMD_EXCHANGE_W1_COLLECTIVES="1", MASTER_ADDR="127.0.0.1",
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1",
                MASTER_PORT=str(_port()), RANK="0", LOCAL_RANK="0", WORLD_SIZE="1")
     extras = "c4,c5,c5_pipe,c4_pipe,c3_pipe,c3_a2a,c3_fused,c4_torch,c5_torch"
-    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--rehearse-exchange", "--steps", "3",
-           "--warmup", "1", "--elems", str(4 << 20), "--extras", extras,
-           "--extras-timeout", "200"]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=260, cwd=ROOT, env=env)
+    argv = ["--rehearse-exchange", "--steps", "3", "--warmup", "1", "--elems", str(4 << 20),
+            "--extras", extras, "--extras-timeout", "200"]
+    code = _BRANCH_CHILD % (ROOT, os.path.join(ROOT, "tests"), argv)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=260,
+                       cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.strip()]
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
-    assert d["value"] > 0 and d["collective"]["exchange"].startswith("native"), d["collective"]
+    assert d["value"] > 0 and d["collective"]["exchange"].startswith("native"), \
+        json.dumps(d["collective"]) + r.stderr[-3000:]
     assert "native_exchange_error" not in d["collective"], d["collective"]
+    assert d["value"] == d["collective"]["algbw_GiBps_per_gpu"]
+    assert abs(d["value_aggregate"] - d["n_gpus"] * d["value"]) < 1e-2
     for k in extras.split(","):
         assert "error" not in d[k] and d[k]["ms_per_step"] > 0, (k, d[k])

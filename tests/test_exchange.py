@@ -775,11 +775,12 @@ def test_named_all_reduce_any_order(world):
 def test_named_all_reduce_mismatch_fails_on_every_rank():
     """A name whose count differs across ranks fails with KF_ERR_ARG on every
     rank (no collective is issued for it); the other names still complete."""
+    import threading
     import torch
     from kungfu_amd import _lib
-    from oracle import oracle
     dev = _gpu()
     world = 2
+    bar = threading.Barrier(world)
 
     def body(rank, ex):
         import torch
@@ -795,13 +796,19 @@ def test_named_all_reduce_mismatch_fails_on_every_rank():
         # the exchange keeps working, and a name may be reused
         ex.all_reduce_named("bad", torch.ones(5, device=dev))
         ex.wait_named()
-        # one name outstanding twice is refused at once
+        # one name outstanding twice is refused at once (rank 1 starts it only
+        # after rank 0 checked, so rank 0's cannot have been issued yet)
         x = torch.ones(8, device=dev)
-        ex.all_reduce_named("twice", x)
-        with pytest.raises(_lib.KungFuAMDError, match="outstanding"):
+        if rank == 0:
+            ex.all_reduce_named("twice", x)
+            with pytest.raises(_lib.KungFuAMDError, match="outstanding"):
+                ex.all_reduce_named("twice", x)
+            bar.wait()
+        else:
+            bar.wait()
             ex.all_reduce_named("twice", x)
         ex.wait_named()
-        del oracle
+        assert torch.all(x == 2.0)
 
     _loop_ranks(world, body)
 

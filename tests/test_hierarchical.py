@@ -170,3 +170,84 @@ def test_two_hosts_two_gpus_each_device():
         pytest.skip("no GPU")
     _run([2, 2], use_gpu=True)
     _run([2, 1], use_gpu=True)
+
+
+@pytest.mark.gpu
+def test_native_hierarchical_threads_two_hosts_two_ranks():
+    """kungfu_amd.hierarchical.NativeHierarchicalExchange — kf_hier_all_reduce
+    behind the C ABI — with 2 emulated hosts x 2 ranks as threads of one
+    process on cuda:0: device-mode sessions across hosts (127.0.0.1 / .2),
+    the test library's loopback inside each host. S-SGD average (f32, both
+    algos, a ragged count), i32 MAX, and SMA through the exchange: bit-exact
+    against the per-host rank-order fold added across the two hosts."""
+    import socket
+    import tempfile
+    import threading
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    sys.path[:0] = [ROOT, HERE]
+    from loopback import LoopbackGroup
+    from kungfu_amd.hierarchical import NativeHierarchicalExchange
+    from kungfu_amd.session import Session
+    from oracle import oracle
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    base = 20000 + s.getsockname()[1] % 20000
+    s.close()
+    hosts = [[0, 1], [2, 3]]
+    peers = ["127.0.0.%d:%d" % (h + 1, base + g) for h, hs in enumerate(hosts) for g in hs]
+    groups = [LoopbackGroup(2), LoopbackGroup(2)]
+    d = tempfile.mkdtemp(prefix="kfnh")
+    dev = torch.device("cuda:0")
+    n = 100003
+    xs = [np.random.default_rng(500 + r).standard_normal(n).astype(np.float32) for r in range(4)]
+    ys = [np.random.default_rng(900 + r).integers(-2 ** 31, 2 ** 31 - 1, 4097).astype(np.int32)
+          for r in range(4)]
+
+    def combine(arrs, name, op):
+        per_host = [oracle.reduce_k([arrs[g] for g in h], name, op) for h in hosts]
+        return oracle.reduce_k(per_host, name, op)
+
+    errs = []
+
+    def run(g):
+        try:
+            torch.cuda.set_device(0)
+            h = 0 if g < 2 else 1
+            local = groups[h].exchange(g % 2)
+            sess = Session(peers=peers, self_spec=peers[g], sock_dir=d, mode="device")
+            ex = NativeHierarchicalExchange(sess, local=local)
+            assert (ex.rank, ex.np, ex.local_rank, ex.local_size, ex.host_count) == \
+                (g, 4, g % 2, 2, 2)
+            for algo in (1, 2):  # reduce-scatter, all-to-all
+                ex.algo = algo
+                b = torch.from_numpy(xs[g].copy()).to(dev)
+                ex.all_reduce_([b], average=True, name="w%d" % algo)
+                torch.cuda.synchronize()
+                want = oracle.reduce_avg([combine(xs, "f32", "sum")], "f32", 4)
+                assert np.array_equal(b.cpu().numpy(), want), algo
+            c = torch.from_numpy(ys[g].copy()).to(dev)
+            ex.all_reduce_([c], op="max", name="imax")
+            torch.cuda.synchronize()
+            assert np.array_equal(c.cpu().numpy(), np.max(np.array(ys), axis=0))
+            v = torch.from_numpy(xs[g].copy()).to(dev)
+            ex.sma_([v], 0.1)
+            torch.cuda.synchronize()
+            want = oracle.sma_blend(xs[g], combine(xs, "f32", "sum"), "f32", 4, 0.1)
+            assert np.array_equal(v.cpu().numpy(), want)
+            ex.close()
+            sess.close()
+        except Exception:
+            import traceback
+            errs.append("rank %d: %s" % (g, traceback.format_exc()))
+
+    ts = [threading.Thread(target=run, args=(g,)) for g in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=240)
+    assert not any(t.is_alive() for t in ts), "a rank did not finish"
+    for gr in groups:
+        gr.close()
+    assert not errs, "\n".join(errs)
