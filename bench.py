@@ -99,6 +99,10 @@ def parse():
                          "one 4 MiB fp32 bucket over the rchannel wire format")
     ap.add_argument("--c1-np", type=int, default=2,
                     help="peers for --config c1 (BASELINE configs[0] is np=2)")
+    ap.add_argument("--c1-modes", default="",
+                    help="--config c1: comma list of modes (default: all)")
+    ap.add_argument("--c1-repeats", type=int, default=1,
+                    help="--config c1: interleaved repeats of the mode list")
     ap.add_argument("--c1-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--c1-rank", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--c1-mode", default="device", help=argparse.SUPPRESS)
@@ -548,6 +552,8 @@ def c1_child(args):
     if args.c1_mode.startswith("device"):
         if args.c1_mode == "device_chain":  # the reference's 2-input recvOnto chain
             os.environ["KUNGFU_AMD_BATCH_FOLD"] = "0"
+        if args.c1_mode == "device_nomirror":  # A/B: the root's result via D2H again
+            os.environ["KUNGFU_AMD_ROOT_MIRROR"] = "0"
         dev = torch.device("cuda", 0)
         xs, ys = torch.from_numpy(x).to(dev), torch.zeros(C1_ELEMS, device=dev)
         sess = Session(r, npeers, args.c1_dir, mode="device")
@@ -677,8 +683,19 @@ def c1_summary(steps=100, warmup=10, repeats=3):
 
 def c1_parent(args):
     modes = ("device", "device_chain", "dropin", "cpu", "cpu_dev") if args.c1_np > 2 else \
-        ("device", "dropin", "cpu", "cpu_dev")
-    res = c1_run(args.c1_np, modes, args.steps, args.warmup)
+        ("device", "device_nomirror", "dropin", "cpu", "cpu_dev")
+    if args.c1_modes:
+        modes = tuple(args.c1_modes.split(","))
+    runs = [c1_run(args.c1_np, modes, args.steps, args.warmup) for _ in range(args.c1_repeats)]
+    res = runs[0]
+    if args.c1_repeats > 1:  # each mode: the median of its runs' medians, every run beside
+        for m in modes:
+            ok = [r[m] for r in runs if "error" not in r[m]]
+            if ok:
+                meds = sorted(x["latency_ms_median"] for x in ok)
+                res[m] = dict(ok[0], latency_ms_median=meds[len(meds) // 2],
+                              run_medians_ms=[x["latency_ms_median"] for x in ok],
+                              correct=all(x.get("correct") is True for x in ok))
     line = {
         "metric": "C1 all-reduce rate 4(np-1)*bytes/t (kungfu-bench-allreduce.go:73-80)",
         "unit": "GiB/s",

@@ -362,15 +362,17 @@ int launch_batch_kc(const void *const *in, int k, void *const *outs, const size_
     using S           = typename Elt<T>::S;
     constexpr int V   = Vec<S>::N;
     constexpr int U   = 4;
+    constexpr int NSEG = KC == 1 ? kBatchSeg1 : kBatchSeg;
+    constexpr int NPTR = KC == 1 ? 1 : kMaxInputs;
     const size_t tile = static_cast<size_t>(kBlock) * U;
-    BatchArgs a;
+    BatchArgsT<NSEG, NPTR> a;
     a.nseg          = 0;
     size_t blocks   = 0;
     auto flush      = [&]() -> int {
         if (a.nseg == 0) return KF_OK;
         a.blk0[a.nseg] = static_cast<unsigned>(blocks);
         a.serial       = KC == 0 && blocks >= kSerialMinBlocks ? 1 : 0;
-        reduce_batch_kernel<T, OP, EPI, KC, kBlock, U>
+        reduce_batch_kernel<T, OP, EPI, KC, kBlock, U, NSEG, NPTR>
             <<<static_cast<unsigned>(blocks), kBlock, 0, s>>>(a, k, np);
         a.nseg = 0;
         blocks = 0;
@@ -399,7 +401,7 @@ int launch_batch_kc(const void *const *in, int k, void *const *outs, const size_
             if (rc != KF_OK) return rc;
         }
         const int j = a.nseg;
-        for (int i = 0; i < kMaxInputs; ++i) a.in[j].p[i] = i < k ? ptrs[i] : nullptr;
+        for (int i = 0; i < NPTR; ++i) a.in[j][i] = i < k ? ptrs[i] : nullptr;
         a.out[j]  = outs[b];
         a.n[j]    = n;
         a.head[j] = p.head;
@@ -407,7 +409,7 @@ int launch_batch_kc(const void *const *in, int k, void *const *outs, const size_
         a.blk0[j] = static_cast<unsigned>(blocks);
         blocks += nblk;
         ++a.nseg;
-        if (a.nseg == kBatchSeg) {
+        if (a.nseg == NSEG) {
             int rc = flush();
             if (rc != KF_OK) return rc;
         }

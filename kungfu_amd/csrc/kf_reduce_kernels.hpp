@@ -555,32 +555,64 @@ __global__ void __launch_bounds__(BLOCK)
 // kernarg segment (scalar loads; the bucket index is wave-uniform).
 // ---------------------------------------------------------------------------
 constexpr int kBatchSeg = 16;
+// k = 1 (the shard /np after a reduce-scatter: one pointer per bucket) fits
+// four times as many buckets in the kernarg segment: C3's 64 shards at N = 8
+// go in ONE launch instead of four (30.0 us -> see DESIGN.md §3).
+constexpr int kBatchSeg1 = 64;
 
-struct BatchArgs {
-    InPtrs in[kBatchSeg];
-    void *out[kBatchSeg];
-    size_t n[kBatchSeg], head[kBatchSeg], nvec[kBatchSeg];
-    unsigned blk0[kBatchSeg + 1];
+template <int NSEG, int NPTR> struct BatchArgsT {
+    const void *in[NSEG][NPTR];
+    void *out[NSEG];
+    size_t n[NSEG], head[NSEG], nvec[NSEG];
+    unsigned blk0[NSEG + 1];
     int nseg;
     int serial;  // the runtime-k fold's one-in-flight schedule (reduce_body)
 };
+using BatchArgs  = BatchArgsT<kBatchSeg, kMaxInputs>;
+using BatchArgs1 = BatchArgsT<kBatchSeg1, 1>;
+static_assert(sizeof(BatchArgs1) <= 3072 && sizeof(BatchArgs) <= 3072, "kernarg budget");
 
-template <typename T, int OP, int EPI, int KC, int BLOCK, int UNROLL>
-__global__ void __launch_bounds__(BLOCK) reduce_batch_kernel(BatchArgs a, int k, Div np)
+// the bucket of block b: the last s with blk0[s] <= b (wave-uniform, scalar
+// loads from the kernarg segment; a binary search past 16 buckets)
+template <int NSEG, int NPTR>
+__device__ __forceinline__ int batch_segment(const BatchArgsT<NSEG, NPTR> &a, unsigned b)
 {
-    const unsigned b = blockIdx.x;
-    int s            = 0;
-    while (s + 1 < a.nseg && b >= a.blk0[s + 1]) ++s;
+    if constexpr (NSEG <= 16) {
+        int s = 0;
+        while (s + 1 < a.nseg && b >= a.blk0[s + 1]) ++s;
+        return s;
+    } else {
+        int lo = 0, hi = a.nseg - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (b >= a.blk0[mid]) lo = mid;
+            else hi = mid - 1;
+        }
+        return lo;
+    }
+}
+
+template <typename T, int OP, int EPI, int KC, int BLOCK, int UNROLL, int NSEG, int NPTR>
+__global__ void __launch_bounds__(BLOCK) reduce_batch_kernel(BatchArgsT<NSEG, NPTR> a, int k,
+                                                             Div np)
+{
+    const unsigned b  = blockIdx.x;
+    const int s       = batch_segment(a, b);
     const size_t nblk = a.blk0[s + 1] - a.blk0[s];
+    InPtrs one;  // NPTR == 1: the bucket's single input (only p[0] is read, KC == 1)
+    if constexpr (NPTR == 1) one.p[0] = a.in[s][0];
+    const InPtrs &in = [&]() -> const InPtrs & {
+        if constexpr (NPTR == 1) return one;
+        else return *reinterpret_cast<const InPtrs *>(a.in[s]);
+    }();
     if constexpr (EPI == EPI_DIV) {
         if (np.pow2) {
             reduce_body<T, OP, EPI_MUL, KC, BLOCK, UNROLL, 1, 0>(
-                a.in[s], k, a.out[s], a.n[s], a.head[s], a.nvec[s], np, b - a.blk0[s], nblk,
-                a.serial);
+                in, k, a.out[s], a.n[s], a.head[s], a.nvec[s], np, b - a.blk0[s], nblk, a.serial);
             return;
         }
     }
-    reduce_body<T, OP, EPI, KC, BLOCK, UNROLL, 1, 0>(a.in[s], k, a.out[s], a.n[s], a.head[s],
+    reduce_body<T, OP, EPI, KC, BLOCK, UNROLL, 1, 0>(in, k, a.out[s], a.n[s], a.head[s],
                                                     a.nvec[s], np, b - a.blk0[s], nblk, a.serial);
 }
 

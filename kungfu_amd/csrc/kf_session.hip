@@ -364,6 +364,9 @@ struct SendItem {  // one chunk to every fd in `fds` (the node's successors)
     void *stream;
     hipEvent_t ready;  // device mode: recorded on `stream` when the chunk is final
     bool slot_ok = false;  // device mode: its D2H into a tx slot was queued
+    bool host    = false;  // device mode: `ptr` is already page-locked host memory
+                           // (the root's fold wrote it there): no D2H, send once
+                           // `ready` has completed
 };
 
 }  // namespace
@@ -407,6 +410,16 @@ struct kf_session {
     int batch_fold = 1;         // device mode: k-input fold at multi-predecessor nodes
     char *stage       = nullptr;  // HBM staging: [predecessor arrival][bucket bytes]
     size_t stage_bytes = 0;
+    // device mode: a page-locked mirror of the bucket. A node that sends its
+    // finished fold onward (a star or tree root to its bcast successors, an
+    // inner tree node up) folds straight into it — the kernel writes the
+    // result over PCIe while it reads — so the sender has no D2H to wait for;
+    // the node's own HBM copy follows as an H2D off the critical path.
+    // KUNGFU_AMD_ROOT_MIRROR=0 turns it off (A/B).
+    char *txm          = nullptr;  // host address (the sockets)
+    char *txm_dev      = nullptr;  // the same pages as the GPU addresses them
+    size_t txm_bytes   = 0;
+    bool mirror        = true;
     char *barrier_dev  = nullptr;  // device mode: the barrier's zeroed u8 workspace
     std::deque<Stashed> stash;  // per-name mailbox for early messages
 
@@ -511,6 +524,7 @@ struct kf_session {
         for (auto e : ev_pool) (void)hipEventDestroy(e);
         if (tx_stream) (void)hipStreamDestroy(tx_stream);
         if (stage) (void)hipFree(stage);
+        if (txm) (void)hipHostFree(txm);
         if (barrier_dev) (void)hipFree(barrier_dev);
     }
 
@@ -568,6 +582,7 @@ struct kf_session {
     // marks the chunk final on the caller's stream; tx_done[slot] marks it landed.
     bool stage_d2h(SendItem &it, size_t slot)
     {
+        if (it.host) return it.ready != nullptr;  // synced at send time
         bool ok = it.ready && it.bytes <= kChunk + 4096 &&
                   hipStreamWaitEvent(tx_stream, it.ready, 0) == hipSuccess &&
                   hipMemcpyAsync(tx[slot], it.ptr, it.bytes, hipMemcpyDeviceToHost, tx_stream) ==
@@ -581,15 +596,26 @@ struct kf_session {
         return ok;
     }
 
-    int send_staged(const SendItem &it, size_t slot, std::string *err)
+    int send_staged(SendItem &it, size_t slot, std::string *err)
     {
-        if (!it.slot_ok || hipEventSynchronize(tx_done[slot]) != hipSuccess) {
+        if (it.host) {  // the fold wrote the chunk to host memory: wait for it
+            const bool ok = it.slot_ok && hipEventSynchronize(it.ready) == hipSuccess;
+            {
+                std::lock_guard<std::mutex> l(ev_mu);
+                ev_pool.push_back(it.ready);
+                it.ready = nullptr;
+            }
+            if (!ok) {
+                *err = "the fold of an outgoing chunk failed";
+                return KF_ERR_HIP;
+            }
+        } else if (!it.slot_ok || hipEventSynchronize(tx_done[slot]) != hipSuccess) {
             *err = "D2H of an outgoing chunk failed";
             return KF_ERR_HIP;
         }
+        const char *data = it.host ? it.ptr : static_cast<const char *>(tx[slot]);
         for (int fd : it.fds) {
-            const int rc = kf_rch_send(fd, it.name.c_str(), it.flags,
-                                       static_cast<const char *>(tx[slot]),
+            const int rc = kf_rch_send(fd, it.name.c_str(), it.flags, data,
                                        static_cast<uint32_t>(it.bytes));
             if (rc != KF_OK) {
                 *err = kf_ingest_last_error();
@@ -877,6 +903,7 @@ int kf_session::all_reduce(const char *send, char *recv, size_t count, KungFu_Da
         bool bcast_done;
         bool batched;  // stage the reduce arrivals, fold them in one launch
         std::vector<int> waiting;  // reduce predecessors not yet heard from
+        hipEvent_t mirror_ev;      // device mode: the last fold went to txm (its end)
     };
     std::vector<Chunk> chunks(parts.size());
     std::unordered_map<std::string, size_t> index;
@@ -893,6 +920,7 @@ int kf_session::all_reduce(const char *send, char *recv, size_t count, KungFu_Da
         c.bcast_done     = false;
         c.batched        = device_mode && batch_fold && dt != KungFu_BFLOAT16 &&
                     c.pending_reduce >= 2 && c.pending_reduce + 1 <= KF_MAX_INPUTS;
+        c.mirror_ev      = nullptr;
         if (c.batched && c.pending_reduce * bytes > need_stage) need_stage = c.pending_reduce * bytes;
         index[c.name]    = i;
     }
@@ -906,10 +934,60 @@ int kf_session::all_reduce(const char *send, char *recv, size_t count, KungFu_Da
         }
         stage_bytes = need_stage;
     }
+    // the fold that completes a chunk goes to the page-locked mirror when the
+    // chunk then leaves this node (reduce successors, or bcast successors of a
+    // node that receives no bcast itself)
+    bool use_mirror = device_mode && mirror && kind == kAllReduce;
+    if (use_mirror && txm_bytes < bytes) {  // the previous all-reduce ended synchronized
+        if (txm) (void)hipHostFree(txm);
+        txm       = nullptr;
+        txm_bytes = 0;
+        void *dv = nullptr;
+        if (hipHostMalloc(reinterpret_cast<void **>(&txm), bytes, hipHostMallocDefault) != hipSuccess ||
+            hipHostGetDevicePointer(&dv, txm, 0) != hipSuccess) {
+            if (txm) (void)hipHostFree(txm);
+            txm        = nullptr;
+            use_mirror = false;
+        } else {
+            txm_bytes = bytes;
+            txm_dev   = static_cast<char *>(dv);
+        }
+    }
     auto cptr = [&](const char *base, size_t i) { return base + parts[i].first * isz; };
     auto clen = [&](size_t i) { return (parts[i].second - parts[i].first) * isz; };
     auto effective = [&](size_t i) -> const char * {
         return (chunks[i].recv_count > 0 || inplace) ? cptr(recv, i) : cptr(send, i);
+    };
+    auto sends_onward = [&](size_t i) {
+        const auto &st = *chunks[i].st;
+        return !st.reduce.next[rank].empty() ||
+               (st.bcast.prev[rank].empty() && !st.bcast.next[rank].empty());
+    };
+    // an outgoing chunk: from the mirror if the fold wrote it there (first
+    // sender takes the fold's event), else from HBM (D2H by the sender)
+    auto send_item = [&](size_t i, std::vector<int> fds, uint32_t fl) {
+        auto &c = chunks[i];
+        if (c.mirror_ev) {
+            SendItem it{fds, c.name, fl, cptr(txm, i), clen(i), stream, c.mirror_ev};
+            it.host     = true;
+            c.mirror_ev = nullptr;
+            enqueue(std::move(it));
+            return;
+        }
+        enqueue({fds, c.name, fl, effective(i), clen(i), stream,
+                 device_mode ? chunk_ready(stream) : nullptr});
+    };
+    // after the completing fold into the mirror: its end marks the chunk
+    // final for the sender; then this node's own copy of it goes to HBM
+    auto mirror_done = [&](size_t i, char *dst) -> int {
+        auto &c     = chunks[i];
+        c.mirror_ev = chunk_ready(stream);
+        if (!c.mirror_ev ||
+            hipMemcpyAsync(dst, cptr(txm, i), clen(i), hipMemcpyHostToDevice,
+                           static_cast<hipStream_t>(stream)) != hipSuccess) {
+            return fail(KF_ERR_HIP, "mirror copy to HBM");
+        }
+        return KF_OK;
     };
     auto finish_bcast = [&](size_t i) {  // after recvInto or at the bcast root
         auto &c = chunks[i];
@@ -924,20 +1002,14 @@ int kf_session::all_reduce(const char *send, char *recv, size_t count, KungFu_Da
         }
         std::vector<int> fds;
         for (int p : c.st->bcast.next[rank]) fds.push_back(out_fd[p]);
-        if (!fds.empty()) {
-            enqueue({fds, c.name, KF_RCH_WAIT_RECV_BUF, effective(i), clen(i), stream,
-                     device_mode ? chunk_ready(stream) : nullptr});
-        }
+        if (!fds.empty()) send_item(i, fds, KF_RCH_WAIT_RECV_BUF);
         c.bcast_done = true;
     };
     auto finish_reduce = [&](size_t i) {  // all predecessors folded
         auto &c = chunks[i];
         std::vector<int> fds;
         for (int p : c.st->reduce.next[rank]) fds.push_back(out_fd[p]);
-        if (!fds.empty()) {
-            enqueue({fds, c.name, KF_RCH_NO_FLAG, effective(i), clen(i), stream,
-                     device_mode ? chunk_ready(stream) : nullptr});
-        }
+        if (!fds.empty()) send_item(i, fds, KF_RCH_NO_FLAG);
         if (c.st->bcast.prev[rank].empty()) finish_bcast(i);
     };
 
@@ -1000,8 +1072,16 @@ int kf_session::all_reduce(const char *send, char *recv, size_t count, KungFu_Da
             for (int a = 0; a < c.recv_count; ++a) {
                 ins[a + 1] = stage + static_cast<size_t>(a) * bytes + parts[i].first * isz;
             }
-            r = kf_bucket_reduce(ins, c.recv_count + 1, dst, n, dt, op, stream);
-            if (r != KF_OK) return fail(r, kf_last_error());
+            if (use_mirror && sends_onward(i)) {
+                r = kf_bucket_reduce(ins, c.recv_count + 1, const_cast<char *>(cptr(txm_dev, i)),
+                                     n, dt, op, stream);
+                if (r != KF_OK) return fail(r, kf_last_error());
+                r = mirror_done(i, dst);
+                if (r != KF_OK) return r;
+            } else {
+                r = kf_bucket_reduce(ins, c.recv_count + 1, dst, n, dt, op, stream);
+                if (r != KF_OK) return fail(r, kf_last_error());
+            }
             finish_reduce(i);
             if (c.bcast_done) --remaining;
             return KF_OK;
@@ -1009,9 +1089,16 @@ int kf_session::all_reduce(const char *send, char *recv, size_t count, KungFu_Da
         // reduce: recvOnto, RecvBuf = effective o peer
         const char *own = effective(i);
         if (device_mode) {
-            r = mem ? kf_ingest_fold_host(ingest, mem, len, dst, own, n, dt, op, stream)
-                    : kf_ingest_recv_onto(ingest, fd, len, dst, own, n, dt, op, stream);
+            // the completing fold of a chunk that leaves this node goes to the mirror
+            const bool to_mirror = use_mirror && c.pending_reduce == 1 && sends_onward(i);
+            char *out            = to_mirror ? const_cast<char *>(cptr(txm_dev, i)) : dst;
+            r = mem ? kf_ingest_fold_host(ingest, mem, len, out, own, n, dt, op, stream)
+                    : kf_ingest_recv_onto(ingest, fd, len, out, own, n, dt, op, stream);
             if (r != KF_OK) return fail(r, kf_ingest_last_error());
+            if (to_mirror) {
+                r = mirror_done(i, dst);
+                if (r != KF_OK) return r;
+            }
         } else {
             const char *peer = mem;
             if (!mem) {
@@ -1146,6 +1233,7 @@ kf_session_t *create_session(int rank, std::vector<PeerAddr> peers, const char *
         s->ingest = kf_ingest_create(kChunk + 4096, 8);
         int nslot = 4;
         if (const char *e = std::getenv("KUNGFU_AMD_TX_SLOTS")) nslot = std::max(1, std::atoi(e));
+        if (const char *e = std::getenv("KUNGFU_AMD_ROOT_MIRROR")) s->mirror = std::atoi(e) != 0;
         bool tx_ok = true;
         for (int i = 0; i < nslot && tx_ok; ++i) {
             void *p      = nullptr;

@@ -156,6 +156,35 @@ def test_batch_kernel_matches_oracle(name, k, avg):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("name", ["f32", "bf16"])
+def test_batch_kernel_k1_past_64_buckets(name):
+    """k = 1 (the shard /np) packs up to 64 buckets per launch (kBatchSeg1):
+    150 ragged buckets — three launches, the last partial — with one
+    misaligned bucket in the middle (a launch of its own), /np and plain."""
+    import torch
+    from kungfu_amd import _lib
+    from oracle import oracle
+    dev = _gpu()
+    lib = _lib.load()
+    sizes = [(4099 * (i % 7) + 13 * i) % 70000 for i in range(150)]
+    hs = [_rand(name, n, 7000 + b) for b, n in enumerate(sizes)]
+    for np_ in (8, 3, 0):
+        ins = [_to_dev(h, name, dev) for h in hs]
+        ins[77] = torch.cat([ins[77][:1], ins[77]])[1:]
+        outs = [torch.empty_like(t) for t in ins]
+        rc = lib.kf_bucket_reduce_batch(
+            _lib.ptr_array([t.data_ptr() for t in ins]), 1,
+            _lib.ptr_array([o.data_ptr() for o in outs]),
+            (ctypes.c_size_t * len(sizes))(*sizes), len(sizes), oracle.DT[name], 0, np_,
+            torch.cuda.current_stream().cuda_stream)
+        _lib.check(rc, "kf_bucket_reduce_batch")
+        torch.cuda.synchronize()
+        for b, h in enumerate(hs):
+            want = oracle.reduce_avg([h], name, np_) if np_ else h
+            assert np.array_equal(_to_np(outs[b], name), want), (np_, b)
+
+
+@pytest.mark.gpu
 def test_world1_native_exchange():
     """A one-rank communicator through the C ABI: every call is the identity
     (a sum of one, / 1), for both algorithms, batch and SMA, out of place too;
