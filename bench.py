@@ -355,8 +355,8 @@ def exchange_phase2(lib, dev, g, world=8):
         ok = ok and torch.equal(o, (acc / world).bfloat16())
     report("c5_a2a_fold_n8_bf16", per_set, us, ok,
            "C5 at N=8: kf_bucket_reduce_batch, k=8 received bf16 shards per bucket "
-           "(%d buckets, shards of %.2f MiB), rank-order fold, /8 fused" %
-           (len(qs), qs[0] * 2 / 2**20), len(qs))
+           "(%d buckets, shards of %.2f-%.2f MiB), rank-order fold, /8 fused" %
+           (len(qs), min(qs) * 2 / 2**20, max(qs) * 2 / 2**20), len(qs))
     del sets
     torch.cuda.empty_cache()
 
