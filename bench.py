@@ -82,7 +82,7 @@ def parse():
                     help="rehearsal only: put every rank on this GPU")
     ap.add_argument("--no-extra", action="store_true",
                     help="N>1: skip the C4/C5/P2P sub-benchmarks")
-    ap.add_argument("--extras", default="c4,c5,c5_pipe,c4_pipe,c3_pipe,c3_a2a,c3_fused,c3_torch_fused,c3_per_bucket,c4_torch,"
+    ap.add_argument("--extras", default="c4,c5,c5_pipe,c4_pipe,c4_named,c3_pipe,c3_a2a,c3_fused,c3_torch_fused,c3_per_bucket,c4_torch,"
                                         "c5_torch,c3_ar,c3_p2p,c3_p2p_push,c3_p2p_hostbar,"
                                         "c4_p2p,c5_p2p",
                     help="N>1: which sub-benchmarks to run (comma list)")
@@ -848,6 +848,7 @@ def main():
                                               exchange="native_pipe")),
                  ("c4_pipe", lambda: bench_c4(world, rank, dev, steps_x, 5,
                                               exchange="native_pipe")),
+                 ("c4_named", lambda: bench_c4_named(world, rank, dev, steps_x, 5)),
                  ("c3_pipe", lambda: bench_c3_native(world, rank, dev, steps_x, 5, n, x, "rs",
                                                      args.buckets, pipe=True)),
                  ("c3_a2a", lambda: bench_c3_native(world, rank, dev, steps_x, 5, n, x,
@@ -1403,6 +1404,57 @@ def bench_c4(world, rank, dev, steps, warmup, exchange="native"):
     return {"workload": "C4: ResNet-50 grads, 25,583,592 fp32 in %d buckets, S-SGD "
                         "(%s)" % (len(mine.buckets), how),
             "bytes": s_bytes, "ms_per_step": round(step_s * 1e3, 4),
+            "GiBps_per_gpu": round(s_bytes / step_s / 2**30, 3),
+            "busbw_GBps": round(busbw, 2),
+            "frac_of_xgmi": _xgmi_frac(busbw, world)}
+
+
+def bench_c4_named(world, rank, dev, steps, warmup):
+    """C4's 214 ResNet-50 gradient tensors one by one through the name-keyed
+    all-reduce (kf_exchange_all_reduce_named, the torch op's path:
+    all_reduce_cuda_async keyed by tensor name), every rank starting them in
+    its OWN random order each step; the exchange negotiates the issue order
+    and sends the names that become ready together as batched calls. S-SGD
+    average, in place."""
+    from kungfu_amd import ops
+    from kungfu_amd.collective import GradBuckets
+    sizes = _models()["resnet50-imagenet"]
+    ex = _NATIVE.get("ex")
+    if ex is None:
+        raise RuntimeError("native exchange unavailable (see collective.native_exchange_error)")
+    gbs = [GradBuckets(sizes, torch.float32, dev, world, n_buckets=16) for _ in range(world)]
+    for r, gb in enumerate(gbs):
+        _fill(gb, 600 + r, dev, torch.float32)
+    mine = gbs[rank]
+    views = mine.views
+    want = [ops.bucket_reduce_avg([gb.views[i].reshape(-1) for gb in gbs], world)
+            for i in range(len(views))]
+    absums = [sum(gb.views[i].reshape(-1).abs() for gb in gbs) for i in range(len(views))]
+    names = ["resnet50/grad/%d" % i for i in range(len(views))]
+    flat = [v.reshape(-1) for v in views]
+    rng = np.random.default_rng(1000 + rank)
+
+    def step():
+        for i in rng.permutation(len(flat)):
+            ex.all_reduce_named(names[i], flat[i], average=True)
+        ex.wait_named()
+
+    step()
+    ok = True
+    for v, w, ab in zip(flat, want, absums):
+        ok &= bool(torch.equal(v, w)) if world <= 2 else _within(v, w, ab, world)
+    del want, absums
+    gbs.clear()
+    if not _agree(ok, dev):
+        return {"error": "C4 named parity check failed (N<=2 bit-exact / N>2 bound)"}
+    s_bytes = sum(sizes) * 4
+    step_s = _timed(step, steps, warmup, dev, world)
+    busbw = 2 * (world - 1) / world * s_bytes / step_s / 1e9
+    return {"workload": "C4: ResNet-50 grads, 214 fp32 tensors, each its own name-keyed "
+                        "all-reduce started in a per-rank random order "
+                        "(kf_exchange_all_reduce_named: negotiated order, batched issue, "
+                        "RCCL RS -> HIP /np -> RCCL AG), S-SGD",
+            "bytes": s_bytes, "tensors": len(flat), "ms_per_step": round(step_s * 1e3, 4),
             "GiBps_per_gpu": round(s_bytes / step_s / 2**30, 3),
             "busbw_GBps": round(busbw, 2),
             "frac_of_xgmi": _xgmi_frac(busbw, world)}

@@ -194,14 +194,15 @@ class NativeExchange:
         on the exchange's completion thread; wait_named() blocks for all."""
         red = OP_NAMES[op] if isinstance(op, str) else OP(op)
         s = stream if stream is not None else torch.cuda.current_stream(buf.device)
-
-        def done(status, _arg):
-            if callback is not None:
-                callback(name, status)
-
-        cfn = _lib.DONE_FN(done)
         self._named_keep = getattr(self, "_named_keep", [])
-        self._named_keep.append((cfn, buf))
+        if callback is not None:
+            def done(status, _arg):
+                callback(name, status)
+            cfn = _lib.DONE_FN(done)
+            self._named_keep.append((cfn, buf))
+        else:  # no callback: a NULL done (no Python call per completion)
+            cfn = None
+            self._named_keep.append(buf)
         rc = self.lib.kf_exchange_all_reduce_named(
             self._h, name.encode(), buf.data_ptr(), buf.data_ptr(), buf.numel(),
             int(kungfu_dtype(buf)), int(red), 1 if average else 0, ALGOS[self.algo],

@@ -115,7 +115,7 @@ def test_bench_exchange_branch_single_rank_rccl():
         pytest.skip("no GPU")
     env = dict(os.environ, MASTER_ADDR="127.0.0.1",
                MASTER_PORT=str(_port()), RANK="0", LOCAL_RANK="0", WORLD_SIZE="1")
-    extras = "c4,c5,c5_pipe,c4_pipe,c3_pipe,c3_a2a,c3_fused,c4_torch,c5_torch"
+    extras = "c4,c5,c5_pipe,c4_pipe,c4_named,c3_pipe,c3_a2a,c3_fused,c4_torch,c5_torch"
     argv = ["--rehearse-exchange", "--steps", "3", "--warmup", "1", "--elems", str(4 << 20),
             "--extras", extras, "--extras-timeout", "200"]
     code = _BRANCH_CHILD % (ROOT, os.path.join(ROOT, "tests"), argv)
