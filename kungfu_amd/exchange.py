@@ -29,6 +29,7 @@ from .base import OP, OP_NAMES
 from .ops import kungfu_dtype
 
 ALGOS = {"auto": 0, "rs": 1, "a2a": 2}
+_NO_DONE = _lib.DONE_FN()  # a NULL kf_done_fn
 
 
 def _arr(t, vals):
@@ -201,7 +202,7 @@ class NativeExchange:
             cfn = _lib.DONE_FN(done)
             self._named_keep.append((cfn, buf))
         else:  # no callback: a NULL done (no Python call per completion)
-            cfn = None
+            cfn = _NO_DONE
             self._named_keep.append(buf)
         rc = self.lib.kf_exchange_all_reduce_named(
             self._h, name.encode(), buf.data_ptr(), buf.data_ptr(), buf.numel(),
