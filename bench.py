@@ -848,7 +848,6 @@ def main():
                                               exchange="native_pipe")),
                  ("c4_pipe", lambda: bench_c4(world, rank, dev, steps_x, 5,
                                               exchange="native_pipe")),
-                 ("c4_named", lambda: bench_c4_named(world, rank, dev, steps_x, 5)),
                  ("c3_pipe", lambda: bench_c3_native(world, rank, dev, steps_x, 5, n, x, "rs",
                                                      args.buckets, pipe=True)),
                  ("c3_a2a", lambda: bench_c3_native(world, rank, dev, steps_x, 5, n, x,
@@ -1071,7 +1070,10 @@ _NATIVE = {}  # the primary's NativeExchange, reused by the sub-benchmarks
 # that has never run across devices before the driver's multi-GPU node. They
 # run in one child process per rank (own process group on its own port), so a
 # fault or an abort there ends the child, not the ranks holding the line.
-P2P_KEYS = ("c3_p2p", "c3_p2p_push", "c3_p2p_hostbar", "c4_p2p", "c5_p2p")
+# run in child processes (their own process group and bounded waits): the
+# xGMI peer mappings and the name negotiation, which run across devices for
+# the first time on the driver's node
+P2P_KEYS = ("c3_p2p", "c3_p2p_push", "c3_p2p_hostbar", "c4_p2p", "c5_p2p", "c4_named")
 
 
 def _p2p_runs(world, rank, dev, steps, n, x):
@@ -1081,7 +1083,21 @@ def _p2p_runs(world, rank, dev, steps, n, x):
         "c3_p2p_hostbar": lambda: bench_c3_p2p(world, rank, dev, steps, 5, n, x, barrier="host"),
         "c4_p2p": lambda: bench_c4(world, rank, dev, steps, 5, exchange="p2p"),
         "c5_p2p": lambda: bench_c5(world, rank, dev, steps, 5, exchange="p2p"),
+        "c4_named": lambda: _named_in_child(world, rank, dev, steps),
     }
+
+
+def _named_in_child(world, rank, dev, steps):
+    """c4_named in a child process: its first run across devices is the
+    name negotiation's first over RCCL (a split-off control communicator and
+    a negotiation thread), so it is isolated like the P2P paths — a hang or
+    fault there ends the child, not the line."""
+    if "ex" not in _NATIVE:
+        if dist.get_backend() != "nccl":
+            raise RuntimeError("the name-keyed path needs the native exchange (nccl backend)")
+        from kungfu_amd.exchange import NativeExchange
+        _NATIVE["ex"] = NativeExchange(algo="auto", device=dev)
+    return bench_c4_named(world, rank, dev, steps, 5)
 
 
 def p2p_extras(args, rank, world, local_rank, dev, keys, seconds):
@@ -1200,6 +1216,8 @@ def p2p_child(args):
             with open(args.p2p_out, "w") as f:
                 json.dump(out, f)
     dog.cancel()
+    if "ex" in _NATIVE:
+        _NATIVE.pop("ex").close()
     dist.barrier()
     dist.destroy_process_group()
     return 0
