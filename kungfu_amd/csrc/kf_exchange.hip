@@ -939,7 +939,10 @@ void kf_exchange::complete_loop()
 int kf_exchange::start_named()
 {
     if (nready) return KF_OK;
-    if (world > 1) {
+    // the built-in transport's single rank has nothing to agree; any other
+    // transport negotiates even alone, so a one-GPU box runs the control
+    // communicator through it (tests/c/kf_testing.cpp's one-rank librccl)
+    if (world > 1 || !builtin) {
         int st = KF_OK;
         ctrl   = split(0, rank, &st);
         if (!ctrl) return st != KF_OK ? st : fail(KF_ERR_RCCL, "control communicator");
@@ -973,7 +976,8 @@ void kf_exchange::fail_outstanding(int rc, const std::string &why)
 void kf_exchange::negotiate_loop()
 {
     (void)hipSetDevice(device);
-    const int W = world;
+    const int W         = world;
+    const bool negotiate = ctrl != nullptr;
     struct Seen {
         int n        = 0;
         uint32_t sig = 0;
@@ -997,7 +1001,7 @@ void kf_exchange::negotiate_loop()
                 ncv.wait_for(lk, us, [&] { return nstop || !nfresh.empty(); });
                 if (nstop) return;
             }
-            if (W == 1) {  // nothing to agree: issue in start order
+            if (!negotiate) {  // one rank, built-in transport: issue in start order
                 for (; !nfresh.empty(); nfresh.pop_front()) {
                     const NamedTask &t = nwait.at(nfresh.front());
                     complete.emplace_back(t.h1, t.h2);
@@ -1013,7 +1017,7 @@ void kf_exchange::negotiate_loop()
             }
         }
         bool news = !complete.empty();
-        if (W > 1) {
+        if (negotiate) {
             int rc        = KF_OK;
             char *d       = static_cast<char *>(cdev);
             hipError_t e  = hipMemcpyAsync(d, row, kCtrlRow, hipMemcpyHostToDevice, cstream);

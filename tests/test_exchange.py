@@ -673,6 +673,24 @@ for algo in ("rs", "a2a", "auto"):
         sch.wait_all()
     torch.cuda.synchronize()
     assert torch.equal(b, w) and all(torch.equal(a, c) for a, c in zip(bufs, keep))
+    # name-keyed through librccl: the control communicator split off by
+    # ncclCommSplit and the negotiation's all-gathers run with one rank
+    nb = [rnd(1000 + 7 * i, torch.float32) for i in range(5)]
+    nk = [t.clone() for t in nb]
+    for i in (3, 1, 4, 0, 2):
+        ex.all_reduce_named("w%%d" %% i, nb[i], average=True)
+    ex.wait_named()
+    torch.cuda.synchronize()
+    assert all(torch.equal(a, c) for a, c in zip(nb, nk)), (algo, "named")
+    # gpu_collective::new_group through ncclCommSplit
+    sub = ex.split(0)
+    assert sub is not None and sub.world == 1
+    t = rnd(4097, torch.float32)
+    t0 = t.clone()
+    sub.all_reduce_([t], average=True)
+    torch.cuda.synchronize()
+    assert torch.equal(t, t0), (algo, "split")
+    sub.close()
     ex.check()
     ex.close()
 print("W1_RCCL_OK")
