@@ -104,6 +104,7 @@ def parse():
     ap.add_argument("--c1-repeats", type=int, default=1,
                     help="--config c1: interleaved repeats of the mode list")
     ap.add_argument("--c1-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--c1-cpus", default="", help=argparse.SUPPRESS)
     ap.add_argument("--c1-rank", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--c1-mode", default="device", help=argparse.SUPPRESS)
     ap.add_argument("--c1-dir", default="", help=argparse.SUPPRESS)
@@ -546,6 +547,8 @@ def c1_child(args):
                timed step."""
     from kungfu_amd.session import Session
     r, npeers = args.c1_rank, args.c1_np
+    if args.c1_cpus:  # the GPU's NUMA node (gpu_local_cpus), every mode alike
+        os.sched_setaffinity(0, [int(c) for c in args.c1_cpus.split(",")])
     x = ((r + 1) * (np.arange(C1_ELEMS) % 1024) / 1024).astype(np.float32)
     # sum_r (r+1) * (i mod 1024) / 1024: every partial sum is exact in fp32
     want = (npeers * (npeers + 1) // 2 * (np.arange(C1_ELEMS) % 1024) / 1024).astype(np.float32)
@@ -615,7 +618,31 @@ def c1_child(args):
         print(json.dumps(rec), flush=True)
 
 
-def c1_run(npeers, modes, steps, warmup, timeout=600):
+def gpu_local_cpus(index=0):
+    """The CPUs this process may use that sit on the GPU's own NUMA node
+    (sysfs local_cpulist of its PCI function), or None: the C1 peers of every
+    mode run there, so no mode's run lands on a far socket by chance (a
+    device-mode chunk crosses PCIe up to three times; the CPU fold's buffers
+    live in host memory)."""
+    try:
+        pr = torch.cuda.get_device_properties(index)
+        bdf = "%04x:%02x:%02x.0" % (pr.pci_domain_id, pr.pci_bus_id, pr.pci_device_id)
+        with open("/sys/bus/pci/devices/%s/local_cpulist" % bdf) as f:
+            spec = f.read().strip()
+    except Exception:
+        return None
+    cpus = set()
+    for part in spec.split(","):
+        if "-" in part:
+            a, b = part.split("-")
+            cpus.update(range(int(a), int(b) + 1))
+        elif part:
+            cpus.add(int(part))
+    cpus &= os.sched_getaffinity(0)
+    return sorted(cpus) or None
+
+
+def c1_run(npeers, modes, steps, warmup, timeout=600, cpus=None):
     """Launch the np peers per mode (subprocesses, one unix socket each);
     {mode: rank 0's record}."""
     import subprocess
@@ -626,6 +653,8 @@ def c1_run(npeers, modes, steps, warmup, timeout=600):
             cmd = [sys.executable, os.path.abspath(__file__), "--c1-child",
                    "--c1-mode", mode, "--c1-dir", d, "--steps", str(steps),
                    "--warmup", str(warmup), "--c1-np", str(npeers)]
+            if cpus:
+                cmd += ["--c1-cpus", ",".join(map(str, cpus))]
             procs = [subprocess.Popen(cmd + ["--c1-rank", str(r)], stdout=subprocess.PIPE,
                                       text=True, cwd=ROOT) for r in range(npeers)]
             try:
@@ -642,7 +671,7 @@ def c1_run(npeers, modes, steps, warmup, timeout=600):
     return res
 
 
-def c1_summary(steps=100, warmup=10, repeats=3):
+def c1_summary(steps=100, warmup=10, repeats=5):
     """BASELINE configs[0] beside the N = 1 line: np = 2 peers on this host,
     one 4 MiB fp32 bucket, median latency and 4(np-1)*bytes/t
     (kungfu-bench-allreduce.go:73-80); the device session against the
@@ -651,7 +680,8 @@ def c1_summary(steps=100, warmup=10, repeats=3):
     between back-to-back runs of the same command on one box
     (profiles/r02/c1_variants.jsonl), so each mode reports the median of its
     runs' medians and every run's median beside it."""
-    runs = [c1_run(2, ("device", "cpu", "cpu_dev"), steps, warmup, timeout=180)
+    cpus = gpu_local_cpus()
+    runs = [c1_run(2, ("device", "cpu", "cpu_dev"), steps, warmup, timeout=180, cpus=cpus)
             for _ in range(repeats)]
     res = {}
     for mode in ("device", "cpu", "cpu_dev"):
@@ -675,7 +705,8 @@ def c1_summary(steps=100, warmup=10, repeats=3):
            "unit": "GiB/s (4(np-1)*bytes/t, median of the runs' medians)",
            "modes": "device: bucket in HBM, HIP fold; cpu: bucket in host memory, the "
                     "reference's CPU fold; cpu_dev: bucket in HBM reduced the reference's "
-                    "way for GPU tensors (D2H, the cpu all-reduce, H2D)"}
+                    "way for GPU tensors (D2H, the cpu all-reduce, H2D)",
+           "cpus": ("the GPU's NUMA node: %d CPUs" % len(cpus)) if cpus else "not pinned"}
     out.update(res)
     out["correct"] = all(r.get("correct") is True for r in res.values())
     return out
@@ -686,7 +717,9 @@ def c1_parent(args):
         ("device", "device_nomirror", "dropin", "cpu", "cpu_dev")
     if args.c1_modes:
         modes = tuple(args.c1_modes.split(","))
-    runs = [c1_run(args.c1_np, modes, args.steps, args.warmup) for _ in range(args.c1_repeats)]
+    cpus = gpu_local_cpus()
+    runs = [c1_run(args.c1_np, modes, args.steps, args.warmup, cpus=cpus)
+            for _ in range(args.c1_repeats)]
     res = runs[0]
     if args.c1_repeats > 1:  # each mode: the median of its runs' medians, every run beside
         for m in modes:
