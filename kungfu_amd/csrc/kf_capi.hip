@@ -355,16 +355,24 @@ int check_args(const void *const *inputs, int k, const void *out, size_t n)
 // ---------------------------------------------------------------------------
 // batch: nb buckets, one launch per kBatchSeg of them (kf_bucket_reduce_batch)
 // ---------------------------------------------------------------------------
+// tile shape of the batched launch (tools/ab_batch_shape.py builds variants)
+#ifndef KF_BATCH_UNROLL
+#define KF_BATCH_UNROLL 4
+#endif
+#ifndef KF_BATCH_BLOCK
+#define KF_BATCH_BLOCK 256
+#endif
 template <typename T, int OP, int EPI, int KC>
 int launch_batch_kc(const void *const *in, int k, void *const *outs, const size_t *counts,
                     int nb, const Div &np, int npi, hipStream_t s)
 {
     using S           = typename Elt<T>::S;
     constexpr int V   = Vec<S>::N;
-    constexpr int U   = 4;
+    constexpr int U   = KF_BATCH_UNROLL;
+    constexpr int B   = KF_BATCH_BLOCK;
     constexpr int NSEG = KC == 1 ? kBatchSeg1 : kBatchSeg;
     constexpr int NPTR = KC == 1 ? 1 : kMaxInputs;
-    const size_t tile = static_cast<size_t>(kBlock) * U;
+    const size_t tile = static_cast<size_t>(B) * U;
     BatchArgsT<NSEG, NPTR> a;
     a.nseg          = 0;
     size_t blocks   = 0;
@@ -372,8 +380,8 @@ int launch_batch_kc(const void *const *in, int k, void *const *outs, const size_
         if (a.nseg == 0) return KF_OK;
         a.blk0[a.nseg] = static_cast<unsigned>(blocks);
         a.serial       = KC == 0 && blocks >= kSerialMinBlocks ? 1 : 0;
-        reduce_batch_kernel<T, OP, EPI, KC, kBlock, U, NSEG, NPTR>
-            <<<static_cast<unsigned>(blocks), kBlock, 0, s>>>(a, k, np);
+        reduce_batch_kernel<T, OP, EPI, KC, B, U, NSEG, NPTR>
+            <<<static_cast<unsigned>(blocks), B, 0, s>>>(a, k, np);
         a.nseg = 0;
         blocks = 0;
         hipError_t e = hipGetLastError();
@@ -392,7 +400,7 @@ int launch_batch_kc(const void *const *in, int k, void *const *outs, const size_
         }
         const size_t nedge = p.head + (n - p.head - p.nvec * V);
         size_t nblk        = (p.nvec + tile - 1) / tile;
-        const size_t eblk  = (nedge + kBlock - 1) / kBlock;
+        const size_t eblk  = (nedge + B - 1) / B;
         if (nblk > static_cast<size_t>(geometry().grid_cap)) nblk = geometry().grid_cap;
         if (nblk < eblk) nblk = eblk;
         if (nblk < 1) nblk = 1;
