@@ -355,9 +355,18 @@ int check_args(const void *const *inputs, int k, const void *out, size_t n)
 // ---------------------------------------------------------------------------
 // batch: nb buckets, one launch per kBatchSeg of them (kf_bucket_reduce_batch)
 // ---------------------------------------------------------------------------
-// tile shape of the batched launch (tools/ab_batch_shape.py builds variants)
+// tile shape of the batched launch (tools/ab_batch_shape.py builds variants;
+// profiles/r03/ab_batch_shape.jsonl). k = 1 (the shard /np after a
+// reduce-scatter) takes two vectors per lane: its launches are small and
+// latency-bound, and twice the blocks for the same bytes finish sooner (C4's
+// 16 shards at N = 8: 8.4 -> 7.0 us; C3's 64: 16.2 -> 15.8 us); k >= 2 keeps
+// four (k = 2 16 x 4 MiB, the k = 8 fold of C5: equal within 1 %, one lane
+// per vector up to 6 % slower).
 #ifndef KF_BATCH_UNROLL
 #define KF_BATCH_UNROLL 4
+#endif
+#ifndef KF_BATCH_UNROLL_K1
+#define KF_BATCH_UNROLL_K1 2
 #endif
 #ifndef KF_BATCH_BLOCK
 #define KF_BATCH_BLOCK 256
@@ -368,7 +377,7 @@ int launch_batch_kc(const void *const *in, int k, void *const *outs, const size_
 {
     using S           = typename Elt<T>::S;
     constexpr int V   = Vec<S>::N;
-    constexpr int U   = KF_BATCH_UNROLL;
+    constexpr int U   = KC == 1 ? KF_BATCH_UNROLL_K1 : KF_BATCH_UNROLL;
     constexpr int B   = KF_BATCH_BLOCK;
     constexpr int NSEG = KC == 1 ? kBatchSeg1 : kBatchSeg;
     constexpr int NPTR = KC == 1 ? 1 : kMaxInputs;

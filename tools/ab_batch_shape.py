@@ -3,7 +3,7 @@
 exchange's phase-2 shapes (bench.py exchange_phase2: C5's k = 8 all-to-all
 fold, C4's and C3's k = 1 shard /np at N = 8) and at C3's 16 x 4 MiB k = 2.
 
-The shape is compile-time (KF_BATCH_UNROLL x KF_BATCH_BLOCK in kf_capi.hip),
+The shape is compile-time (KF_BATCH_UNROLL[_K1] x KF_BATCH_BLOCK in kf_capi.hip),
 so `build` compiles kf_capi.hip once per shape into tools/ab_lib/ (on the
 CPU, before the GPU call); `run` loads every variant into one process
 (RTLD_LOCAL) and times them interleaved on the same buffers, cycling over
@@ -38,6 +38,7 @@ def build():
         cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
                "-shared", "-ffp-contract=off", "-fvisibility=hidden",
                "-I" + os.path.join(ROOT, "include"), "-DKF_BATCH_UNROLL=%d" % u,
+               "-DKF_BATCH_UNROLL_K1=%d" % u,
                "-DKF_BATCH_BLOCK=%d" % b, "-o", lib_path(u, b), src]
         subprocess.run(cmd, check=True)
         print("built", lib_path(u, b), flush=True)
