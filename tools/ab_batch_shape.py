@@ -59,6 +59,7 @@ def run():
         lib.kf_bucket_reduce_batch.argtypes = argt
         lib.kf_bucket_reduce_batch.restype = ctypes.c_int
         libs["u%d_b%d" % (u, b)] = lib
+    libs["shipped"] = ship
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(5)
     sp = torch.cuda.current_stream().cuda_stream
