@@ -334,13 +334,16 @@ int kf_session_reduce(kf_session_t *s, const void *send, void *recv, size_t coun
 int kf_session_broadcast(kf_session_t *s, const void *send, void *recv, size_t count,
                          KungFu_Datatype dt, const char *name, void *stream);
 /* GoKungfuAllReduce with done != nil (srcs/go/libkungfu-comm/collective.go:
- * 34-45, main.go:184-191): queue the all-reduce on the session's worker
+ * 34-45, main.go:184-191): start the all-reduce on the session's worker
  * thread and return KF_OK at once; done(status, arg) runs on that thread when
  * it has finished (the reference drops the error, main.go:188; here it is
- * passed on). Queued all-reduces run one after another in submission order,
- * so every peer submits the same names in the same order (the rule RCCL has
- * too; the reference's goroutine per call does not need it). Buffers stay
- * valid and untouched until done; the name is copied. A synchronous
+ * passed on). Every started all-reduce is in flight at once in the worker's
+ * poll loop and peers' chunks pair by name, as with the reference's goroutine
+ * per call (rchannel/handler/collective.go:48-64), so peers may start their
+ * names in different orders; done callbacks come in completion order. A name
+ * started while its previous call is in flight waits for it (the next step's
+ * call of the same name). Buffers stay valid and untouched until done; the
+ * name is copied. A synchronous
  * kf_session_all_reduce first waits for everything queued before it; from
  * inside a done callback it (and kf_session_wait_all) returns KF_ERR_ARG
  * instead of waiting for itself. */

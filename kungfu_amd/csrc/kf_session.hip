@@ -43,6 +43,7 @@
 #include <netinet/in.h>
 #include <netinet/tcp.h>
 #include <poll.h>
+#include <sys/eventfd.h>
 #include <sys/socket.h>
 #include <sys/un.h>
 #include <unistd.h>
@@ -355,6 +356,8 @@ int read_exact(int fd, void *buf, size_t n)
     return KF_OK;
 }
 
+struct SessOp;
+
 struct SendItem {  // one chunk to every fd in `fds` (the node's successors)
     std::vector<int> fds;
     std::string name;
@@ -367,22 +370,60 @@ struct SendItem {  // one chunk to every fd in `fds` (the node's successors)
     bool host    = false;  // device mode: `ptr` is already page-locked host memory
                            // (the root's fold wrote it there): no D2H, send once
                            // `ready` has completed
+    SessOp *owner = nullptr;  // the collective whose chunk this is
+};
+
+// A buffer lent to one collective in flight: HBM staging for the k-input fold,
+// or the page-locked mirror (host address p, device address dev).
+struct Lease {
+    char *p   = nullptr;
+    char *dev = nullptr;
+    size_t cap = 0;
+};
+
+struct SessChunk {
+    std::string name;
+    const Strategy *st;
+    size_t pending_reduce;  // reduce-graph predecessors not yet folded
+    int recv_count;
+    bool bcast_done;
+    bool batched;              // stage the reduce arrivals, fold them in one launch
+    std::vector<int> waiting;  // reduce predecessors not yet heard from
+    hipEvent_t mirror_ev;      // device mode: the last fold went to the mirror (its end)
+};
+
+// One collective call (all-reduce, reduce, broadcast, subset all-reduce): the
+// request, its chunk plan and its progress. Several are in flight at once on
+// the async path, as the reference runs a goroutine per GoKungfuAllReduce
+// call (libkungfu-comm/collective.go:34-45, main.go:184-191), their messages
+// told apart by chunk name (handler/collective.go:48-64).
+struct SessOp {
+    const char *send = nullptr;
+    char *recv       = nullptr;
+    size_t count     = 0;
+    KungFu_Datatype dt = KungFu_FLOAT;
+    KungFu_Op op       = KungFu_SUM;
+    std::string name;
+    void *stream = nullptr;
+    int kind     = 0;
+    std::vector<Strategy> own;  // SubsetAllReduce's one strategy
+    kf_done_fn done = nullptr;
+    void *arg       = nullptr;
+    // the plan
+    const std::vector<Strategy> *L = nullptr;
+    size_t isz = 0, bytes = 0;
+    bool inplace = false, may_forward = true, use_mirror = false, trivial = false;
+    Strategy single{Graph(0), Graph(0)};
+    std::vector<std::pair<size_t, size_t>> parts;
+    std::vector<SessChunk> chunks;
+    size_t remaining = 0;
+    Lease stage, mir;
+    size_t sends = 0;  // its chunks queued for the sender, not yet written (kf_session::mu)
+    int rc       = KF_OK;
+    std::string err;
 };
 
 }  // namespace
-
-// One queued kf_session_all_reduce_async call.
-struct AsyncOp {
-    const char *send;
-    char *recv;
-    size_t count;
-    KungFu_Datatype dt;
-    KungFu_Op op;
-    std::string name;
-    void *stream;
-    kf_done_fn done;
-    void *arg;
-};
 
 struct kf_session {
     int rank = 0, size = 1;
@@ -408,20 +449,21 @@ struct kf_session {
     kf_host_reduce_fn host_fn = nullptr;
     std::vector<char> scratch;  // host-mode landing buffer (one chunk)
     int batch_fold = 1;         // device mode: k-input fold at multi-predecessor nodes
-    char *stage       = nullptr;  // HBM staging: [predecessor arrival][bucket bytes]
-    size_t stage_bytes = 0;
-    // device mode: a page-locked mirror of the bucket. A node that sends its
-    // finished fold onward (a star or tree root to its bcast successors, an
-    // inner tree node up) folds straight into it — the kernel writes the
-    // result over PCIe while it reads — so the sender has no D2H to wait for;
-    // the node's own HBM copy follows as an H2D off the critical path.
-    // KUNGFU_AMD_ROOT_MIRROR=0 turns it off (A/B).
-    char *txm          = nullptr;  // host address (the sockets)
-    char *txm_dev      = nullptr;  // the same pages as the GPU addresses them
-    size_t txm_bytes   = 0;
+    // per collective in flight, lent from these pools (device mode):
+    //  * HBM staging for the k-input fold: [predecessor arrival][bucket bytes];
+    //  * a page-locked mirror of the bucket. A node that sends its finished
+    //    fold onward (a star or tree root to its bcast successors, an inner
+    //    tree node up) folds straight into it — the kernel writes the result
+    //    over PCIe while it reads — so the sender has no D2H to wait for; the
+    //    node's own HBM copy follows as an H2D off the critical path.
+    //    KUNGFU_AMD_ROOT_MIRROR=0 turns it off (A/B).
+    std::vector<Lease> stage_pool, mirror_pool;
     bool mirror        = true;
+    int device         = 0;        // device mode: the GPU the session was created on
     char *barrier_dev  = nullptr;  // device mode: the barrier's zeroed u8 workspace
     std::deque<Stashed> stash;  // per-name mailbox for early messages
+    std::mutex run_mu;          // one poll loop over the sockets at a time
+    int wake_fd = -1;           // eventfd: a submission, or an op's last chunk sent
 
     // sender thread
     std::thread sender;
@@ -433,52 +475,42 @@ struct kf_session {
     int send_rc     = KF_OK;
     std::string send_err;
 
-    // async all-reduces: one worker thread runs them in submission order
+    // async all-reduces: a worker thread runs every submitted one at once in
+    // one poll loop (run(nullptr)), each started as soon as it is submitted,
+    // so peers may start their names in different orders (a goroutine per
+    // call in the reference, main.go:184-191); done(status, arg) as each
+    // completes. A name submitted again waits for its previous call.
     std::thread aworker;
     std::mutex amu;
     std::condition_variable acv, aidle;
-    std::deque<AsyncOp> aq;
-    size_t apending = 0;  // queued + running
+    std::deque<SessOp *> aq;  // submitted, not yet started
+    size_t apending = 0;      // queued + running
     bool astop      = false;
     int arc         = KF_OK;  // first failure since the last wait_all
     std::string aerr;
 
-    void async_loop()
+    void wake()
     {
-        for (;;) {
-            AsyncOp op;
-            {
-                std::unique_lock<std::mutex> l(amu);
-                acv.wait(l, [&] { return astop || !aq.empty(); });
-                if (aq.empty()) return;
-                op = aq.front();
-                aq.pop_front();
-            }
-            t_sess_error.clear();
-            const int rc = all_reduce(op.send, op.recv, op.count, op.dt, op.op, op.name, op.stream);
-            {
-                std::lock_guard<std::mutex> l(amu);
-                if (rc != KF_OK && arc == KF_OK) {
-                    arc  = rc;
-                    aerr = op.name + ": " + t_sess_error;
-                }
-            }
-            if (op.done) op.done(rc, op.arg);
-            {
-                std::lock_guard<std::mutex> l(amu);
-                if (--apending == 0) aidle.notify_all();
-            }
-        }
+        const uint64_t one = 1;
+        if (wake_fd >= 0) (void)!::write(wake_fd, &one, sizeof(one));
     }
 
-    int submit(const AsyncOp &op)
+    int submit(SessOp *op)
     {
-        std::lock_guard<std::mutex> l(amu);
-        if (astop) return KF_ERR_ARG;
-        if (!aworker.joinable()) aworker = std::thread([this] { async_loop(); });
-        aq.push_back(op);
-        ++apending;
+        {
+            std::lock_guard<std::mutex> l(amu);
+            if (astop) return KF_ERR_ARG;
+            if (!aworker.joinable()) {
+                aworker = std::thread([this] {
+                    if (device_mode) (void)hipSetDevice(device);
+                    (void)run(nullptr);
+                });
+            }
+            aq.push_back(op);
+            ++apending;
+        }
         acv.notify_one();
+        wake();
         return KF_OK;
     }
 
@@ -501,6 +533,7 @@ struct kf_session {
                 astop = true;
             }
             acv.notify_all();
+            wake();
             aworker.join();
         }
         if (sender.joinable()) {
@@ -523,9 +556,10 @@ struct kf_session {
         for (auto e : tx_done) (void)hipEventDestroy(e);
         for (auto e : ev_pool) (void)hipEventDestroy(e);
         if (tx_stream) (void)hipStreamDestroy(tx_stream);
-        if (stage) (void)hipFree(stage);
-        if (txm) (void)hipHostFree(txm);
+        for (auto &l : stage_pool) (void)hipFree(l.p);
+        for (auto &l : mirror_pool) (void)hipHostFree(l.p);
         if (barrier_dev) (void)hipFree(barrier_dev);
+        if (wake_fd >= 0) ::close(wake_fd);
     }
 
     void sender_loop()
@@ -567,14 +601,17 @@ struct kf_session {
             } else if (send_rc == KF_OK) {
                 rc = send_item(it, &err);
             }
+            bool last = false;
             {
                 std::lock_guard<std::mutex> l(mu);
                 if (rc != KF_OK && send_rc == KF_OK) {
                     send_rc  = rc;
                     send_err = err;
                 }
-                if (--inflight == 0) cv_idle.notify_all();
+                if (it.owner) last = --it.owner->sends == 0;
+                if (--inflight == 0 || last) cv_idle.notify_all();
             }
+            if (last) wake();  // that collective may complete now
         }
     }
 
@@ -666,6 +703,7 @@ struct kf_session {
     {
         {
             std::lock_guard<std::mutex> l(mu);
+            if (it.owner) ++it.owner->sends;
             queue.push_back(std::move(it));
             ++inflight;
         }
@@ -857,305 +895,528 @@ struct kf_session {
     int all_reduce(const char *send, char *recv, size_t count, KungFu_Datatype dt,
                    KungFu_Op op, const std::string &name, void *stream, int kind = 0,
                    const std::vector<Strategy> *slist = nullptr);
+
+    // one collective's steps (SessOp), driven by the poll loop run()
+    int plan(SessOp &o);
+    bool expects(const SessOp &o, size_t i, uint32_t flags, int peer) const;
+    int handle(SessOp &o, size_t i, uint32_t flags, int peer, int fd, const char *mem);
+    void send_chunk(SessOp &o, size_t i, std::vector<int> fds, uint32_t fl);
+    int mirror_done(SessOp &o, size_t i, char *dst);
+    void finish_bcast(SessOp &o, size_t i);
+    void finish_reduce(SessOp &o, size_t i);
+    int complete(SessOp &o);
+    int run(SessOp *one);
+    bool take(std::vector<Lease> &pool, size_t need, bool host, Lease *out);
+    void give(std::vector<Lease> &pool, Lease &l);
 };
 
 enum { kAllReduce = 0, kReduce = 1, kBroadcast = 2 };
 
-int kf_session::all_reduce(const char *send, char *recv, size_t count, KungFu_Datatype dt,
-                           KungFu_Op op, const std::string &name, void *stream, int kind,
-                           const std::vector<Strategy> *slist)
+// A buffer of at least `need` bytes from the pool (the smallest that fits); if
+// none fits, the idle ones are freed (their collectives completed, streams
+// synchronized) and one of exactly `need` bytes is allocated.
+bool kf_session::take(std::vector<Lease> &pool, size_t need, bool host, Lease *out)
 {
-    const std::vector<Strategy> &L = slist ? *slist : sl;
-    const size_t isz   = kungfu_type_size(dt);
-    const bool inplace = send == recv;
-    const size_t bytes = count * isz;
-    if (count == 0) return KF_OK;  // w.IsEmpty()
-    if (size == 1) {               // every graph isolated: w.Forward()
-        if (inplace) return KF_OK;
+    int best = -1;
+    for (size_t i = 0; i < pool.size(); ++i) {
+        if (pool[i].cap >= need && (best < 0 || pool[i].cap < pool[best].cap)) {
+            best = static_cast<int>(i);
+        }
+    }
+    if (best >= 0) {
+        *out = pool[best];
+        pool.erase(pool.begin() + best);
+        return true;
+    }
+    for (auto &l : pool) host ? (void)hipHostFree(l.p) : (void)hipFree(l.p);
+    pool.clear();
+    Lease l;
+    if (host) {
+        void *dv = nullptr;
+        if (hipHostMalloc(reinterpret_cast<void **>(&l.p), need, hipHostMallocDefault) != hipSuccess) {
+            return false;
+        }
+        if (hipHostGetDevicePointer(&dv, l.p, 0) != hipSuccess) {
+            (void)hipHostFree(l.p);
+            return false;
+        }
+        l.dev = static_cast<char *>(dv);
+    } else {
+        if (hipMalloc(reinterpret_cast<void **>(&l.p), need) != hipSuccess) return false;
+        l.dev = l.p;
+    }
+    l.cap = need;
+    *out  = l;
+    return true;
+}
+
+void kf_session::give(std::vector<Lease> &pool, Lease &l)
+{
+    if (l.p) pool.push_back(l);
+    l = Lease{};
+}
+
+// The chunk plan of one collective (session.go:301-326): chunks, their
+// strategy by name hash, leases; then the chunks this node has nothing to
+// receive for go out at once. o.remaining == 0 afterwards: nothing to wait for.
+int kf_session::plan(SessOp &o)
+{
+    const std::vector<Strategy> &L = o.L ? *o.L : sl;
+    o.isz     = kungfu_type_size(o.dt);
+    o.inplace = o.send == o.recv;
+    o.bytes   = o.count * o.isz;
+    if (o.count == 0) {  // w.IsEmpty()
+        o.trivial = true;
+        return KF_OK;
+    }
+    if (size == 1) {  // every graph isolated: w.Forward()
+        o.trivial = true;
+        if (o.inplace) return KF_OK;
         if (device_mode) {
-            hipStream_t s = static_cast<hipStream_t>(stream);
-            if (hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, s) != hipSuccess ||
-                hipStreamSynchronize(s) != hipSuccess) {
+            hipStream_t st = static_cast<hipStream_t>(o.stream);
+            if (hipMemcpyAsync(o.recv, o.send, o.bytes, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+                hipStreamSynchronize(st) != hipSuccess) {
                 return fail(KF_ERR_HIP, "forward copy");
             }
         } else {
-            std::memmove(recv, send, bytes);
+            std::memmove(o.recv, o.send, o.bytes);
         }
         return KF_OK;
     }
-    const size_t k   = (bytes + kChunk - 1) / kChunk;
-    const auto parts = even_partition(count, k);
+    const size_t k = (o.bytes + kChunk - 1) / kChunk;
+    o.parts        = even_partition(o.count, k);
     // Reduce / Broadcast: one graph of the first strategy for every chunk (the
     // reference sends the workspace as one message; chunking it the same way
     // as the all-reduce changes no element's result)
-    Strategy single{kind == kBroadcast ? Graph(size) : L[0].reduce,
-                    kind == kReduce ? Graph(size) : L[0].bcast};
+    o.single = Strategy{o.kind == kBroadcast ? Graph(size) : L[0].reduce,
+                        o.kind == kReduce ? Graph(size) : L[0].bcast};
     // runGraphs forwards SendBuf only in a graph without self loops (the bcast
     // graph) or when the node is isolated in every graph it runs
-    const bool isolated = single.reduce.prev[rank].empty() && single.reduce.next[rank].empty() &&
-                          single.bcast.prev[rank].empty() && single.bcast.next[rank].empty();
-    const bool may_forward = kind != kReduce || isolated;
-    struct Chunk {
-        std::string name;
-        const Strategy *st;
-        size_t pending_reduce;  // reduce-graph predecessors not yet folded
-        int recv_count;
-        bool bcast_done;
-        bool batched;  // stage the reduce arrivals, fold them in one launch
-        std::vector<int> waiting;  // reduce predecessors not yet heard from
-        hipEvent_t mirror_ev;      // device mode: the last fold went to txm (its end)
-    };
-    std::vector<Chunk> chunks(parts.size());
-    std::unordered_map<std::string, size_t> index;
+    const Strategy &sg   = o.single;
+    const bool isolated  = sg.reduce.prev[rank].empty() && sg.reduce.next[rank].empty() &&
+                          sg.bcast.prev[rank].empty() && sg.bcast.next[rank].empty();
+    o.may_forward = o.kind != kReduce || isolated;
+    o.chunks.resize(o.parts.size());
     size_t need_stage = 0;
-    for (size_t i = 0; i < parts.size(); ++i) {
-        auto &c = chunks[i];
-        c.name  = "part::" + name + "[" + std::to_string(parts[i].first) + ":" +
-                 std::to_string(parts[i].second) + "]";
+    for (size_t i = 0; i < o.parts.size(); ++i) {
+        auto &c = o.chunks[i];
+        c.name  = "part::" + o.name + "[" + std::to_string(o.parts[i].first) + ":" +
+                 std::to_string(o.parts[i].second) + "]";
         const uint64_t h = hash_name ? name_hash(c.name) : static_cast<uint64_t>(i);
-        c.st             = kind == kAllReduce ? &L[h % L.size()] : &single;
+        c.st             = o.kind == kAllReduce ? &L[h % L.size()] : &o.single;
         c.pending_reduce = c.st->reduce.prev[rank].size();
         c.waiting        = c.st->reduce.prev[rank];
         c.recv_count     = 0;
         c.bcast_done     = false;
-        c.batched        = device_mode && batch_fold && dt != KungFu_BFLOAT16 &&
+        c.batched        = device_mode && batch_fold && o.dt != KungFu_BFLOAT16 &&
                     c.pending_reduce >= 2 && c.pending_reduce + 1 <= KF_MAX_INPUTS;
         c.mirror_ev      = nullptr;
-        if (c.batched && c.pending_reduce * bytes > need_stage) need_stage = c.pending_reduce * bytes;
-        index[c.name]    = i;
+        if (c.batched && c.pending_reduce * o.bytes > need_stage) need_stage = c.pending_reduce * o.bytes;
     }
-    if (need_stage > stage_bytes) {  // the previous all-reduce ended synchronized
-        if (stage) (void)hipFree(stage);
-        stage       = nullptr;
-        stage_bytes = 0;
-        if (hipMalloc(&stage, need_stage) != hipSuccess) {
-            stage = nullptr;
-            return fail(KF_ERR_HIP, "hipMalloc staging for the k-input fold");
-        }
-        stage_bytes = need_stage;
+    if (need_stage > 0 && !take(stage_pool, need_stage, false, &o.stage)) {
+        return fail(KF_ERR_HIP, "hipMalloc staging for the k-input fold");
     }
     // the fold that completes a chunk goes to the page-locked mirror when the
     // chunk then leaves this node (reduce successors, or bcast successors of a
     // node that receives no bcast itself)
-    bool use_mirror = device_mode && mirror && kind == kAllReduce;
-    if (use_mirror && txm_bytes < bytes) {  // the previous all-reduce ended synchronized
-        if (txm) (void)hipHostFree(txm);
-        txm       = nullptr;
-        txm_bytes = 0;
-        void *dv = nullptr;
-        if (hipHostMalloc(reinterpret_cast<void **>(&txm), bytes, hipHostMallocDefault) != hipSuccess ||
-            hipHostGetDevicePointer(&dv, txm, 0) != hipSuccess) {
-            if (txm) (void)hipHostFree(txm);
-            txm        = nullptr;
-            use_mirror = false;
-        } else {
-            txm_bytes = bytes;
-            txm_dev   = static_cast<char *>(dv);
+    o.use_mirror = device_mode && mirror && o.kind == kAllReduce &&
+                   take(mirror_pool, o.bytes, true, &o.mir);
+    o.remaining = o.chunks.size();
+    for (size_t i = 0; i < o.chunks.size(); ++i) {
+        if (o.chunks[i].pending_reduce == 0) {
+            finish_reduce(o, i);
+            if (o.chunks[i].bcast_done) --o.remaining;
         }
     }
-    auto cptr = [&](const char *base, size_t i) { return base + parts[i].first * isz; };
-    auto clen = [&](size_t i) { return (parts[i].second - parts[i].first) * isz; };
-    auto effective = [&](size_t i) -> const char * {
-        return (chunks[i].recv_count > 0 || inplace) ? cptr(recv, i) : cptr(send, i);
-    };
-    auto sends_onward = [&](size_t i) {
-        const auto &st = *chunks[i].st;
-        return !st.reduce.next[rank].empty() ||
-               (st.bcast.prev[rank].empty() && !st.bcast.next[rank].empty());
-    };
-    // an outgoing chunk: from the mirror if the fold wrote it there (first
-    // sender takes the fold's event), else from HBM (D2H by the sender)
-    auto send_item = [&](size_t i, std::vector<int> fds, uint32_t fl) {
-        auto &c = chunks[i];
-        if (c.mirror_ev) {
-            SendItem it{fds, c.name, fl, cptr(txm, i), clen(i), stream, c.mirror_ev};
-            it.host     = true;
-            c.mirror_ev = nullptr;
-            enqueue(std::move(it));
-            return;
-        }
-        enqueue({fds, c.name, fl, effective(i), clen(i), stream,
-                 device_mode ? chunk_ready(stream) : nullptr});
-    };
-    // after the completing fold into the mirror: its end marks the chunk
-    // final for the sender; then this node's own copy of it goes to HBM
-    auto mirror_done = [&](size_t i, char *dst) -> int {
-        auto &c     = chunks[i];
-        c.mirror_ev = chunk_ready(stream);
-        if (!c.mirror_ev ||
-            hipMemcpyAsync(dst, cptr(txm, i), clen(i), hipMemcpyHostToDevice,
-                           static_cast<hipStream_t>(stream)) != hipSuccess) {
-            return fail(KF_ERR_HIP, "mirror copy to HBM");
-        }
-        return KF_OK;
-    };
-    auto finish_bcast = [&](size_t i) {  // after recvInto or at the bcast root
-        auto &c = chunks[i];
-        if (may_forward && c.st->bcast.prev[rank].empty() && c.recv_count == 0 && !inplace) {
-            // w.Forward(): nothing received in either graph
-            if (device_mode) {  // errors surface at the final stream sync
-                (void)hipMemcpyAsync(const_cast<char *>(cptr(recv, i)), cptr(send, i), clen(i),
-                                     hipMemcpyDeviceToDevice, static_cast<hipStream_t>(stream));
-            } else {
-                std::memcpy(const_cast<char *>(cptr(recv, i)), cptr(send, i), clen(i));
-            }
-        }
-        std::vector<int> fds;
-        for (int p : c.st->bcast.next[rank]) fds.push_back(out_fd[p]);
-        if (!fds.empty()) send_item(i, fds, KF_RCH_WAIT_RECV_BUF);
-        c.bcast_done = true;
-    };
-    auto finish_reduce = [&](size_t i) {  // all predecessors folded
-        auto &c = chunks[i];
-        std::vector<int> fds;
-        for (int p : c.st->reduce.next[rank]) fds.push_back(out_fd[p]);
-        if (!fds.empty()) send_item(i, fds, KF_RCH_NO_FLAG);
-        if (c.st->bcast.prev[rank].empty()) finish_bcast(i);
-    };
+    return KF_OK;
+}
 
-    size_t remaining = chunks.size();
-    for (size_t i = 0; i < chunks.size(); ++i) {
-        if (chunks[i].pending_reduce == 0) {
-            finish_reduce(i);
-            if (chunks[i].bcast_done) --remaining;
+namespace
+{
+inline const char *cptr(const SessOp &o, const char *base, size_t i)
+{
+    return base + o.parts[i].first * o.isz;
+}
+inline size_t clen(const SessOp &o, size_t i) { return (o.parts[i].second - o.parts[i].first) * o.isz; }
+inline const char *effective(const SessOp &o, size_t i)
+{
+    return (o.chunks[i].recv_count > 0 || o.inplace) ? cptr(o, o.recv, i) : cptr(o, o.send, i);
+}
+inline bool sends_onward(const SessOp &o, size_t i, int rank)
+{
+    const auto &st = *o.chunks[i].st;
+    return !st.reduce.next[rank].empty() ||
+           (st.bcast.prev[rank].empty() && !st.bcast.next[rank].empty());
+}
+}  // namespace
+
+// an outgoing chunk: from the mirror if the fold wrote it there (first
+// sender takes the fold's event), else from HBM (D2H by the sender)
+void kf_session::send_chunk(SessOp &o, size_t i, std::vector<int> fds, uint32_t fl)
+{
+    auto &c = o.chunks[i];
+    if (c.mirror_ev) {
+        SendItem it{fds, c.name, fl, cptr(o, o.mir.p, i), clen(o, i), o.stream, c.mirror_ev};
+        it.host     = true;
+        it.owner    = &o;
+        c.mirror_ev = nullptr;
+        enqueue(std::move(it));
+        return;
+    }
+    SendItem it{fds, c.name, fl, effective(o, i), clen(o, i), o.stream,
+                device_mode ? chunk_ready(o.stream) : nullptr};
+    it.owner = &o;
+    enqueue(std::move(it));
+}
+
+// after the completing fold into the mirror: its end marks the chunk final
+// for the sender; then this node's own copy of it goes to HBM
+int kf_session::mirror_done(SessOp &o, size_t i, char *dst)
+{
+    auto &c     = o.chunks[i];
+    c.mirror_ev = chunk_ready(o.stream);
+    if (!c.mirror_ev ||
+        hipMemcpyAsync(dst, cptr(o, o.mir.p, i), clen(o, i), hipMemcpyHostToDevice,
+                       static_cast<hipStream_t>(o.stream)) != hipSuccess) {
+        return fail(KF_ERR_HIP, "mirror copy to HBM");
+    }
+    return KF_OK;
+}
+
+void kf_session::finish_bcast(SessOp &o, size_t i)  // after recvInto or at the bcast root
+{
+    auto &c = o.chunks[i];
+    if (o.may_forward && c.st->bcast.prev[rank].empty() && c.recv_count == 0 && !o.inplace) {
+        // w.Forward(): nothing received in either graph
+        if (device_mode) {  // errors surface at the final stream sync
+            (void)hipMemcpyAsync(const_cast<char *>(cptr(o, o.recv, i)), cptr(o, o.send, i),
+                                 clen(o, i), hipMemcpyDeviceToDevice,
+                                 static_cast<hipStream_t>(o.stream));
+        } else {
+            std::memcpy(const_cast<char *>(cptr(o, o.recv, i)), cptr(o, o.send, i), clen(o, i));
         }
     }
-    if (!device_mode && scratch.size() < kChunk + 64) scratch.resize(kChunk + 64);
-    int rc = KF_OK;
-    // Is this message (from `peer`) one chunk i still waits for in THIS call?
-    // The same names recur every step, and a peer that has finished this step
-    // may already send the next one's; such a message waits in the stash, as
-    // in the reference's per-name mailbox (handler/collective.go:27-61).
-    auto expects = [&](size_t i, uint32_t flags, int peer) -> bool {
-        const auto &c = chunks[i];
-        if (flags & KF_RCH_WAIT_RECV_BUF) {
-            const auto &bp = c.st->bcast.prev[rank];
-            return !c.bcast_done && std::find(bp.begin(), bp.end(), peer) != bp.end();
-        }
-        return std::find(c.waiting.begin(), c.waiting.end(), peer) != c.waiting.end();
-    };
-    // one message for chunk i: from the socket fd (mem == nullptr) or from a
-    // stashed copy in host memory
-    auto handle = [&](size_t i, uint32_t flags, int peer, int fd, const char *mem) -> int {
-        auto &c            = chunks[i];
-        if (!(flags & KF_RCH_WAIT_RECV_BUF)) {
-            c.waiting.erase(std::find(c.waiting.begin(), c.waiting.end(), peer));
-        }
-        const size_t n     = parts[i].second - parts[i].first;
-        char *dst          = const_cast<char *>(cptr(recv, i));
-        const uint32_t len = static_cast<uint32_t>(clen(i));
-        int r              = KF_OK;
-        if (flags & KF_RCH_WAIT_RECV_BUF) {  // bcast: recvInto RecvBuf
-            if (device_mode) {
-                r = mem ? kf_ingest_copy_host(ingest, mem, len, dst, stream)
-                        : kf_ingest_recv_into(ingest, fd, len, dst, stream);
-            } else if (mem) {
-                std::memcpy(dst, mem, len);
-            } else {
-                r = kf_rch_recv_body(fd, dst, len);
-            }
-            if (r != KF_OK) return fail(r, kf_ingest_last_error());
-            ++c.recv_count;
-            finish_bcast(i);
-            --remaining;
-            return KF_OK;
-        }
-        if (c.batched) {  // stage arrival #recv_count; fold once all are in
-            char *slot = stage + static_cast<size_t>(c.recv_count) * bytes + parts[i].first * isz;
-            r = mem ? kf_ingest_copy_host(ingest, mem, len, slot, stream)
-                    : kf_ingest_recv_into(ingest, fd, len, slot, stream);
-            if (r != KF_OK) return fail(r, kf_ingest_last_error());
-            ++c.recv_count;
-            if (--c.pending_reduce > 0) return KF_OK;
-            const void *ins[KF_MAX_INPUTS];
-            ins[0] = inplace ? dst : cptr(send, i);  // effective before the first receive
-            for (int a = 0; a < c.recv_count; ++a) {
-                ins[a + 1] = stage + static_cast<size_t>(a) * bytes + parts[i].first * isz;
-            }
-            if (use_mirror && sends_onward(i)) {
-                r = kf_bucket_reduce(ins, c.recv_count + 1, const_cast<char *>(cptr(txm_dev, i)),
-                                     n, dt, op, stream);
-                if (r != KF_OK) return fail(r, kf_last_error());
-                r = mirror_done(i, dst);
-                if (r != KF_OK) return r;
-            } else {
-                r = kf_bucket_reduce(ins, c.recv_count + 1, dst, n, dt, op, stream);
-                if (r != KF_OK) return fail(r, kf_last_error());
-            }
-            finish_reduce(i);
-            if (c.bcast_done) --remaining;
-            return KF_OK;
-        }
-        // reduce: recvOnto, RecvBuf = effective o peer
-        const char *own = effective(i);
+    std::vector<int> fds;
+    for (int p : c.st->bcast.next[rank]) fds.push_back(out_fd[p]);
+    if (!fds.empty()) send_chunk(o, i, fds, KF_RCH_WAIT_RECV_BUF);
+    c.bcast_done = true;
+}
+
+void kf_session::finish_reduce(SessOp &o, size_t i)  // all predecessors folded
+{
+    auto &c = o.chunks[i];
+    std::vector<int> fds;
+    for (int p : c.st->reduce.next[rank]) fds.push_back(out_fd[p]);
+    if (!fds.empty()) send_chunk(o, i, fds, KF_RCH_NO_FLAG);
+    if (c.st->bcast.prev[rank].empty()) finish_bcast(o, i);
+}
+
+// Is this message (from `peer`) one chunk i still waits for in THIS call?
+// The same names recur every step, and a peer that has finished this step
+// may already send the next one's; such a message waits in the stash, as in
+// the reference's per-name mailbox (handler/collective.go:27-61).
+bool kf_session::expects(const SessOp &o, size_t i, uint32_t flags, int peer) const
+{
+    const auto &c = o.chunks[i];
+    if (flags & KF_RCH_WAIT_RECV_BUF) {
+        const auto &bp = c.st->bcast.prev[rank];
+        return !c.bcast_done && std::find(bp.begin(), bp.end(), peer) != bp.end();
+    }
+    return std::find(c.waiting.begin(), c.waiting.end(), peer) != c.waiting.end();
+}
+
+// one message for chunk i: from the socket fd (mem == nullptr) or from a
+// stashed copy in host memory
+int kf_session::handle(SessOp &o, size_t i, uint32_t flags, int peer, int fd, const char *mem)
+{
+    auto &c = o.chunks[i];
+    if (!(flags & KF_RCH_WAIT_RECV_BUF)) {
+        c.waiting.erase(std::find(c.waiting.begin(), c.waiting.end(), peer));
+    }
+    const size_t n     = o.parts[i].second - o.parts[i].first;
+    char *dst          = const_cast<char *>(cptr(o, o.recv, i));
+    const uint32_t len = static_cast<uint32_t>(clen(o, i));
+    void *stream       = o.stream;
+    int r              = KF_OK;
+    if (flags & KF_RCH_WAIT_RECV_BUF) {  // bcast: recvInto RecvBuf
         if (device_mode) {
-            // the completing fold of a chunk that leaves this node goes to the mirror
-            const bool to_mirror = use_mirror && c.pending_reduce == 1 && sends_onward(i);
-            char *out            = to_mirror ? const_cast<char *>(cptr(txm_dev, i)) : dst;
-            r = mem ? kf_ingest_fold_host(ingest, mem, len, out, own, n, dt, op, stream)
-                    : kf_ingest_recv_onto(ingest, fd, len, out, own, n, dt, op, stream);
+            r = mem ? kf_ingest_copy_host(ingest, mem, len, dst, stream)
+                    : kf_ingest_recv_into(ingest, fd, len, dst, stream);
+        } else if (mem) {
+            std::memcpy(dst, mem, len);
+        } else {
+            r = kf_rch_recv_body(fd, dst, len);
+        }
+        if (r != KF_OK) return fail(r, kf_ingest_last_error());
+        ++c.recv_count;
+        finish_bcast(o, i);
+        --o.remaining;
+        return KF_OK;
+    }
+    if (c.batched) {  // stage arrival #recv_count; fold once all are in
+        char *slot = o.stage.p + static_cast<size_t>(c.recv_count) * o.bytes + o.parts[i].first * o.isz;
+        r = mem ? kf_ingest_copy_host(ingest, mem, len, slot, stream)
+                : kf_ingest_recv_into(ingest, fd, len, slot, stream);
+        if (r != KF_OK) return fail(r, kf_ingest_last_error());
+        ++c.recv_count;
+        if (--c.pending_reduce > 0) return KF_OK;
+        const void *ins[KF_MAX_INPUTS];
+        ins[0] = o.inplace ? dst : cptr(o, o.send, i);  // effective before the first receive
+        for (int a = 0; a < c.recv_count; ++a) {
+            ins[a + 1] = o.stage.p + static_cast<size_t>(a) * o.bytes + o.parts[i].first * o.isz;
+        }
+        if (o.use_mirror && sends_onward(o, i, rank)) {
+            r = kf_bucket_reduce(ins, c.recv_count + 1, const_cast<char *>(cptr(o, o.mir.dev, i)), n,
+                                 o.dt, o.op, stream);
+            if (r != KF_OK) return fail(r, kf_last_error());
+            r = mirror_done(o, i, dst);
+            if (r != KF_OK) return r;
+        } else {
+            r = kf_bucket_reduce(ins, c.recv_count + 1, dst, n, o.dt, o.op, stream);
+            if (r != KF_OK) return fail(r, kf_last_error());
+        }
+        finish_reduce(o, i);
+        if (c.bcast_done) --o.remaining;
+        return KF_OK;
+    }
+    // reduce: recvOnto, RecvBuf = effective o peer
+    const char *own = effective(o, i);
+    if (device_mode) {
+        // the completing fold of a chunk that leaves this node goes to the mirror
+        const bool to_mirror = o.use_mirror && c.pending_reduce == 1 && sends_onward(o, i, rank);
+        char *out            = to_mirror ? const_cast<char *>(cptr(o, o.mir.dev, i)) : dst;
+        r = mem ? kf_ingest_fold_host(ingest, mem, len, out, own, n, o.dt, o.op, stream)
+                : kf_ingest_recv_onto(ingest, fd, len, out, own, n, o.dt, o.op, stream);
+        if (r != KF_OK) return fail(r, kf_ingest_last_error());
+        if (to_mirror) {
+            r = mirror_done(o, i, dst);
+            if (r != KF_OK) return r;
+        }
+    } else {
+        const char *pd = mem;
+        if (!mem) {
+            r = kf_rch_recv_body(fd, scratch.data(), len);
             if (r != KF_OK) return fail(r, kf_ingest_last_error());
-            if (to_mirror) {
-                r = mirror_done(i, dst);
-                if (r != KF_OK) return r;
+            pd = scratch.data();
+        }
+        if (host_fn) {
+            if (host_fn(own, pd, dst, static_cast<int64_t>(n), static_cast<int>(o.dt),
+                        static_cast<int>(o.op)) != 0) {
+                return fail(KF_ERR_OP, "host reduce callback failed");
             }
         } else {
-            const char *peer = mem;
-            if (!mem) {
-                r = kf_rch_recv_body(fd, scratch.data(), len);
-                if (r != KF_OK) return fail(r, kf_ingest_last_error());
-                peer = scratch.data();
-            }
-            if (host_fn) {
-                if (host_fn(own, peer, dst, static_cast<int64_t>(n), static_cast<int>(dt),
-                            static_cast<int>(op)) != 0) {
-                    return fail(KF_ERR_OP, "host reduce callback failed");
-                }
-            } else {
-                r = kf_transform2_host(own, peer, dst, n, dt, op);
-                if (r != KF_OK) return fail(r, kf_last_error());
-            }
+            r = kf_transform2_host(own, pd, dst, n, o.dt, o.op);
+            if (r != KF_OK) return fail(r, kf_last_error());
         }
-        ++c.recv_count;
-        if (--c.pending_reduce == 0) {
-            finish_reduce(i);
-            if (c.bcast_done) --remaining;
-        }
-        return KF_OK;
-    };
-    // messages of this all-reduce that arrived during the previous one
-    for (auto it = stash.begin(); it != stash.end() && rc == KF_OK;) {
-        auto f = index.find(it->name);
-        if (f == index.end() || !expects(f->second, it->flags, it->peer)) {
-            ++it;
-            continue;
-        }
-        rc = handle(f->second, it->flags, it->peer, -1, it->data.data());
-        it = stash.erase(it);
     }
+    ++c.recv_count;
+    if (--c.pending_reduce == 0) {
+        finish_reduce(o, i);
+        if (c.bcast_done) --o.remaining;
+    }
+    return KF_OK;
+}
+
+// Every chunk received and every outgoing chunk written: the device work
+// lands before the buffers return to the caller; the leases go back.
+int kf_session::complete(SessOp &o)
+{
+    int rc = o.rc;
+    if (!o.trivial && device_mode) {
+        const int irc = kf_ingest_sync(ingest);
+        if (irc != KF_OK && rc == KF_OK) rc = fail(irc, kf_ingest_last_error());
+        if (hipStreamSynchronize(static_cast<hipStream_t>(o.stream)) != hipSuccess && rc == KF_OK) {
+            rc = fail(KF_ERR_HIP, "stream sync");
+        }
+    }
+    for (auto &c : o.chunks) {  // a failed collective may leave a mirror event unsent
+        if (c.mirror_ev) {
+            std::lock_guard<std::mutex> l(ev_mu);
+            ev_pool.push_back(c.mirror_ev);
+            c.mirror_ev = nullptr;
+        }
+    }
+    give(stage_pool, o.stage);
+    give(mirror_pool, o.mir);
+    if (rc != KF_OK && o.err.empty()) o.err = t_sess_error;
+    o.rc = rc;
+    return rc;
+}
+
+// The poll loop: every collective in flight advances on whatever message
+// arrives next (a chunk's reduce-phase NoFlag message, or its bcast-phase
+// WaitRecvBuf one); messages of calls not started here yet wait in the stash.
+// one != nullptr: that single (blocking) call, returning its status; nullptr:
+// the async worker, which starts every submitted call at once and calls
+// done(status, arg) as each completes, until the session stops.
+int kf_session::run(SessOp *one)
+{
+    std::unique_lock<std::mutex> rl(run_mu);
+    std::vector<SessOp *> active;
+    std::unordered_map<std::string, std::pair<SessOp *, size_t>> index;  // chunk -> op, chunk
     std::vector<pollfd> pfds;
     std::vector<int> pfd_peer;
     for (auto &kv : in_fd) {
         pfds.push_back({kv.second, POLLIN, 0});
         pfd_peer.push_back(kv.first);
     }
+    if (!one && wake_fd >= 0) {
+        pfds.push_back({wake_fd, POLLIN, 0});
+        pfd_peer.push_back(-1);
+    }
+    if (!device_mode && scratch.size() < kChunk + 64) scratch.resize(kChunk + 64);
+
+    // a failure while reading the sockets leaves no message boundary to trust:
+    // every collective in flight fails with it (its chunks stop being routed)
+    auto fail_all = [&](int rc) {
+        const std::string why = t_sess_error;
+        for (SessOp *o : active) {
+            if (o->rc == KF_OK) {
+                o->rc  = rc;
+                o->err = why;
+            }
+            for (auto &c : o->chunks) index.erase(c.name);
+            o->remaining = 0;
+        }
+    };
+    auto start = [&](SessOp *o) {
+        t_sess_error.clear();
+        o->rc = plan(*o);
+        if (o->rc != KF_OK) {
+            o->err       = t_sess_error;
+            o->remaining = 0;
+        }
+        active.push_back(o);
+        if (o->rc != KF_OK) return;
+        for (size_t i = 0; i < o->chunks.size(); ++i) index[o->chunks[i].name] = {o, i};
+        // messages of this call that arrived before it started
+        for (auto it = stash.begin(); it != stash.end();) {
+            auto f = index.find(it->name);
+            if (f == index.end() || f->second.first != o ||
+                !expects(*o, f->second.second, it->flags, it->peer)) {
+                ++it;
+                continue;
+            }
+            const int rc = handle(*o, f->second.second, it->flags, it->peer, -1, it->data.data());
+            it           = stash.erase(it);
+            if (rc != KF_OK) {  // a stashed copy: the sockets are intact
+                o->rc        = rc;
+                o->err       = t_sess_error;
+                o->remaining = 0;
+                for (auto &c : o->chunks) index.erase(c.name);
+                return;
+            }
+        }
+    };
+    if (one) start(one);
+
     char hname[512];
     uint32_t flags = 0;
-    while (remaining > 0 && rc == KF_OK) {
+    for (;;) {
+        if (!one) {  // start what was submitted; a name in flight waits for its call
+            std::vector<SessOp *> fresh;
+            {
+                std::lock_guard<std::mutex> l(amu);
+                std::vector<std::string> busy;
+                for (SessOp *o : active) busy.push_back(o->name);
+                for (auto it = aq.begin(); it != aq.end();) {
+                    if (std::find(busy.begin(), busy.end(), (*it)->name) != busy.end()) {
+                        ++it;
+                        continue;
+                    }
+                    busy.push_back((*it)->name);
+                    fresh.push_back(*it);
+                    it = aq.erase(it);
+                }
+            }
+            for (SessOp *o : fresh) start(o);
+        }
+        // complete the collectives whose chunks are all in and all sent
+        for (size_t a = 0; a < active.size();) {
+            SessOp *o = active[a];
+            bool sent = false;
+            {
+                std::lock_guard<std::mutex> l(mu);
+                sent = o->sends == 0;
+                if (sent && o->remaining == 0 && send_rc != KF_OK && o->rc == KF_OK) {
+                    o->rc  = send_rc;
+                    o->err = "send: " + send_err;
+                }
+            }
+            if (o->remaining > 0 || !sent) {
+                ++a;
+                continue;
+            }
+            active.erase(active.begin() + a);
+            for (auto &c : o->chunks) {
+                auto f = index.find(c.name);
+                if (f != index.end() && f->second.first == o) index.erase(f);
+            }
+            if (active.empty()) {  // a send failure is reported once everything in flight saw it
+                std::lock_guard<std::mutex> l(mu);
+                send_rc = KF_OK;
+                send_err.clear();
+            }
+            t_sess_error = o->err;
+            const int rc = complete(*o);
+            if (o == one) {
+                if (rc != KF_OK) t_sess_error = o->err;
+                return rc;
+            }
+            {
+                std::lock_guard<std::mutex> l(amu);
+                if (rc != KF_OK && arc == KF_OK) {
+                    arc  = rc;
+                    aerr = o->name + ": " + o->err;
+                }
+            }
+            t_sess_error = o->err;
+            if (o->done) o->done(rc, o->arg);
+            delete o;
+            {
+                std::lock_guard<std::mutex> l(amu);
+                if (--apending == 0) aidle.notify_all();
+            }
+        }
+        if (!one && active.empty()) {  // idle: wait for a submission, or the end;
+            rl.unlock();               // blocking calls run their own loop meanwhile
+            {
+                std::unique_lock<std::mutex> l(amu);
+                acv.wait(l, [&] { return astop || !aq.empty(); });
+                if (aq.empty()) return KF_OK;
+            }
+            rl.lock();
+            continue;
+        }
+        bool waiting_rx = false;  // anything still expected from the sockets?
+        for (SessOp *o : active) waiting_rx = waiting_rx || o->remaining > 0;
+        if (!waiting_rx && one) {  // only our own sends are left: the sender wakes no one here
+            std::unique_lock<std::mutex> l(mu);
+            cv_idle.wait(l, [&] { return one->sends == 0; });
+            continue;
+        }
         if (::poll(pfds.data(), pfds.size(), -1) < 0) {
             if (errno == EINTR) continue;
-            rc = fail(KF_ERR_IO, std::string("poll: ") + strerror(errno));
-            break;
+            fail_all(fail(KF_ERR_IO, std::string("poll: ") + strerror(errno)));
+            continue;
         }
         size_t open_fds = 0;
-        for (auto &pf : pfds) open_fds += pf.fd >= 0;
-        if (open_fds == 0) {
-            rc = fail(KF_ERR_IO, "every peer connection closed before the all-reduce finished");
-            break;
+        for (size_t q = 0; q < pfds.size(); ++q) open_fds += pfds[q].fd >= 0 && pfd_peer[q] >= 0;
+        if (open_fds == 0 && waiting_rx) {
+            fail_all(fail(KF_ERR_IO, "every peer connection closed before the all-reduce finished"));
+            continue;
         }
-        for (size_t q = 0; q < pfds.size() && rc == KF_OK && remaining > 0; ++q) {
+        int rc  = KF_OK;
+        int bad = -1;  // the socket a failure happened on
+        for (size_t q = 0; q < pfds.size() && rc == KF_OK; ++q) {
+            bad = static_cast<int>(q);
             if (pfds[q].fd < 0 || !(pfds[q].revents & (POLLIN | POLLHUP | POLLERR))) continue;
             const int fd = pfds[q].fd;
+            if (pfd_peer[q] < 0) {  // the wake-up counter
+                uint64_t v;
+                (void)!::read(fd, &v, sizeof(v));
+                continue;
+            }
             char probe;
             if (::recv(fd, &probe, 1, MSG_PEEK | MSG_DONTWAIT) == 0) {
                 // clean EOF at a message boundary: that peer is done with us
@@ -1171,34 +1432,43 @@ int kf_session::all_reduce(const char *send, char *recv, size_t count, KungFu_Da
             }
             const int peer = pfd_peer[q];
             auto it        = index.find(hname);
-            if (it != index.end() && expects(it->second, flags, peer)) {
-                rc = handle(it->second, flags, peer, fd, nullptr);
+            if (it != index.end() && expects(*it->second.first, it->second.second, flags, peer)) {
+                rc = handle(*it->second.first, it->second.second, flags, peer, fd, nullptr);
                 continue;
             }
-            // not ours (yet): keep it for the all-reduce call it belongs to
+            // not ours (yet): keep it for the call it belongs to
             Stashed m{peer, hname, flags, {}};
-            uint32_t len = 0;
             unsigned char lb[4];
             rc = read_exact(fd, lb, 4);
             if (rc != KF_OK) break;
-            len = uint32_t(lb[0]) | (uint32_t(lb[1]) << 8) | (uint32_t(lb[2]) << 16) |
-                  (uint32_t(lb[3]) << 24);
+            const uint32_t len = uint32_t(lb[0]) | (uint32_t(lb[1]) << 8) |
+                                 (uint32_t(lb[2]) << 16) | (uint32_t(lb[3]) << 24);
             m.data.resize(len);
             rc = read_exact(fd, m.data.data(), len);
             if (rc == KF_OK) stash.push_back(std::move(m));
         }
-    }
-    const int drc = drain();  // our sends must be out before the buffers return
-    if (rc != KF_OK) return rc;
-    if (drc != KF_OK) return drc;
-    if (device_mode) {
-        rc = kf_ingest_sync(ingest);
-        if (rc != KF_OK) return fail(rc, kf_ingest_last_error());
-        if (hipStreamSynchronize(static_cast<hipStream_t>(stream)) != hipSuccess) {
-            return fail(KF_ERR_HIP, "stream sync");
+        if (rc != KF_OK) {
+            pfds[bad].fd = -1;  // no message boundary left on it
+            fail_all(rc);
         }
     }
-    return KF_OK;
+}
+
+int kf_session::all_reduce(const char *send, char *recv, size_t count, KungFu_Datatype dt,
+                           KungFu_Op op, const std::string &name, void *stream, int kind,
+                           const std::vector<Strategy> *slist)
+{
+    SessOp o;
+    o.send   = send;
+    o.recv   = recv;
+    o.count  = count;
+    o.dt     = dt;
+    o.op     = op;
+    o.name   = name;
+    o.stream = stream;
+    o.kind   = kind;
+    o.L      = slist;
+    return run(&o);
 }
 
 namespace
@@ -1229,7 +1499,14 @@ kf_session_t *create_session(int rank, std::vector<PeerAddr> peers, const char *
         s->hash_name = std::strcmp(e, "NAME") == 0 || std::strcmp(e, "name") == 0;
     }
     s->sl = strategy_list(s->strategy, s->hosts());
+    s->wake_fd = ::eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+    if (s->wake_fd < 0) {
+        t_sess_error = std::string("eventfd: ") + strerror(errno);
+        delete s;
+        return nullptr;
+    }
     if (s->device_mode) {
+        (void)hipGetDevice(&s->device);
         s->ingest = kf_ingest_create(kChunk + 4096, 8);
         int nslot = 4;
         if (const char *e = std::getenv("KUNGFU_AMD_TX_SLOTS")) nslot = std::max(1, std::atoi(e));
@@ -1414,9 +1691,19 @@ int kf_session_all_reduce_async(kf_session_t *s, const void *send, void *recv, s
     default: return KF_ERR_DTYPE;
     }
     if (static_cast<unsigned>(op) > KungFu_PROD) return KF_ERR_OP;
-    AsyncOp a{static_cast<const char *>(send), static_cast<char *>(recv), count, dt, op, name,
-              stream, done, arg};
-    return s->submit(a);
+    auto *o   = new SessOp;
+    o->send   = static_cast<const char *>(send);
+    o->recv   = static_cast<char *>(recv);
+    o->count  = count;
+    o->dt     = dt;
+    o->op     = op;
+    o->name   = name;
+    o->stream = stream;
+    o->done   = done;
+    o->arg    = arg;
+    const int rc = s->submit(o);
+    if (rc != KF_OK) delete o;
+    return rc;
 }
 
 int kf_session_barrier(kf_session_t *s)

@@ -168,12 +168,14 @@ class Session:
         return recv
 
     def all_reduce_async(self, send, recv, name, op="sum", callback=None):
-        """Queue an all-reduce and return at once (GoKungfuAllReduce with a
+        """Start an all-reduce and return at once (GoKungfuAllReduce with a
         done callback, libkungfu-comm/collective.go:34-45): the session's
-        worker thread runs queued all-reduces in submission order, so every
-        peer submits the same names in the same order. ``callback(status)``
-        runs on that thread when the all-reduce is done; ``handle.wait()``
-        blocks until then and raises on failure. send/recv must not be touched
+        worker thread runs every started all-reduce at once, pairing peers'
+        messages by name as the reference's goroutine per call does, so peers
+        may start their names in different orders (a name started again waits
+        for its previous call). ``callback(status)`` runs on that thread when
+        the all-reduce is done, in completion order; ``handle.wait()`` blocks
+        until then and raises on failure. send/recv must not be touched
         before that."""
         red = OP_NAMES[op] if isinstance(op, str) else OP(op)
         count, dt, sp = self._meta(send)

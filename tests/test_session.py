@@ -382,7 +382,7 @@ def _async_body(rank, size, sock_dir, mode, errq):
         assert all(h.done() for h in hs)
         outs = [h.wait() for h in hs]
         s.wait_all()
-        assert [n for n, _ in seen] == [n for n, _, _ in specs]  # submission order
+        assert sorted(n for n, _ in seen) == sorted(n for n, _, _ in specs)  # completion order
         assert all(st == 0 for _, st in seen)
         assert len(nested) == 1 and "KF_ERR_ARG" in nested[0], nested
         s.close()
@@ -424,6 +424,89 @@ def test_session_async_device():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     _run_async(3, "device")
+
+
+def _any_order_body(rank, size, sock_dir, mode, strategy, errq):
+    """Every peer starts the same named all-reduces in its OWN random order,
+    two steps of them (a name's second call waits for its first), as the
+    reference allows: each GoKungfuAllReduce is its own goroutine and peers'
+    messages pair by name (handler/collective.go:48-64). Exact inputs (ints,
+    and the C1 floats whose sums are exact in any order)."""
+    sys.path[:0] = [ROOT, HERE]
+    try:
+        import time
+        if strategy is not None:
+            os.environ["KUNGFU_ALLREDUCE_STRATEGY"] = strategy
+        from kungfu_amd.session import Session
+        specs = [("w%d" % j, "iota" if j % 2 else "c1", n)
+                 for j, n in enumerate([5, 1 << 18, (5 << 20) // 4 + 3, 4099, 77, (3 << 20) // 4])]
+        rng = np.random.default_rng(1000 + rank)
+        if mode == "device":
+            import torch
+            dev = torch.device("cuda:0")
+            s = Session(rank, size, sock_dir, mode="device")
+        else:
+            s = Session(rank, size, sock_dir, mode="host", host_reduce_fn=oracle_reduce_fn())
+        for step in range(2):
+            hs = []
+            for j in rng.permutation(len(specs)):
+                name, kind, n = specs[j]
+                x = inputs(rank, n, kind) * (step + 1)
+                if mode == "device":
+                    snd = torch.from_numpy(x).to(dev)
+                    rcv = torch.zeros_like(snd) if j % 3 else snd  # some in place
+                else:
+                    snd = x.copy()
+                    rcv = np.zeros_like(x) if j % 3 else snd
+                hs.append((j, s.all_reduce_async(snd, rcv, name)))
+                if rng.random() < 0.3:
+                    time.sleep(0.01)  # let some run before the rest start
+            s.wait_all()
+            for j, h in hs:
+                name, kind, n = specs[j]
+                got = h.wait()
+                if mode == "device":
+                    got = got.cpu().numpy()
+                want = sum(inputs(r, n, kind) for r in range(size)) * (step + 1)
+                assert np.array_equal(got, want.astype(got.dtype)), (rank, step, name)
+        s.close()
+    except Exception:
+        errq.put("rank %d: %s" % (rank, traceback.format_exc()))
+
+
+def _run_any_order(size, mode, strategy=None):
+    ctx = mp.get_context("spawn")
+    errq = ctx.SimpleQueue()
+    with tempfile.TemporaryDirectory() as d:
+        ps = [ctx.Process(target=_any_order_body, args=(r, size, d, mode, strategy, errq))
+              for r in range(size)]
+        for p in ps:
+            p.start()
+        for p in ps:
+            p.join(timeout=120)
+        for p in ps:
+            if p.exitcode is None:
+                p.kill()
+    errs = []
+    while not errq.empty():
+        errs.append(errq.get())
+    assert not errs, "\n".join(errs)
+    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+
+
+@pytest.mark.parametrize("size,strategy", [(2, None), (3, None), (4, "RING"), (3, "CLIQUE"),
+                                           (4, "BINARY_TREE")])
+def test_session_async_any_order_host(size, strategy):
+    _run_any_order(size, "host", strategy)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("size,strategy", [(3, None), (4, "RING")])
+def test_session_async_any_order_device(size, strategy):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _run_any_order(size, "device", strategy)
 
 
 def test_session_async_arg_errors():
