@@ -428,7 +428,8 @@ def test_session_async_device():
 
 def _any_order_body(rank, size, sock_dir, mode, strategy, errq):
     """Every peer starts the same named all-reduces in its OWN random order,
-    two steps of them (a name's second call waits for its first), as the
+    two steps of them back to back (a name's second call waits for its
+    first; the peers' step-2 chunks wait in the stash meanwhile), as the
     reference allows: each GoKungfuAllReduce is its own goroutine and peers'
     messages pair by name (handler/collective.go:48-64). Exact inputs (ints,
     and the C1 floats whose sums are exact in any order)."""
@@ -447,8 +448,8 @@ def _any_order_body(rank, size, sock_dir, mode, strategy, errq):
             s = Session(rank, size, sock_dir, mode="device")
         else:
             s = Session(rank, size, sock_dir, mode="host", host_reduce_fn=oracle_reduce_fn())
-        for step in range(2):
-            hs = []
+        hs = []
+        for step in range(2):  # step 2 starts while step 1 may be in flight
             for j in rng.permutation(len(specs)):
                 name, kind, n = specs[j]
                 x = inputs(rank, n, kind) * (step + 1)
@@ -458,17 +459,17 @@ def _any_order_body(rank, size, sock_dir, mode, strategy, errq):
                 else:
                     snd = x.copy()
                     rcv = np.zeros_like(x) if j % 3 else snd
-                hs.append((j, s.all_reduce_async(snd, rcv, name)))
+                hs.append((step, j, s.all_reduce_async(snd, rcv, name)))
                 if rng.random() < 0.3:
                     time.sleep(0.01)  # let some run before the rest start
-            s.wait_all()
-            for j, h in hs:
-                name, kind, n = specs[j]
-                got = h.wait()
-                if mode == "device":
-                    got = got.cpu().numpy()
-                want = sum(inputs(r, n, kind) for r in range(size)) * (step + 1)
-                assert np.array_equal(got, want.astype(got.dtype)), (rank, step, name)
+        s.wait_all()
+        for step, j, h in hs:
+            name, kind, n = specs[j]
+            got = h.wait()
+            if mode == "device":
+                got = got.cpu().numpy()
+            want = sum(inputs(r, n, kind) for r in range(size)) * (step + 1)
+            assert np.array_equal(got, want.astype(got.dtype)), (rank, step, name)
         s.close()
     except Exception:
         errq.put("rank %d: %s" % (rank, traceback.format_exc()))
