@@ -510,6 +510,52 @@ def test_session_async_any_order_device(size, strategy):
     _run_any_order(size, "device", strategy)
 
 
+def _dead_peer_body(rank, sock_dir, errq):
+    """Rank 1 connects and leaves without joining; rank 0's in-flight async
+    all-reduces must fail (every peer connection closed), not hang."""
+    sys.path[:0] = [ROOT, HERE]
+    try:
+        from kungfu_amd.session import Session
+        s = Session(rank, 2, sock_dir, mode="host", host_reduce_fn=oracle_reduce_fn())
+        if rank == 1:
+            s.close()
+            return
+        xs = [inputs(0, n, "iota") for n in (9, 1 << 19)]
+        got = []
+        hs = [s.all_reduce_async(x, np.zeros_like(x), "dead/%d" % i,
+                                 callback=lambda st: got.append(st))
+              for i, x in enumerate(xs)]
+        try:
+            s.wait_all()
+            raise AssertionError("wait_all succeeded with the peer gone")
+        except RuntimeError as e:
+            assert "closed" in str(e) or "KF_ERR_IO" in str(e), e
+        assert len(got) == 2 and all(st != 0 for st in got), got
+        assert all(h.done() for h in hs)
+        s.close()
+    except Exception:
+        errq.put("rank %d: %s" % (rank, traceback.format_exc()))
+
+
+def test_session_async_peer_gone():
+    ctx = mp.get_context("spawn")
+    errq = ctx.SimpleQueue()
+    with tempfile.TemporaryDirectory() as d:
+        ps = [ctx.Process(target=_dead_peer_body, args=(r, d, errq)) for r in range(2)]
+        for p in ps:
+            p.start()
+        for p in ps:
+            p.join(timeout=60)
+        for p in ps:
+            if p.exitcode is None:
+                p.kill()
+    errs = []
+    while not errq.empty():
+        errs.append(errq.get())
+    assert not errs, "\n".join(errs)
+    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+
+
 def test_session_async_arg_errors():
     import ctypes
     from kungfu_amd import _lib
