@@ -82,7 +82,7 @@ def parse():
                     help="rehearsal only: put every rank on this GPU")
     ap.add_argument("--no-extra", action="store_true",
                     help="N>1: skip the C4/C5/P2P sub-benchmarks")
-    ap.add_argument("--extras", default="c4,c5,c5_pipe,c4_pipe,c4_named,c3_pipe,c3_a2a,c3_fused,c3_torch_fused,c3_per_bucket,c4_torch,"
+    ap.add_argument("--extras", default="c4,c5,c5_pipe,c5_overlap,c4_pipe,c4_named,c3_pipe,c3_a2a,c3_fused,c3_torch_fused,c3_per_bucket,c4_torch,"
                                         "c5_torch,c3_ar,c3_p2p,c3_p2p_push,c3_p2p_hostbar,"
                                         "c4_p2p,c5_p2p",
                     help="N>1: which sub-benchmarks to run (comma list)")
@@ -879,6 +879,7 @@ def main():
                  ("c5", lambda: bench_c5(world, rank, dev, steps_x, 5, exchange="native")),
                  ("c5_pipe", lambda: bench_c5(world, rank, dev, steps_x, 5,
                                               exchange="native_pipe")),
+                 ("c5_overlap", lambda: bench_c5_overlap(world, rank, dev, min(steps_x, 20), 3)),
                  ("c4_pipe", lambda: bench_c4(world, rank, dev, steps_x, 5,
                                               exchange="native_pipe")),
                  ("c3_pipe", lambda: bench_c3_native(world, rank, dev, steps_x, 5, n, x, "rs",
@@ -1655,6 +1656,79 @@ def bench_c5(world, rank, dev, steps, warmup, alpha=0.1, exchange="native"):
             "parity": "bf16 unpinned (DESIGN.md); bit-exact vs the local rank-order fold "
                       "+ blend"}
 
+
+def bench_c5_overlap(world, rank, dev, steps, warmup, alpha=0.1):
+    """C5's SMA exchange overlapped with compute, as
+    SynchronousAveragingOptimizer(overlap=True) runs it: the sum of the
+    variables starts on the exchange's own stream (NativeExchange.start_ on a
+    copy), a stand-in for the step's forward and backward (bf16 GEMMs sized
+    to about the exchange's own time) runs on the current stream meanwhile,
+    then the step waits and blends (the batched HIP kernel). Against the
+    serial step (compute, then the synchronous sma_). Checked first: the
+    overlapped blend equals the synchronous one bit for bit."""
+    from kungfu_amd import ops
+    from kungfu_amd.collective import GradBuckets
+    ex = _exchange("native")
+    sizes = _models()["bert"][:201]
+    mine = GradBuckets(sizes, torch.bfloat16, dev, world, bucket_bytes=16 << 20)
+    _fill(mine, 700 + rank, dev, torch.bfloat16)
+    sums = [torch.empty_like(b) for b in mine.buckets]
+    v0 = [b.clone() for b in mine.buckets]
+
+    def start():
+        for s, b in zip(sums, mine.buckets):
+            s.copy_(b)
+        return ex.start_(sums, op="sum", average=False, coalesce=False, key="c5o")
+
+    def finish(h):
+        h.wait()
+        ops.sma_blend_batch_(mine.buckets, sums, world, alpha)
+
+    finish(start())
+    over = [b.clone() for b in mine.buckets]
+    for b, v in zip(mine.buckets, v0):
+        b.copy_(v)
+    ex.sma_(mine.buckets, alpha)
+    ok = all(torch.equal(a, b) for a, b in zip(over, mine.buckets))
+    del over, v0
+    if not _agree(ok, dev):
+        return {"error": "overlapped SMA differs from the synchronous sma_"}
+    t_x = _timed(lambda: ex.sma_(mine.buckets, alpha), steps, warmup, dev, world)
+    n = 4096
+    a = torch.randn(n, n, device=dev, dtype=torch.bfloat16)
+    w = torch.randn(n, n, device=dev, dtype=torch.bfloat16) / n
+    t_mm = _timed(lambda: torch.mm(a, w), 20, 3, dev, world)
+    k = max(1, int(round(t_x / t_mm)))
+
+    def compute():
+        x = a
+        for _ in range(k):
+            x = torch.mm(x, w)
+        return x
+
+    t_c = _timed(compute, steps, warmup, dev, world)
+
+    def serial():
+        compute()
+        ex.sma_(mine.buckets, alpha)
+
+    def overlapped():
+        h = start()
+        compute()
+        finish(h)
+
+    t_s = _timed(serial, steps, warmup, dev, world)
+    t_o = _timed(overlapped, steps, warmup, dev, world)
+    hidden = (t_s - t_o) / min(t_c, t_x) if min(t_c, t_x) > 0 else None
+    return {"workload": "C5: BERT-base bf16 SMA (%d buckets) beside %d bf16 GEMMs of %d^3 on the "
+                        "current stream, overlapped (the sum on the exchange's stream, "
+                        "SynchronousAveragingOptimizer(overlap=True)) vs serial"
+                        % (len(mine.buckets), k, n),
+            "exchange_ms": round(t_x * 1e3, 4), "compute_ms": round(t_c * 1e3, 4),
+            "serial_ms": round(t_s * 1e3, 4), "overlapped_ms": round(t_o * 1e3, 4),
+            "ms_per_step": round(t_o * 1e3, 4),
+            "hidden_frac": round(hidden, 3) if hidden is not None else None,
+            "parity": "overlapped blend == synchronous sma_ bit for bit"}
 
 
 if __name__ == "__main__":

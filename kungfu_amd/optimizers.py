@@ -184,14 +184,19 @@ def SynchronousSGDOptimizer(optimizer, named_parameters=None, op=None,
 
 
 class _SMA(_Bucketed):
+    def _kf_build_sma(self):
+        self._kf_build(None)
+        for ps, gb in self._kf_groups:  # move the variables into buckets
+            for p, view in zip(ps, gb.views):
+                v = view.view_as(p)
+                v.copy_(p.data)
+                p.data = v
+
     def sync_variables(self):
         if self._kf_groups is None:
-            self._kf_build(None)
-            for ps, gb in self._kf_groups:  # move the variables into buckets
-                for p, view in zip(ps, gb.views):
-                    v = view.view_as(p)
-                    v.copy_(p.data)
-                    p.data = v
+            self._kf_build_sma()
+        if self._kf_overlap:
+            return self._kf_sync_overlapped()
         for ps, gb in self._kf_groups:
             # sma_sgd.py:53-57: only variables that have a gradient take part;
             # others are restored after the blend
@@ -200,17 +205,71 @@ class _SMA(_Bucketed):
             for p, d in saved:
                 p.data.copy_(d)
 
+    # overlap=True: the sum of the variables is all-reduced while the next
+    # step's forward and backward run. SMA reduces v_t, the variables the
+    # step's forward used (sma_sgd.py:60-65: group_all_reduce(variables)
+    # before the blend and the gradient update), and they do not change
+    # between the end of step t-1 and the blend of step t, so the sum can
+    # start as soon as step t-1 has updated them — on the exchange's own
+    # stream, into a workspace per bucket — and step t only waits for it and
+    # blends. The collectives and the blend kernel are those of sma_(), so the
+    # result is the same bit for bit.
+    def _kf_start_sums(self):
+        if self._kf_sums is None:
+            import torch
+            self._kf_sums = [[torch.empty_like(b) for b in gb.buckets]
+                             for _, gb in self._kf_groups]
+        self._kf_pending = []
+        for gi, ((_, gb), sums) in enumerate(zip(self._kf_groups, self._kf_sums)):
+            for s, b in zip(sums, gb.buckets):
+                s.copy_(b)
+            self._kf_pending.append(self._kf_ex.start_(sums, op="sum", average=False,
+                                                       coalesce=False, key=("sma", gi)))
+
+    def _kf_sync_overlapped(self):
+        if self._kf_pending is None:  # the first step: nothing started yet
+            self._kf_start_sums()
+        world = self._kf_ex.world
+        epilogue = getattr(self._kf_ex, "epilogue", None)
+        for (ps, gb), sums, h in zip(self._kf_groups, self._kf_sums, self._kf_pending):
+            saved = [(p, p.data.clone()) for p in ps if p.grad is None]
+            h.wait()
+            if epilogue is not None:  # collective.Exchange: its own epilogue
+                for b, s in zip(gb.buckets, sums):
+                    epilogue.sma_blend_(b, s, world, self._kf_alpha)
+            else:  # the native exchange's blend: the batched HIP kernel
+                from . import ops
+                ops.sma_blend_batch_(gb.buckets, sums, world, self._kf_alpha)
+            for p, d in saved:
+                p.data.copy_(d)
+        self._kf_pending = None
+
     def step(self, closure=None):
         self.sync_variables()
         _finish(self._kf_ex)
-        return super().step(closure)
+        out = super().step(closure)
+        if self._kf_overlap:  # v_{t+1} is final: start its sum now
+            self._kf_start_sums()
+        return out
 
 
 def SynchronousAveragingOptimizer(optimizer, named_parameters=None, alpha=0.1,
-                                  exchange=None, bucket_bytes=32 << 20):
+                                  exchange=None, bucket_bytes=32 << 20, overlap=False):
     """SMA: v <- (1 - alpha) v + alpha * mean_ranks(v) before each local step
-    (sma_sgd.py:50-74)."""
+    (sma_sgd.py:50-74).
+
+    overlap=True starts the all-reduce of the next step's variables at the
+    end of step() on the exchange's stream, so it runs during that step's
+    forward and backward; step() then waits for it and blends. Same values as
+    overlap=False, provided the variables change only through step() (the
+    first step reduces synchronously)."""
     opt = _wrap(optimizer, _SMA)
     opt._kf_setup(named_parameters, exchange, bucket_bytes)
     opt._kf_alpha = float(alpha)
+    opt._kf_overlap = bool(overlap)
+    opt._kf_sums = None
+    opt._kf_pending = None
+    if opt._kf_overlap and not hasattr(opt._kf_ex, "start_"):
+        raise ValueError("overlap=True needs an exchange with start_() "
+                         "(collective.Exchange or exchange.NativeExchange)")
     return opt

@@ -63,6 +63,7 @@ res = {
     "c4_pipe": bench.bench_c4(1, 0, dev, 3, 1, exchange="native_pipe"),
     "c5": bench.bench_c5(1, 0, dev, 3, 1, exchange="native"),
     "c5_pipe": bench.bench_c5(1, 0, dev, 3, 1, exchange="native_pipe"),
+    "c5_overlap": bench.bench_c5_overlap(1, 0, dev, 3, 1),
     "c3_a2a": bench.bench_c3_native(1, 0, dev, 3, 1, n, x, "a2a", 64),
     "c3_fused": bench.bench_c3_native(1, 0, dev, 3, 1, n, x, "rs", 64, fused=True),
     "c3_pipe": bench.bench_c3_native(1, 0, dev, 3, 1, n, x, "rs", 64, pipe=True),
@@ -75,8 +76,8 @@ print("NATIVE_SUB_OK" if not bad else "NATIVE_SUB_BAD %%r" %% bad)
 
 
 def test_bench_native_subbenchmarks_world1_rccl():
-    """bench.py's native sub-benchmark bodies (c4, c5, c3_a2a, c3_fused and the
-    pipelined c3/c4/c5) run end to end — parity check, timed loop — over a
+    """bench.py's native sub-benchmark bodies (c4, c5, c3_a2a, c3_fused, the
+    pipelined c3/c4/c5 and C5 overlapped with compute) run end to end — parity check, timed loop — over a
     one-rank RCCL communicator bound through the test library's rccl1
     transport (librccl's collectives, no world-1 copy), so the code the
     driver's multi-GPU node runs first has run on real RCCL here."""
@@ -115,7 +116,7 @@ def test_bench_exchange_branch_single_rank_rccl():
         pytest.skip("no GPU")
     env = dict(os.environ, MASTER_ADDR="127.0.0.1",
                MASTER_PORT=str(_port()), RANK="0", LOCAL_RANK="0", WORLD_SIZE="1")
-    extras = "c4,c5,c5_pipe,c4_pipe,c4_named,c3_pipe,c3_a2a,c3_fused,c4_torch,c5_torch"
+    extras = "c4,c5,c5_pipe,c5_overlap,c4_pipe,c4_named,c3_pipe,c3_a2a,c3_fused,c4_torch,c5_torch"
     argv = ["--rehearse-exchange", "--steps", "3", "--warmup", "1", "--elems", str(4 << 20),
             "--extras", extras, "--extras-timeout", "200"]
     code = _BRANCH_CHILD % (ROOT, os.path.join(ROOT, "tests"), argv)

@@ -218,6 +218,26 @@ def body_sma(rank, world, use_gpu):
         assert_within(p.detach(), want, sma_bound(ab, alpha, before[j], avg), "sma %d" % j)
 
 
+def body_sma_overlap(rank, world, use_gpu):
+    """SMA with overlap=True (the next step's sum started at the end of
+    step()) gives the same parameters, bit for bit, as overlap=False, over
+    three SGD steps from replicas that start different."""
+    from kungfu_amd.collective import Exchange
+    from kungfu_amd.optimizers import SynchronousAveragingOptimizer
+    ms = [_model(seed=rank), _model(seed=rank)]
+    opts = [SynchronousAveragingOptimizer(torch.optim.SGD(m.parameters(), lr=0.1), alpha=0.1,
+                                          exchange=Exchange(epilogue=_epilogue(use_gpu)),
+                                          overlap=ov)
+            for m, ov in zip(ms, (False, True))]
+    for step in range(3):
+        for m, opt in zip(ms, opts):
+            opt.zero_grad()
+            _loss(m, rank + 10 * step).backward()
+            opt.step()
+        for a, b in zip(ms[0].parameters(), ms[1].parameters()):
+            assert torch.equal(a.detach(), b.detach()), step
+
+
 # ---- tests -------------------------------------------------------------------
 
 @pytest.mark.parametrize("world", [2, 3])
@@ -242,6 +262,11 @@ def test_sync_sgd_optimizer(world):
 @pytest.mark.parametrize("world", [2, 3])
 def test_sma_optimizer(world):
     run_world("body_sma", world)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_sma_optimizer_overlap_same_bits(world):
+    run_world("body_sma_overlap", world)
 
 
 def test_world1_identity():

@@ -374,6 +374,50 @@ def test_scheduler_orders_across_ranks(world):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_sma_overlap_native_same_bits(world):
+    """SynchronousAveragingOptimizer(overlap=True) over the native exchange
+    (loopback ranks; the next step's sum on the exchange's stream, then the
+    batched HIP blend) equals overlap=False (kf_exchange_sma_batch) bit for
+    bit, f32 and bf16, over three SGD steps from different replicas."""
+    import torch
+    from kungfu_amd.optimizers import SynchronousAveragingOptimizer
+    dev = _gpu()
+
+    def model(seed, dtype):
+        g = torch.Generator(device=dev).manual_seed(seed)
+        m = torch.nn.Sequential(torch.nn.Linear(33, 65), torch.nn.Tanh(),
+                                torch.nn.Linear(65, 7)).to(dev)
+        with torch.no_grad():
+            for p in m.parameters():
+                p.copy_(torch.randn(p.shape, device=dev, generator=g) * 0.1)
+        return m.to(dtype)
+
+    def body(rank, ex):
+        for dtype in (torch.float32, torch.bfloat16):
+            ms = [model(rank, dtype), model(rank, dtype)]
+            opts = [SynchronousAveragingOptimizer(torch.optim.SGD(m.parameters(), lr=0.1),
+                                                  alpha=0.1, exchange=ex, overlap=ov)
+                    for m, ov in zip(ms, (False, True))]
+            for step in range(3):
+                for m, opt in zip(ms, opts):
+                    g = torch.Generator(device=dev).manual_seed(100 * step + rank)
+                    x = torch.randn(16, 33, device=dev, generator=g).to(dtype)
+                    opt.zero_grad()
+                    (m(x).float() ** 2).mean().backward()
+                    opt.step()
+                torch.cuda.synchronize()
+                for a, b in zip(ms[0].parameters(), ms[1].parameters()):
+                    assert torch.equal(a.detach(), b.detach()), (dtype, step)
+
+    if world == 1:
+        from kungfu_amd.exchange import NativeExchange
+        body(0, NativeExchange())
+    else:
+        _loop_ranks(world, body)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("world", [2, 3])
 def test_optimizers_over_native_exchange(world):
     """SynchronousSGDOptimizer / SynchronousAveragingOptimizer with
