@@ -1334,6 +1334,9 @@ class _AlgoView:
     def sma_(self, *a, **kw):
         return self._run(self.ex.sma_, *a, **kw)
 
+    def start_(self, *a, **kw):  # issued inside the call: the algo applies
+        return self._run(self.ex.start_, *a, **kw)
+
 
 def bench_c3_native(world, rank, dev, steps, warmup, n, x, algo, nb, fused=False, pipe=False):
     """C3 through the native exchange with another algo or layout: "a2a" =
