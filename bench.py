@@ -82,7 +82,7 @@ def parse():
                     help="rehearsal only: put every rank on this GPU")
     ap.add_argument("--no-extra", action="store_true",
                     help="N>1: skip the C4/C5/P2P sub-benchmarks")
-    ap.add_argument("--extras", default="c4,c5,c5_pipe,c5_overlap,c4_pipe,c4_named,c3_pipe,c3_a2a,c3_fused,c3_torch_fused,c3_per_bucket,c4_torch,"
+    ap.add_argument("--extras", default="c4,c5,c5_pipe,c5_overlap,c4_overlap,c4_pipe,c4_named,c3_pipe,c3_a2a,c3_fused,c3_torch_fused,c3_per_bucket,c4_torch,"
                                         "c5_torch,c3_ar,c3_p2p,c3_p2p_push,c3_p2p_hostbar,"
                                         "c4_p2p,c5_p2p",
                     help="N>1: which sub-benchmarks to run (comma list)")
@@ -880,6 +880,7 @@ def main():
                  ("c5_pipe", lambda: bench_c5(world, rank, dev, steps_x, 5,
                                               exchange="native_pipe")),
                  ("c5_overlap", lambda: bench_c5_overlap(world, rank, dev, min(steps_x, 20), 3)),
+                 ("c4_overlap", lambda: bench_c4_overlap(world, rank, dev, min(steps_x, 20), 3)),
                  ("c4_pipe", lambda: bench_c4(world, rank, dev, steps_x, 5,
                                               exchange="native_pipe")),
                  ("c3_pipe", lambda: bench_c3_native(world, rank, dev, steps_x, 5, n, x, "rs",
@@ -1660,6 +1661,82 @@ def bench_c5(world, rank, dev, steps, warmup, alpha=0.1, exchange="native"):
                       "+ blend"}
 
 
+def _gemm_standin(dev, world, t_target):
+    """A stand-in for a training step's compute: bf16 GEMMs of 4096^3 on the
+    current stream, as many as take about t_target seconds (at least one).
+    Returns (run(k), k, n): run(k) queues k of them."""
+    n = 4096
+    a = torch.randn(n, n, device=dev, dtype=torch.bfloat16)
+    w = torch.randn(n, n, device=dev, dtype=torch.bfloat16) / n
+    t_mm = _timed(lambda: torch.mm(a, w), 20, 3, dev, world)
+
+    def run(k):
+        x = a
+        for _ in range(k):
+            x = torch.mm(x, w)
+        return x
+    return run, max(1, int(round(t_target / t_mm))), n
+
+
+def bench_c4_overlap(world, rank, dev, steps, warmup):
+    """C4's S-SGD exchange overlapped with backward, as
+    SynchronousSGDOptimizer(overlap=True) runs it: a stand-in for backward
+    (bf16 GEMMs, about the exchange's own time in all) produces the 16
+    ResNet-50 buckets last to first, and each bucket's exchange starts on the
+    exchange's own stream as soon as its share of the compute is queued
+    (NativeExchange.start_); the step then waits for all. Against the serial
+    step (the whole compute, then one all_reduce_ of the 16 buckets)."""
+    from kungfu_amd import ops
+    from kungfu_amd.collective import GradBuckets
+    ex = _exchange("native")
+    sizes = _models()["resnet50-imagenet"]
+    gbs = [GradBuckets(sizes, torch.float32, dev, world, n_buckets=16) for _ in range(world)]
+    for r, gb in enumerate(gbs):
+        _fill(gb, 500 + r, dev, torch.float32)
+    mine = gbs[rank]
+    nb = len(mine.buckets)
+    want = [ops.bucket_reduce_avg([gb.buckets[i] for gb in gbs], world) for i in range(nb)]
+    absums = [sum(gb.buckets[i].abs() for gb in gbs) for i in range(nb)]
+
+    def start_all(work=None, k=0):
+        hs = []
+        for i in reversed(range(nb)):  # backward produces the last bucket first
+            if work is not None:
+                work(k * (i + 1) // nb - k * i // nb)
+            hs.append(ex.start_([mine.buckets[i]], average=True, coalesce=False, key=i))
+        for h in hs:
+            h.wait()
+
+    start_all()
+    ok = True
+    for b, w, ab, sp in zip(mine.buckets, want, absums, mine.spans):
+        ok &= (bool(torch.equal(b[:sp], w[:sp])) if world <= 2 else _within(b[:sp], w[:sp],
+                                                                          ab[:sp], world))
+    del want, absums
+    gbs.clear()
+    if not _agree(ok, dev):
+        return {"error": "overlapped C4 exchange failed its parity check"}
+    t_x = _timed(lambda: ex.all_reduce_(mine.buckets, average=True), steps, warmup, dev, world)
+    work, k, n = _gemm_standin(dev, world, t_x)
+    t_c = _timed(lambda: work(k), steps, warmup, dev, world)
+
+    def serial():
+        work(k)
+        ex.all_reduce_(mine.buckets, average=True)
+
+    t_s = _timed(serial, steps, warmup, dev, world)
+    t_o = _timed(lambda: start_all(work, k), steps, warmup, dev, world)
+    hidden = (t_s - t_o) / min(t_c, t_x) if min(t_c, t_x) > 0 else None
+    return {"workload": "C4: ResNet-50 grads in %d buckets, S-SGD, each bucket's exchange started "
+                        "as a backward stand-in (%d bf16 GEMMs of %d^3 in all) produces it "
+                        "(SynchronousSGDOptimizer(overlap=True)) vs serial" % (nb, k, n),
+            "exchange_ms": round(t_x * 1e3, 4), "compute_ms": round(t_c * 1e3, 4),
+            "serial_ms": round(t_s * 1e3, 4), "overlapped_ms": round(t_o * 1e3, 4),
+            "ms_per_step": round(t_o * 1e3, 4),
+            "hidden_frac": round(hidden, 3) if hidden is not None else None,
+            "parity": "N=2 bit-exact / N>2 order bound vs the rank-order average"}
+
+
 def bench_c5_overlap(world, rank, dev, steps, warmup, alpha=0.1):
     """C5's SMA exchange overlapped with compute, as
     SynchronousAveragingOptimizer(overlap=True) runs it: the sum of the
@@ -1697,17 +1774,10 @@ def bench_c5_overlap(world, rank, dev, steps, warmup, alpha=0.1):
     if not _agree(ok, dev):
         return {"error": "overlapped SMA differs from the synchronous sma_"}
     t_x = _timed(lambda: ex.sma_(mine.buckets, alpha), steps, warmup, dev, world)
-    n = 4096
-    a = torch.randn(n, n, device=dev, dtype=torch.bfloat16)
-    w = torch.randn(n, n, device=dev, dtype=torch.bfloat16) / n
-    t_mm = _timed(lambda: torch.mm(a, w), 20, 3, dev, world)
-    k = max(1, int(round(t_x / t_mm)))
+    work, k, n = _gemm_standin(dev, world, t_x)
 
     def compute():
-        x = a
-        for _ in range(k):
-            x = torch.mm(x, w)
-        return x
+        return work(k)
 
     t_c = _timed(compute, steps, warmup, dev, world)
 

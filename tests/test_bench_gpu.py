@@ -64,6 +64,7 @@ res = {
     "c5": bench.bench_c5(1, 0, dev, 3, 1, exchange="native"),
     "c5_pipe": bench.bench_c5(1, 0, dev, 3, 1, exchange="native_pipe"),
     "c5_overlap": bench.bench_c5_overlap(1, 0, dev, 3, 1),
+    "c4_overlap": bench.bench_c4_overlap(1, 0, dev, 3, 1),
     "c3_a2a": bench.bench_c3_native(1, 0, dev, 3, 1, n, x, "a2a", 64),
     "c3_fused": bench.bench_c3_native(1, 0, dev, 3, 1, n, x, "rs", 64, fused=True),
     "c3_pipe": bench.bench_c3_native(1, 0, dev, 3, 1, n, x, "rs", 64, pipe=True),
@@ -116,7 +117,7 @@ def test_bench_exchange_branch_single_rank_rccl():
         pytest.skip("no GPU")
     env = dict(os.environ, MASTER_ADDR="127.0.0.1",
                MASTER_PORT=str(_port()), RANK="0", LOCAL_RANK="0", WORLD_SIZE="1")
-    extras = "c4,c5,c5_pipe,c5_overlap,c4_pipe,c4_named,c3_pipe,c3_a2a,c3_fused,c4_torch,c5_torch"
+    extras = "c4,c5,c5_pipe,c5_overlap,c4_overlap,c4_pipe,c4_named,c3_pipe,c3_a2a,c3_fused,c4_torch,c5_torch"
     argv = ["--rehearse-exchange", "--steps", "3", "--warmup", "1", "--elems", str(4 << 20),
             "--extras", extras, "--extras-timeout", "200"]
     code = _BRANCH_CHILD % (ROOT, os.path.join(ROOT, "tests"), argv)
