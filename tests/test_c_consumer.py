@@ -158,3 +158,24 @@ def test_cpp_hier_all_reduce_on_gpu(hier_binary):
     r = subprocess.run([hier_binary] + _hier_args(), capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "hier ok" in r.stdout
+
+
+@pytest.fixture(scope="module")
+def session_async_binary(tmp_path_factory):
+    """tests/c/test_session_async.cpp: host-mode sessions as threads of one C++
+    process, async all-reduces started in a different order on every rank."""
+    out = str(tmp_path_factory.mktemp("cs") / "test_session_async")
+    lib = os.path.join(ROOT, "kungfu_amd")
+    subprocess.run(["g++", "-std=c++17", "-O1", "-Wall", "-Wextra", "-Werror",
+                    "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "c", "test_session_async.cpp"),
+                    "-L", lib, "-lkungfu_amd", "-Wl,-rpath," + lib, "-lpthread", "-o", out],
+                   check=True)
+    return out
+
+
+@pytest.mark.parametrize("np_", [2, 3, 4])
+def test_c_session_async_any_order(session_async_binary, tmp_path, np_):
+    r = subprocess.run([session_async_binary, str(np_), "2", str(tmp_path)],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "OK" in r.stdout, r.stdout + r.stderr
