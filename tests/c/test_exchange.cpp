@@ -174,6 +174,7 @@ int multi_rank_named(int world)
 
 int main()
 {
+    std::setvbuf(stdout, nullptr, _IOLBF, 0);  // lines survive an abort at exit
     if (kf_device_count() < 1) {
         std::printf("no device: build checked only\n");
         return 77;

@@ -161,6 +161,7 @@ int run_layout(const std::vector<std::vector<int>> &hosts, int base_port, const 
 
 int main(int argc, char **argv)
 {
+    std::setvbuf(stdout, nullptr, _IOLBF, 0);  // lines survive an abort at exit
     if (argc < 3) {
         std::fprintf(stderr, "usage: test_hier <base_port> <sock_dir>\n");
         return 2;

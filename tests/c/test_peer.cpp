@@ -86,6 +86,7 @@ int test_AllReduce(Peer &world, int np, bool device)
 
 int main(int argc, char **argv)
 {
+    std::setvbuf(stdout, nullptr, _IOLBF, 0);  // lines survive an abort at exit
     if (argc < 4) {
         Peer kf;
         if (kf.Rank() != 0 || kf.Size() != 1) return 1;

@@ -1,0 +1,74 @@
+#!/usr/bin/env bash
+# AddressSanitizer on the HOST code of the C++ hosts that drive the GPU: the
+# exchange (world 1 on librccl, three loopback ranks incl. the name-keyed
+# negotiation), the hierarchical all-reduce (device-mode sessions across
+# emulated hosts) and the Peer facade over device-mode sessions (np 2-4).
+# Device code is not instrumented (-Xarch_host only; GPU ASan is not
+# available on this pool).
+#   bash tools/sanitize_gpu_hosts.sh build     # here, on the CPU
+#   bash tools/sanitize_gpu_hosts.sh run       # on the GPU box
+set -eu
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+D="$ROOT/tools/san_build"
+INC="-I$ROOT/include -I$ROOT/tests/c -I/opt/rocm/include"
+HIPL="-L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib"
+case "${1:-}" in
+build)
+    mkdir -p "$D"
+    SRC="$ROOT/kungfu_amd/csrc"
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O1 -g -std=c++17 -fPIC -shared -ffp-contract=off \
+        -fvisibility=hidden -Xarch_host -fsanitize=address -Wl,-soname,libkungfu_amd.so \
+        -I"$ROOT/include" -o "$D/libkungfu_amd.so" \
+        $SRC/kf_capi.hip $SRC/kf_ingest.hip $SRC/kf_session.hip $SRC/kf_p2p.hip $SRC/kf_exchange.hip -ldl
+    CXX="/opt/rocm/lib/llvm/bin/clang++ -std=c++17 -O1 -g -fsanitize=address -D__HIP_PLATFORM_AMD__"
+    $CXX -fPIC -shared $INC -o "$D/libkf_testing.so" "$ROOT/tests/c/kf_testing.cpp" \
+        -L"$D" -lkungfu_amd -Wl,-rpath,'$ORIGIN' $HIPL -ldl -lpthread
+    for t in test_exchange test_hier test_peer; do
+        $CXX $INC -o "$D/$t" "$ROOT/tests/c/$t.cpp" -L"$D" -lkungfu_amd -lkf_testing \
+            -Wl,-rpath,'$ORIGIN' $HIPL -lpthread
+    done
+    echo "built $D"
+    ;;
+run)
+    # A host passes when it printed its ok line and ASan reported no error.
+    # ASan's device-allocator CHECK ("dev_runtime_unloaded_") can fire inside
+    # the ROCm runtime's own teardown in __cxa_finalize, after main returned;
+    # that is recorded (the exit status is printed) but is not a report about
+    # this code.
+    export ASAN_OPTIONS="detect_leaks=0 halt_on_error=1 protect_shadow_gap=0"
+    cd "$D"
+    check() {  # check <log> <ok-pattern> <status>
+        cat "$1"
+        echo "   exit status $3"
+        case $3 in 124|134|137|139) echo "stopping: abort, fault or time limit"; exit 1 ;; esac
+        if grep -q "ERROR: AddressSanitizer" "$1"; then echo "ASAN ERROR"; exit 1; fi
+        grep -q "$2" "$1" || { echo "no '$2' line"; exit 1; }
+    }
+    L=$(mktemp)
+    echo "== test_exchange"
+    st=0; timeout -k 10 240 ./test_exchange > "$L" 2>&1 || st=$?
+    check "$L" "exchange ok" $st
+    echo "== test_hier"
+    P=$((20000 + RANDOM % 20000))
+    H=$(mktemp -d)
+    st=0; timeout -k 10 240 ./test_hier $P "$H" > "$L" 2>&1 || st=$?
+    check "$L" "hier ok" $st
+    for np in 2 3 4; do
+        echo "== test_peer np=$np dev"
+        S=$(mktemp -d)
+        pids=""
+        for r in $(seq 0 $((np - 1))); do
+            timeout -k 10 120 ./test_peer $r $np "$S" dev > "$S/out.$r" 2>&1 &
+            pids="$pids $!"
+        done
+        st=0
+        for p in $pids; do wait $p || st=$?; done
+        for r in $(seq 0 $((np - 1))); do check "$S/out.$r" "peer ok" $st; done
+    done
+    echo "asan gpu hosts: no AddressSanitizer report"
+    ;;
+*)
+    echo "usage: $0 build|run" >&2
+    exit 2
+    ;;
+esac
