@@ -7,9 +7,12 @@
 # available on this pool).
 #   bash tools/sanitize_gpu_hosts.sh build     # here, on the CPU
 #   bash tools/sanitize_gpu_hosts.sh run       # on the GPU box
+# SAN=thread selects ThreadSanitizer instead (tools/san_build_thread/).
 set -eu
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
+SAN=${SAN:-address}
 D="$ROOT/tools/san_build"
+[ "$SAN" = address ] || D="$ROOT/tools/san_build_$SAN"
 INC="-I$ROOT/include -I$ROOT/tests/c -I/opt/rocm/include"
 HIPL="-L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib"
 case "${1:-}" in
@@ -17,10 +20,10 @@ build)
     mkdir -p "$D"
     SRC="$ROOT/kungfu_amd/csrc"
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O1 -g -std=c++17 -fPIC -shared -ffp-contract=off \
-        -fvisibility=hidden -Xarch_host -fsanitize=address -Wl,-soname,libkungfu_amd.so \
+        -fvisibility=hidden -Xarch_host -fsanitize=$SAN -Wl,-soname,libkungfu_amd.so \
         -I"$ROOT/include" -o "$D/libkungfu_amd.so" \
         $SRC/kf_capi.hip $SRC/kf_ingest.hip $SRC/kf_session.hip $SRC/kf_p2p.hip $SRC/kf_exchange.hip -ldl
-    CXX="/opt/rocm/lib/llvm/bin/clang++ -std=c++17 -O1 -g -fsanitize=address -D__HIP_PLATFORM_AMD__"
+    CXX="/opt/rocm/lib/llvm/bin/clang++ -std=c++17 -O1 -g -fsanitize=$SAN -D__HIP_PLATFORM_AMD__"
     $CXX -fPIC -shared $INC -o "$D/libkf_testing.so" "$ROOT/tests/c/kf_testing.cpp" \
         -L"$D" -lkungfu_amd -Wl,-rpath,'$ORIGIN' $HIPL -ldl -lpthread
     for t in test_exchange test_hier test_peer; do
@@ -36,12 +39,15 @@ run)
     # that is recorded (the exit status is printed) but is not a report about
     # this code.
     export ASAN_OPTIONS="detect_leaks=0 halt_on_error=1 protect_shadow_gap=0"
+    export TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1 suppressions=$ROOT/tools/tsan_rocm.supp"
     cd "$D"
     check() {  # check <log> <ok-pattern> <status>
         cat "$1"
         echo "   exit status $3"
         case $3 in 124|134|137|139) echo "stopping: abort, fault or time limit"; exit 1 ;; esac
-        if grep -q "ERROR: AddressSanitizer" "$1"; then echo "ASAN ERROR"; exit 1; fi
+        if grep -q "ERROR: AddressSanitizer\|WARNING: ThreadSanitizer" "$1"; then
+            echo "SANITIZER REPORT"; exit 1
+        fi
         grep -q "$2" "$1" || { echo "no '$2' line"; exit 1; }
     }
     L=$(mktemp)
@@ -65,7 +71,7 @@ run)
         for p in $pids; do wait $p || st=$?; done
         for r in $(seq 0 $((np - 1))); do check "$S/out.$r" "peer ok" $st; done
     done
-    echo "asan gpu hosts: no AddressSanitizer report"
+    echo "$SAN sanitizer, gpu hosts: no report"
     ;;
 *)
     echo "usage: $0 build|run" >&2
