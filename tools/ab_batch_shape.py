@@ -23,25 +23,31 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 OUT = os.path.join(ROOT, "tools", "ab_lib")
-SHAPES = [(4, 256), (2, 256), (1, 256), (2, 512), (1, 512), (1, 1024)]
+# variant name -> compile-time flags (kf_capi.hip / kf_reduce_kernels.hpp)
+VARIANTS = {"u%d_b%d" % (u, b): {"KF_BATCH_UNROLL": u, "KF_BATCH_UNROLL_K1": u, "KF_BATCH_BLOCK": b}
+            for u, b in [(4, 256), (2, 256), (1, 256), (2, 512), (1, 512), (1, 1024)]}
+# (round 3 also built a KF_FOLD_ALLIN variant of the runtime-k fold here —
+# every input's vectors in flight before the first add on resident grids —
+# equal within noise at every shape, profiles/r03/ab_fold_allin_r03u.jsonl;
+# the variant was not kept)
 F32, BF16, SUM = 0x20408, 0x20209, 0
 
 
-def lib_path(u, b):
-    return os.path.join(OUT, "libkf_batch_u%d_b%d.so" % (u, b))
+def lib_path(name):
+    return os.path.join(OUT, "libkf_ab_%s.so" % name)
 
 
 def build():
     os.makedirs(OUT, exist_ok=True)
     src = os.path.join(ROOT, "kungfu_amd", "csrc", "kf_capi.hip")
-    for u, b in SHAPES:
+    for name, flags in VARIANTS.items():
         cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
                "-shared", "-ffp-contract=off", "-fvisibility=hidden",
-               "-I" + os.path.join(ROOT, "include"), "-DKF_BATCH_UNROLL=%d" % u,
-               "-DKF_BATCH_UNROLL_K1=%d" % u,
-               "-DKF_BATCH_BLOCK=%d" % b, "-o", lib_path(u, b), src]
+               "-I" + os.path.join(ROOT, "include")]
+        cmd += ["-D%s=%d" % kv for kv in flags.items()]
+        cmd += ["-o", lib_path(name), src]
         subprocess.run(cmd, check=True)
-        print("built", lib_path(u, b), flush=True)
+        print("built", lib_path(name), flush=True)
 
 
 def run():
@@ -54,11 +60,14 @@ def run():
     argt = [ctypes.POINTER(vp), ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_size_t),
             ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp]
     libs = {}
-    for u, b in SHAPES:
-        lib = ctypes.CDLL(lib_path(u, b), mode=ctypes.RTLD_LOCAL)
+    for name in VARIANTS:
+        lib = ctypes.CDLL(lib_path(name), mode=ctypes.RTLD_LOCAL)
         lib.kf_bucket_reduce_batch.argtypes = argt
         lib.kf_bucket_reduce_batch.restype = ctypes.c_int
-        libs["u%d_b%d" % (u, b)] = lib
+        lib.kf_bucket_reduce.argtypes = [ctypes.POINTER(vp), ctypes.c_int, vp, ctypes.c_size_t,
+                                         ctypes.c_int, ctypes.c_int, vp]
+        lib.kf_bucket_reduce.restype = ctypes.c_int
+        libs[name] = lib
     libs["shipped"] = ship
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(5)
@@ -125,6 +134,20 @@ def run():
         nsb, lambda lib, i: lib.kf_bucket_reduce_batch(sb[i][0], 2, sb[i][1], sb[i][2], nb, F32,
                                                        SUM, 0, sp), 12 * n * nb,
         lambda i: torch.cat(sb[i][4]).clone(), None)
+
+    # the star root's k-input fold of 1 MiB chunks and of 4 MiB buckets
+    # (kf_bucket_reduce, resident grids), k = 4 and 8
+    for k, n in ((4, 1 << 18), (8, 1 << 18), (8, 1 << 20)):
+        ns = max(2, -(-(768 << 20) // ((k + 1) * n * 4)))
+        fs = []
+        for _ in range(ns):
+            xs = [torch.randn(n, device=dev, generator=g) for _ in range(k)]
+            z = torch.empty(n, device=dev)
+            fs.append((_lib.ptr_array([x.data_ptr() for x in xs]), z, xs))
+        cases["fold_k%d_%dKiB_f32" % (k, n * 4 >> 10)] = (
+            ns, lambda lib, i, fs=fs, k=k, n=n: lib.kf_bucket_reduce(fs[i][0], k, fs[i][1].data_ptr(),
+                                                                     n, F32, SUM, sp),
+            (k + 1) * n * 4, lambda i, fs=fs: fs[i][1].clone(), None)
 
     # bits: every variant equals the shipped library on set 0
     ok = {}
