@@ -92,6 +92,10 @@ def parse():
     ap.add_argument("--native-timeout", type=float, default=120.0,
                     help="N>1: seconds for the native exchange's communicator to come up "
                          "before the torch.distributed path is used instead")
+    ap.add_argument("--c3-schedule", default="auto",
+                    choices=["auto", "grouped", "fused", "a2a", "pipelined"],
+                    help="N>1, native exchange: the C3 schedule timed as `value` (auto: "
+                         "the fastest of a short parity-checked trial of all four)")
     ap.add_argument("--no-c1", action="store_true",
                     help="N=1: skip the C1 (np=2 localhost) sub-object")
     ap.add_argument("--config", default="default", choices=["default", "c1"],
@@ -845,6 +849,41 @@ def main():
             fallback = "native exchange failed the C3 parity check; torch path used"
             gb.views[0].copy_(x)
             ok = parity()
+        trial = None
+        if ok and fallback is None and args.c3_schedule != "grouped":
+            # the native exchange's schedules for the same S-SGD step, each
+            # parity-checked, timed briefly on every rank (max over ranks, so
+            # every rank picks the same), the fastest kept for the timed
+            # region; all of them are in the line (collective.schedule_trial_ms)
+            cands = {
+                "grouped": (prim_ex, False, how),
+                "fused": (prim_ex, True, "native C-ABI exchange: the %d contiguous buckets as ONE "
+                          "RCCL reduce-scatter -> HIP /np -> RCCL all-gather (the reference's "
+                          "nccl_fusion, sync_sgd.py:87-92)" % len(pieces)),
+                "a2a": (_AlgoView(prim_ex, "a2a"), False, "native C-ABI exchange: per bucket RCCL "
+                        "all-to-all -> HIP rank-order fold with /np -> RCCL all-gather, the "
+                        "buckets of a step in one call"),
+                "pipelined": (_AlgoView(prim_ex, "rs", PIPE_GROUPS), False,
+                              "native C-ABI exchange: per bucket RCCL reduce-scatter -> HIP /np "
+                              "-> RCCL all-gather, pipelined in %d groups (HIP /np on a second "
+                              "stream between the groups' collectives)" % PIPE_GROUPS),
+            }
+            if args.c3_schedule != "auto":
+                cands = {args.c3_schedule: cands[args.c3_schedule]}
+            trial = {}
+            for name, (ex_c, co_c, _) in cands.items():
+                prim_ex, coalesce = ex_c, co_c
+                gb.views[0].copy_(x)
+                if name != "grouped" and not parity():
+                    trial[name] = None
+                    continue
+                gb.views[0].copy_(x)
+                trial[name] = _timed(lambda: ex_c.all_reduce_(pieces, average=True,
+                                                              coalesce=co_c), 10, 3, dev, world)
+            best = min((t, nm) for nm, t in trial.items() if t is not None)[1]
+            prim_ex, coalesce, how = cands[best]
+            _progress(rank, "C3 schedule %s (trial ms %s)" % (
+                best, {k: None if v is None else round(v * 1e3, 3) for k, v in trial.items()}))
         del want, absum
         if not ok:
             raise SystemExit("C3 all-reduce parity check failed (N=2 bit-exact / N>2 bound)")
@@ -864,6 +903,9 @@ def main():
             "buckets": args.buckets,
             "exchange": how,
         }
+        if trial is not None:
+            out["collective"]["schedule_trial_ms"] = {
+                k: None if v is None else round(v * 1e3, 4) for k, v in trial.items()}
         if fallback is not None:
             out["collective"]["native_exchange_error"] = fallback
         workload = ("C3: S-SGD all-reduce of %d fp32 buckets (%d MiB) per rank: %s"

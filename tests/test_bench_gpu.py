@@ -131,6 +131,10 @@ def test_bench_exchange_branch_single_rank_rccl():
         json.dumps(d["collective"]) + r.stderr[-3000:]
     assert "native_exchange_error" not in d["collective"], d["collective"]
     assert d["value"] == d["collective"]["algbw_GiBps_per_gpu"]
+    # the primary's schedule trial: every schedule parity-checked and timed
+    trial = d["collective"]["schedule_trial_ms"]
+    assert sorted(trial) == ["a2a", "fused", "grouped", "pipelined"], trial
+    assert all(v is not None and v > 0 for v in trial.values()), trial
     assert abs(d["value_aggregate"] - d["n_gpus"] * d["value"]) < 1e-2
     for k in extras.split(","):
         assert "error" not in d[k] and d[k]["ms_per_step"] > 0, (k, d[k])
