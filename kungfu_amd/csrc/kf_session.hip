@@ -59,6 +59,7 @@
 #include <string>
 #include <thread>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "kungfu_amd.h"
@@ -1317,14 +1318,14 @@ int kf_session::run(SessOp *one)
             std::vector<SessOp *> fresh;
             {
                 std::lock_guard<std::mutex> l(amu);
-                std::vector<std::string> busy;
-                for (SessOp *o : active) busy.push_back(o->name);
+                std::unordered_set<std::string> busy;
+                for (SessOp *o : active) busy.insert(o->name);
                 for (auto it = aq.begin(); it != aq.end();) {
-                    if (std::find(busy.begin(), busy.end(), (*it)->name) != busy.end()) {
+                    if (busy.count((*it)->name)) {
                         ++it;
                         continue;
                     }
-                    busy.push_back((*it)->name);
+                    busy.insert((*it)->name);
                     fresh.push_back(*it);
                     it = aq.erase(it);
                 }
