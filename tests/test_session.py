@@ -426,7 +426,7 @@ def test_session_async_device():
     _run_async(3, "device")
 
 
-def _any_order_body(rank, size, sock_dir, mode, strategy, errq):
+def _any_order_body(rank, size, sock_dir, mode, strategy, errq, steps=2):
     """Every peer starts the same named all-reduces in its OWN random order,
     two steps of them back to back (a name's second call waits for its
     first; the peers' step-2 chunks wait in the stash meanwhile), as the
@@ -449,7 +449,7 @@ def _any_order_body(rank, size, sock_dir, mode, strategy, errq):
         else:
             s = Session(rank, size, sock_dir, mode="host", host_reduce_fn=oracle_reduce_fn())
         hs = []
-        for step in range(2):  # step 2 starts while step 1 may be in flight
+        for step in range(steps):  # step t+1 starts while step t may be in flight
             for j in rng.permutation(len(specs)):
                 name, kind, n = specs[j]
                 x = inputs(rank, n, kind) * (step + 1)
@@ -475,11 +475,11 @@ def _any_order_body(rank, size, sock_dir, mode, strategy, errq):
         errq.put("rank %d: %s" % (rank, traceback.format_exc()))
 
 
-def _run_any_order(size, mode, strategy=None):
+def _run_any_order(size, mode, strategy=None, steps=2):
     ctx = mp.get_context("spawn")
     errq = ctx.SimpleQueue()
     with tempfile.TemporaryDirectory() as d:
-        ps = [ctx.Process(target=_any_order_body, args=(r, size, d, mode, strategy, errq))
+        ps = [ctx.Process(target=_any_order_body, args=(r, size, d, mode, strategy, errq, steps))
               for r in range(size)]
         for p in ps:
             p.start()
