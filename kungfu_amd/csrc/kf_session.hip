@@ -1396,15 +1396,18 @@ int kf_session::run(SessOp *one)
             cv_idle.wait(l, [&] { return one->sends == 0; });
             continue;
         }
-        if (::poll(pfds.data(), pfds.size(), -1) < 0) {
-            if (errno == EINTR) continue;
-            fail_all(fail(KF_ERR_IO, std::string("poll: ") + strerror(errno)));
-            continue;
-        }
+        // checked before polling: a peer seen closing while an earlier call
+        // was in flight is no longer polled, and a call started after that
+        // would otherwise wait for a message that cannot come
         size_t open_fds = 0;
         for (size_t q = 0; q < pfds.size(); ++q) open_fds += pfds[q].fd >= 0 && pfd_peer[q] >= 0;
         if (open_fds == 0 && waiting_rx) {
             fail_all(fail(KF_ERR_IO, "every peer connection closed before the all-reduce finished"));
+            continue;
+        }
+        if (::poll(pfds.data(), pfds.size(), -1) < 0) {
+            if (errno == EINTR) continue;
+            fail_all(fail(KF_ERR_IO, std::string("poll: ") + strerror(errno)));
             continue;
         }
         int rc  = KF_OK;

@@ -532,6 +532,14 @@ def _dead_peer_body(rank, sock_dir, errq):
             assert "closed" in str(e) or "KF_ERR_IO" in str(e), e
         assert len(got) == 2 and all(st != 0 for st in got), got
         assert all(h.done() for h in hs)
+        # started after the peer was seen gone: fails at once too
+        h = s.all_reduce_async(xs[0], np.zeros_like(xs[0]), "dead/late")
+        try:
+            s.wait_all()
+            raise AssertionError("a call started after the peer left succeeded")
+        except RuntimeError:
+            pass
+        assert h.done() and h.status != 0
         s.close()
     except Exception:
         errq.put("rank %d: %s" % (rank, traceback.format_exc()))
