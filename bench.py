@@ -1380,6 +1380,9 @@ class _AlgoView:
     def start_(self, *a, **kw):  # issued inside the call: the algo applies
         return self._run(self.ex.start_, *a, **kw)
 
+    def start_into_(self, *a, **kw):
+        return self._run(self.ex.start_into_, *a, **kw)
+
 
 def bench_c3_native(world, rank, dev, steps, warmup, n, x, algo, nb, fused=False, pipe=False):
     """C3 through the native exchange with another algo or layout: "a2a" =
@@ -1782,8 +1785,8 @@ def bench_c4_overlap(world, rank, dev, steps, warmup):
 def bench_c5_overlap(world, rank, dev, steps, warmup, alpha=0.1):
     """C5's SMA exchange overlapped with compute, as
     SynchronousAveragingOptimizer(overlap=True) runs it: the sum of the
-    variables starts on the exchange's own stream (NativeExchange.start_ on a
-    copy), a stand-in for the step's forward and backward (bf16 GEMMs sized
+    variables starts on the exchange's own stream (NativeExchange.start_into_,
+    out of place), a stand-in for the step's forward and backward (bf16 GEMMs sized
     to about the exchange's own time) runs on the current stream meanwhile,
     then the step waits and blends (the batched HIP kernel). Against the
     serial step (compute, then the synchronous sma_). Checked first: the
@@ -1797,10 +1800,8 @@ def bench_c5_overlap(world, rank, dev, steps, warmup, alpha=0.1):
     sums = [torch.empty_like(b) for b in mine.buckets]
     v0 = [b.clone() for b in mine.buckets]
 
-    def start():
-        for s, b in zip(sums, mine.buckets):
-            s.copy_(b)
-        return ex.start_(sums, op="sum", average=False, coalesce=False, key="c5o")
+    def start():  # out of place, as the optimizer does on the native exchange
+        return ex.start_into_(mine.buckets, sums, op="sum")
 
     def finish(h):
         h.wait()

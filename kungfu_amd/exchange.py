@@ -124,13 +124,14 @@ class NativeExchange:
             if b.dtype != buckets[0].dtype:
                 raise ValueError("one dtype per call")
 
-    def _issue(self, buckets, op, average, stream):
+    def _issue(self, buckets, op, average, stream, recvs=None):
         red = OP_NAMES[op] if isinstance(op, str) else OP(op)
         if average and red != OP.SUM:
             raise ValueError("average requires op='sum'")
         ptrs = [b.data_ptr() for b in buckets]
+        rptrs = ptrs if recvs is None else [r.data_ptr() for r in recvs]
         rc = self.lib.kf_exchange_all_reduce_batch(
-            self._h, _lib.ptr_array(ptrs), _lib.ptr_array(ptrs),
+            self._h, _lib.ptr_array(ptrs), _lib.ptr_array(rptrs),
             _arr(ctypes.c_size_t, [b.numel() for b in buckets]), len(buckets),
             int(kungfu_dtype(buckets[0])), int(red), 1 if average else 0, ALGOS[self.algo],
             stream.cuda_stream)
@@ -164,6 +165,28 @@ class NativeExchange:
         ev = torch.cuda.Event()
         ev.record(self._side)
         for b in buckets:
+            b.record_stream(self._side)
+        return _Handle(ev, self.device)
+
+    def start_into_(self, sends, recvs, op="sum", average=False):
+        """start_ out of place: recvs[i] <- all-reduce(sends[i]), on the
+        exchange's stream after the current one's queued work; sends are only
+        read. (SMA's overlapped sum: the variables stay where they are, no copy
+        of them is made first.)"""
+        sends, recvs = list(sends), list(recvs)
+        self._check(sends)
+        self._check(recvs)
+        if len(sends) != len(recvs) or any(a.numel() != b.numel() or a.dtype != b.dtype
+                                           for a, b in zip(sends, recvs)):
+            raise ValueError("sends and recvs must pair up in size and dtype")
+        if self._side is None:
+            self._side = torch.cuda.Stream(self.device)
+        cur = torch.cuda.current_stream(self.device)
+        self._side.wait_stream(cur)
+        self._issue(sends, op, average, self._side, recvs=recvs)
+        ev = torch.cuda.Event()
+        ev.record(self._side)
+        for b in sends + recvs:
             b.record_stream(self._side)
         return _Handle(ev, self.device)
 

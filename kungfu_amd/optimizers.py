@@ -211,8 +211,9 @@ class _SMA(_Bucketed):
     # before the blend and the gradient update), and they do not change
     # between the end of step t-1 and the blend of step t, so the sum can
     # start as soon as step t-1 has updated them — on the exchange's own
-    # stream, into a workspace per bucket — and step t only waits for it and
-    # blends. The collectives and the blend kernel are those of sma_(), so the
+    # stream, into a workspace per bucket (out of place on the native
+    # exchange; a copy, then in place, on collective.Exchange) — and step t
+    # only waits for it and blends. The collectives and the blend kernel are those of sma_(), so the
     # result is the same bit for bit.
     def _kf_start_sums(self):
         if self._kf_sums is None:
@@ -220,7 +221,11 @@ class _SMA(_Bucketed):
             self._kf_sums = [[torch.empty_like(b) for b in gb.buckets]
                              for _, gb in self._kf_groups]
         self._kf_pending = []
+        into = getattr(self._kf_ex, "start_into_", None)
         for gi, ((_, gb), sums) in enumerate(zip(self._kf_groups, self._kf_sums)):
+            if into is not None:  # the native exchange: out of place, no copy
+                self._kf_pending.append(into(gb.buckets, sums, op="sum"))
+                continue
             for s, b in zip(sums, gb.buckets):
                 s.copy_(b)
             self._kf_pending.append(self._kf_ex.start_(sums, op="sum", average=False,
