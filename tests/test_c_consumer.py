@@ -140,7 +140,7 @@ def _hier_args():
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    return [str(20000 + port % 20000), tempfile.mkdtemp(prefix="kfh")]
+    return [str(20000 + port % 12000), tempfile.mkdtemp(prefix="kfh")]  # below the ephemeral range
 
 
 def test_cpp_hier_host_builds(hier_binary):

@@ -109,7 +109,7 @@ def _body(rank, peers, port, sock_dir, errq, use_gpu):
 
 
 def _run(hosts_sizes, use_gpu=False):
-    peers = _peers(hosts_sizes, random.Random().randrange(20000, 60000, 16))
+    peers = _peers(hosts_sizes, random.Random().randrange(20000, 32000, 16))  # below the ephemeral range (32768+), where gloo's own connections live
     ctx = mp.get_context("spawn")
     errq = ctx.SimpleQueue()
     port = _free_port()
@@ -193,7 +193,7 @@ def test_native_hierarchical_threads_two_hosts_two_ranks():
     from oracle import oracle
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
-    base = 20000 + s.getsockname()[1] % 20000
+    base = 20000 + s.getsockname()[1] % 12000  # below the ephemeral range (32768+)
     s.close()
     hosts = [[0, 1], [2, 3]]
     peers = ["127.0.0.%d:%d" % (h + 1, base + g) for h, hs in enumerate(hosts) for g in hs]

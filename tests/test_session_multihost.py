@@ -91,7 +91,7 @@ def check(peers, kind, n, strategy, got):
 
 
 def run(hosts_sizes, kind, n, strategy, mode="host"):
-    peers = layout(hosts_sizes, random.Random().randrange(20000, 60000, 16))
+    peers = layout(hosts_sizes, random.Random().randrange(20000, 32000, 16))  # below the ephemeral range (32768+), where gloo's own connections live
     ctx = mp.get_context("spawn")
     errq = ctx.SimpleQueue()
     with tempfile.TemporaryDirectory() as d:
