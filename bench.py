@@ -3,7 +3,8 @@
 per GPU; % of HBM3E peak".
 
   python bench.py [--gpus N --steps K --warmup W]
-  (N > 1: launched by torch.distributed.run, one rank per GPU)
+  (N > 1: one rank per GPU under torch.distributed.run; without a launcher
+  around it, bench.py starts that launcher itself as a child)
 
 N = 1 (BASELINE.json configs[1], C2): one step = one launch of the HIP bucket
 reduce z = x + y over a device-resident 256 MiB fp32 bucket (67,108,864
@@ -30,7 +31,8 @@ sources by `make -C oracle ref` (kind "reference"; built by __graft_entry__
 .build() where /root/reference exists, shipped as oracle/_ref/*.so), or the
 oracle's bit-exact restatement with the same -O2 -mavx -mf16c flags (kind
 "port") when that build is absent; 1 thread on the same 256 MiB sum repeated
-for about --cpu-seconds, plus 1 MiB chunks on up to 16 threads; rank 0 at
+for about --cpu-seconds, plus 1 MiB chunks on every core of the GPU's
+NUMA node (GOMAXPROCS); rank 0 at
 N = 1 only.
 """
 import argparse
@@ -435,19 +437,47 @@ def cpu_baseline(x, y, seconds):
                     break
     except OSError:
         pass
-    nt = min(16, os.cpu_count() or 1)
-    tm1 = run(2, nt) / 2
-    mreps = max(1, min(1000, int(seconds / 2 / max(tm1, 1e-6))))
-    tm = run(mreps, nt)
+    # the reference's fan-out: one goroutine per 1 MiB chunk, run by
+    # GOMAXPROCS threads, which Go sets to the CPUs the process may use
+    # (runtime.NumCPU = the affinity mask); also at the GPU's NUMA node and
+    # at 16 threads (the box's nominal CPU share), so the curve is visible
+    gomaxprocs = len(os.sched_getaffinity(0))
+    numa = gpu_local_cpus()
+    legs = {"gomaxprocs": gomaxprocs, "numa_node": len(numa) if numa else None,
+            "16": min(16, gomaxprocs)}
+    by_threads = {}
+    for key, nt in legs.items():
+        if nt is None or nt < 2:
+            continue
+        nt = min(nt, 1024)  # the harness's pool limit (oracle/kf_oracle.c MAX_POOL)
+        tm1 = run(2, nt) / 2
+        mreps = max(2, min(1000, int(seconds / 3 / max(tm1, 1e-6))))
+        tm = run(mreps, nt)
+        by_threads[key] = {"threads": nt, "value": round(mreps * s_bytes / tm / 2**30, 3),
+                           "seconds": round(tm, 2), "reps": mreps}
+    top = by_threads.get("gomaxprocs") or next(iter(by_threads.values()), None)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()
+            quota = None if q == "max" else round(int(q) / int(p), 2)
+    except (OSError, ValueError):
+        pass
+    multi = None
+    if top is not None:
+        multi = {"value": top["value"], "unit": "GiB/s", "cores": top["threads"],
+                 "sample": "%d x 256 MiB in 1 MiB chunks, one pool of %d threads taking the "
+                           "chunks of every rep in turn (GOMAXPROCS = the %d CPUs of the "
+                           "affinity mask), %.1f s" % (top["reps"], top["threads"],
+                                                       gomaxprocs, top["seconds"]),
+                 "by_threads": by_threads, "cgroup_cpu_quota": quota}
     return {
         "value": round(reps * s_bytes / t / 2**30, 3),
         "unit": "GiB/s",
         "cores": 1,
         "kind": kind,
         "correct": ok,
-        "multi_thread": {"value": round(mreps * s_bytes / tm / 2**30, 3), "unit": "GiB/s",
-                         "cores": nt, "sample": "%d x 256 MiB in 1 MiB chunks on %d threads, "
-                                                "%.1f s" % (mreps, nt, tm)},
+        "multi_thread": multi,
         "sample": "%d x std_transform_2(f32, SUM) over the same 256 MiB bucket, 1 thread, "
                   "%s, %.1f s, %s" % (reps, what, t, cpu_model),
     }
@@ -746,6 +776,27 @@ def c1_parent(args):
     print(json.dumps(line), flush=True)
 
 
+def launch_ranks(args):
+    """`bench.py --gpus N` (N > 1) with no launcher around it: start the N
+    ranks as ONE child, `torch.distributed.run --nproc-per-node N` on
+    127.0.0.1, the way the reference's `kungfu-run -np N`
+    (srcs/go/kungfu/runner/flags.go:73) starts its benchmark
+    (tests/go/cmd/kungfu-bench-allreduce). The child inherits stdout, so
+    rank 0's JSON line is this process's line; its exit status is ours. Runs
+    before anything in this process touches the GPU (no exec)."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node", str(args.gpus), "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    sys.stdout.flush()
+    rc = subprocess.call(cmd, env=env)
+    if rc != 0:
+        print("bench.py: the %d ranks ended with status %d" % (args.gpus, rc), file=sys.stderr)
+    return rc
+
+
 def main():
     args = parse()
     if args.c1_child:
@@ -754,11 +805,16 @@ def main():
         return c1_parent(args)
     if args.p2p_child:
         return p2p_child(args)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # nothing has touched the GPU yet: the ranks are children
+        return launch_ranks(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
+    if world != args.gpus and not (args.rehearse_exchange and world == 1):
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE %d (launch with --nproc-per-node "
+                         "%d, or leave WORLD_SIZE unset and bench.py starts its own ranks)"
+                         % (args.gpus, world, args.gpus))
     dev_index = local_rank if args.device_index is None else args.device_index
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
@@ -889,8 +945,9 @@ def main():
             raise SystemExit("C3 all-reduce parity check failed (N=2 bit-exact / N>2 bound)")
         _progress(rank, "C3 parity ok; timing %d steps" % args.steps)
         gb.views[0].copy_(x)
-        step_s = _timed(lambda: prim_ex.all_reduce_(pieces, average=True, coalesce=coalesce),
-                        args.steps, args.warmup, dev, world)
+        step_s, phase_us = _timed_phases(
+            prim_ex, lambda: prim_ex.all_reduce_(pieces, average=True, coalesce=coalesce),
+            args.steps, args.warmup, dev, world)
         value = s_bytes / step_s / 2**30  # per GPU, as the metric says
         busbw = 2 * (world - 1) / world * s_bytes / step_s / 1e9
         _progress(rank, "C3 %.3f ms per step" % (step_s * 1e3))
@@ -903,6 +960,8 @@ def main():
             "buckets": args.buckets,
             "exchange": how,
         }
+        if phase_us is not None:
+            out["collective"]["phase_us"] = phase_us
         if trial is not None:
             out["collective"]["schedule_trial_ms"] = {
                 k: None if v is None else round(v * 1e3, 4) for k, v in trial.items()}
@@ -1117,12 +1176,16 @@ def _agree(ok, dev):
     return bool(t.item())
 
 
-def _timed(fn, steps, warmup, dev, world):
+def _timed(fn, steps, warmup, dev, world, on_timed=None):
+    """Seconds per step, the max over ranks. on_timed: called once the
+    warmup is done, right before the timed region starts."""
     for _ in range(warmup):
         fn()
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
+    if on_timed is not None:
+        on_timed()
     t0 = time.perf_counter()
     for _ in range(steps):
         fn()
@@ -1132,6 +1195,28 @@ def _timed(fn, steps, warmup, dev, world):
     t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return t.item() / steps
+
+
+def _timed_phases(ex, fn, steps, warmup, dev, world):
+    """_timed over the exchange's per-phase timing window (set_timing /
+    phase_times: HIP events at the phase boundaries on the launch stream):
+    (seconds per step, {phase: us per step, ...} of this rank, or None when
+    the exchange has no timing). The phases of an un-pipelined call partition
+    its stream time, so their sum is the step minus the host's gaps between
+    calls; pipelined calls overlap two streams and are counted, not split."""
+    if not hasattr(ex, "set_timing"):
+        return _timed(fn, steps, warmup, dev, world), None
+    step_s = _timed(fn, steps, warmup, dev, world, on_timed=lambda: ex.set_timing(True))
+    ph = ex.phase_times()
+    ex.set_timing(False)
+    calls, untimed = ph.pop("calls"), ph.pop("untimed_calls")
+    out = {k: round(v / steps, 2) for k, v in ph.items()}
+    out["sum"] = round(sum(ph.values()) / steps, 2)
+    out["timed_calls_per_step"] = round(calls / steps, 3)
+    if untimed:
+        out["pipelined_calls_untimed"] = untimed
+    out["step_us"] = round(step_s * 1e6, 2)
+    return step_s, out
 
 
 def _fill(gb, rank_seed, dev, dtype):
@@ -1383,6 +1468,12 @@ class _AlgoView:
     def start_into_(self, *a, **kw):
         return self._run(self.ex.start_into_, *a, **kw)
 
+    def set_timing(self, on):
+        return self.ex.set_timing(on)
+
+    def phase_times(self):
+        return self.ex.phase_times()
+
 
 def bench_c3_native(world, rank, dev, steps, warmup, n, x, algo, nb, fused=False, pipe=False):
     """C3 through the native exchange with another algo or layout: "a2a" =
@@ -1490,7 +1581,8 @@ def bench_c4(world, rank, dev, steps, warmup, exchange="native"):
     if not _agree(ok, dev):
         return {"error": "C4 parity check failed (N=2 or P2P bit-exact / N>2 bound)"}
     s_bytes = sum(sizes) * 4
-    step_s = _timed(lambda: ex.all_reduce_(mine.buckets, average=True), steps, warmup, dev, world)
+    step_s, phase_us = _timed_phases(ex, lambda: ex.all_reduce_(mine.buckets, average=True),
+                                     steps, warmup, dev, world)
     if exchange == "p2p":
         ex.close()
     busbw = 2 * (world - 1) / world * s_bytes / step_s / 1e9
@@ -1507,7 +1599,8 @@ def bench_c4(world, rank, dev, steps, warmup, exchange="native"):
             "bytes": s_bytes, "ms_per_step": round(step_s * 1e3, 4),
             "GiBps_per_gpu": round(s_bytes / step_s / 2**30, 3),
             "busbw_GBps": round(busbw, 2),
-            "frac_of_xgmi": _xgmi_frac(busbw, world)}
+            "frac_of_xgmi": _xgmi_frac(busbw, world),
+            "phase_us": phase_us}
 
 
 def bench_c4_named(world, rank, dev, steps, warmup):
@@ -1683,7 +1776,8 @@ def bench_c5(world, rank, dev, steps, warmup, alpha=0.1, exchange="native"):
     if not _agree(ok, dev):
         return {"error": "C5 not bit-exact against the rank-order bf16 fold + blend"}
     s_bytes = sum(sizes) * 2
-    step_s = _timed(lambda: ex.sma_(mine.buckets, alpha), steps, warmup, dev, world)
+    step_s, phase_us = _timed_phases(ex, lambda: ex.sma_(mine.buckets, alpha), steps, warmup,
+                                     dev, world)
     if exchange == "p2p":
         ex.close()
     busbw = 2 * (world - 1) / world * s_bytes / step_s / 1e9
@@ -1702,6 +1796,7 @@ def bench_c5(world, rank, dev, steps, warmup, alpha=0.1, exchange="native"):
             "GiBps_per_gpu": round(s_bytes / step_s / 2**30, 3),
             "busbw_GBps": round(busbw, 2),
             "frac_of_xgmi": _xgmi_frac(busbw, world),
+            "phase_us": phase_us,
             "parity": "bf16 unpinned (DESIGN.md); bit-exact vs the local rank-order fold "
                       "+ blend"}
 
@@ -1848,4 +1943,4 @@ def bench_c5_overlap(world, rank, dev, steps, warmup, alpha=0.1):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

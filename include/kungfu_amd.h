@@ -169,6 +169,15 @@ const char *kf_version(void);
 /* Last HIP error string recorded by the library on this thread. */
 const char *kf_last_error(void);
 
+/* Release the library's process-wide HIP resources (the streams and HBM
+ * scratch std_transform_2 / kf_transform2_host lend to their calls) while the
+ * HIP runtime is still up. No destructor in the library calls HIP at process
+ * exit, so a host that never calls this leaves those to the OS. Call it once
+ * no host-API call is running (KF_ERR_ARG otherwise: the busy ones are kept);
+ * the library stays usable afterwards. The Python binding calls it at
+ * interpreter exit. */
+int kf_shutdown(void);
+
 /* kf_bucket_reduce / kf_bucket_reduce_avg for inputs that sit behind
  * different links (kungfu_amd/p2p.py: shard `rank` of every peer's bucket,
  * mapped over xGMI): every thread has the loads of up to 8 inputs in flight
@@ -197,7 +206,8 @@ int kf_set_geometry(int unroll, int grid_cap, int loadnt, int stplain);
 int kf_set_occupancy(int lds_small, int lds_fold);
 
 /* Host-pointer reduce with a status code instead of exit(): the path
- * std_transform_2 takes. Synchronous, per-thread stream and device scratch.
+ * std_transform_2 takes. Synchronous, a stream and device scratch lent to the
+ * call from a process-wide pool (kf_shutdown frees them).
  * If x, y and out are all device-accessible (page-locked by hipHostMalloc or
  * kf_host_register, or HBM of the current device) the kernel reads and writes
  * them in place (zero copy, over PCIe for host memory); otherwise pageable
@@ -485,6 +495,19 @@ int kf_exchange_sma_batch(kf_exchange_t *ex, void *const *vs, void *const *sums,
  * rank-order fold, and for SMA its blends) runs on the exchange's own stream
  * meanwhile, ordered by events. Same results bit for bit. */
 int kf_exchange_set_pipeline(kf_exchange_t *ex, int groups);
+/* Opt-in per-phase timing of the batch calls (kf_exchange_all_reduce,
+ * kf_exchange_all_reduce_batch, kf_exchange_sma_batch) on the un-pipelined
+ * schedule: timing events on the caller's stream before phase 1 (every
+ * bucket's reduce-scatter or all-to-all, and the tail gathers), phase 2 (the
+ * /np epilogue or rank-order fold), phase 3 (the all-gathers), the SMA blend,
+ * and after it. on != 0 starts a window with zeroed sums, 0 ends it. Costs
+ * five event records per call; off by default. */
+int kf_exchange_set_timing(kf_exchange_t *ex, int on);
+/* The window's sums in microseconds: us[0] phase 1, us[1] phase 2, us[2]
+ * phase 3, us[3] blend; *calls the timed calls, *untimed the pipelined ones
+ * (their phases overlap on two streams, so they are not split). Waits for the
+ * timed calls queued so far. calls / untimed may be NULL. */
+int kf_exchange_phase_times(kf_exchange_t *ex, double *us, int64_t *calls, int64_t *untimed);
 /* Ordered issue of concurrently produced all-reduces, the reference's
  * NCCLScheduler / LinearExecutor (srcs/cpp/src/nccl/scheduler.cpp:8-130):
  * begin_step fixes this step's names in an order every rank shares;

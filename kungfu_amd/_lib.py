@@ -4,6 +4,7 @@ The shared library is built in-tree by ``kungfu_amd/csrc/Makefile``
 (``__graft_entry__.build()``). There is deliberately no fallback: if the
 library is missing, or the process has no GPU, the product path raises.
 """
+import atexit
 import ctypes
 import os
 
@@ -23,6 +24,7 @@ EXPORTED = (
     "kf_device_count",
     "kf_version",
     "kf_last_error",
+    "kf_shutdown",
     "kf_transform2_host",
     "kf_set_geometry",
     "kf_host_register",
@@ -74,6 +76,8 @@ EXPORTED = (
     "kf_sma_blend_batch",
     "kf_exchange_sma_batch",
     "kf_exchange_set_pipeline",
+    "kf_exchange_set_timing",
+    "kf_exchange_phase_times",
     "kf_exchange_begin_step",
     "kf_exchange_start",
     "kf_exchange_wait_all",
@@ -158,6 +162,8 @@ def load():
     lib.kf_version.restype = ctypes.c_char_p
     lib.kf_last_error.argtypes = []
     lib.kf_last_error.restype = ctypes.c_char_p
+    lib.kf_shutdown.argtypes = []
+    lib.kf_shutdown.restype = c_int
     lib.kf_transform2_host.argtypes = [c_void_p, c_void_p, c_void_p, c_size_t,
                                        c_int, c_int]
     lib.kf_transform2_host.restype = c_int
@@ -295,6 +301,11 @@ def load():
     lib.kf_exchange_check.restype = c_int
     lib.kf_exchange_set_pipeline.argtypes = [c_void_p, c_int]
     lib.kf_exchange_set_pipeline.restype = c_int
+    lib.kf_exchange_set_timing.argtypes = [c_void_p, c_int]
+    lib.kf_exchange_set_timing.restype = c_int
+    lib.kf_exchange_phase_times.argtypes = [c_void_p, P(ctypes.c_double), P(ctypes.c_int64),
+                                            P(ctypes.c_int64)]
+    lib.kf_exchange_phase_times.restype = c_int
     lib.kf_exchange_info.argtypes = [c_void_p, P(c_int), P(c_int), P(c_int)]
     lib.kf_exchange_info.restype = c_int
     lib.kf_exchange_destroy.argtypes = [c_void_p]
@@ -319,6 +330,9 @@ def load():
                                        c_int, c_int, c_int, ctypes.c_char_p, c_void_p]
     lib.kf_hier_all_reduce.restype = c_int
     _lib = lib
+    # HIP resources go back while the runtime is alive, before the C exit
+    # handlers run (include/kungfu_amd.h kf_shutdown)
+    atexit.register(lib.kf_shutdown)
     return lib
 
 

@@ -113,6 +113,43 @@ def padded_count(count, world, itemsize):
     return ((count + unit - 1) // unit) * unit
 
 
+PHASES = ("reduce_scatter", "epilogue", "all_gather", "blend")
+
+
+class _PhaseClock:
+    """Per-phase timing of the calls in a window (Exchange.set_timing): timing
+    events on the current stream at every point where it moves from one phase
+    to the next, so the segments partition the stream's time from a call's
+    first launch to its last wait. A segment counts for the phase that ends
+    at its closing mark: waiting on a reduce-scatter (or all-to-all) is
+    phase 1, the HIP shard work phase 2, waiting on the all-gathers phase 3."""
+
+    def __init__(self):
+        self.calls = []
+
+    def begin(self):
+        marks = []
+        self.calls.append(marks)
+        self.mark(marks, "start")
+        return marks
+
+    @staticmethod
+    def mark(marks, label):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        marks.append((label, ev))
+
+    def sums(self):
+        out = dict.fromkeys(PHASES, 0.0)
+        for marks in self.calls:
+            marks[-1][1].synchronize()
+            for (_, a), (label, b) in zip(marks, marks[1:]):
+                out[label] += 1e3 * a.elapsed_time(b)
+        out["calls"] = len(self.calls)
+        out["untimed_calls"] = 0
+        return out
+
+
 class Exchange:
     """One process group, its shard workspaces and the epilogue."""
 
@@ -124,6 +161,26 @@ class Exchange:
         self.algo = algo
         resolve_algo(algo, torch.float32, OP.SUM, self.world)  # validates
         self._ws = {}
+        self._clock = None
+
+    def set_timing(self, on):
+        """Start (zeroed) or stop the per-phase timing window (the native
+        exchange's kf_exchange_set_timing, for this path)."""
+        self._clock = _PhaseClock() if on else None
+
+    def phase_times(self):
+        """The window's per-phase sums in us (PHASES) and the timed calls."""
+        if self._clock is None:
+            return dict(dict.fromkeys(PHASES, 0.0), calls=0, untimed_calls=0)
+        return self._clock.sums()
+
+    def _marks(self):
+        return self._clock.begin() if self._clock is not None else None
+
+    @staticmethod
+    def _mark(marks, label):
+        if marks is not None:
+            _PhaseClock.mark(marks, label)
 
     def _workspace(self, key, n, like):
         t = self._ws.get(key)
@@ -172,6 +229,7 @@ class Exchange:
             runs = coalesce_runs(buckets)
             if len(runs) < len(buckets):
                 return self.start_(runs, op=op, average=average, coalesce=False, key=key)
+        marks = self._marks()
         shards = []
         works = []
         for i, b in enumerate(buckets):
@@ -181,14 +239,17 @@ class Exchange:
         gathers = []
         for b, shard, (w, recv) in zip(buckets, shards, works):
             w.wait()
+            self._mark(marks, "reduce_scatter")
             if recv is not None:  # the rank-order fold of the received shards
                 self.epilogue.fold_(list(recv.chunk(self.world)), shard, red,
                                     self.world if average else 0)
             elif average:
                 self.epilogue.div_(shard, self.world)
+            self._mark(marks, "epilogue")
             gathers.append(dist.all_gather_into_tensor(b, shard, group=self.group,
                                                        async_op=True))
-        return _Handle(gathers)
+        return _Handle(gathers, None if marks is None else
+                       (lambda: _PhaseClock.mark(marks, "all_gather")))
 
     def _scatter(self, b, shard, red, key):
         """Step 1 for one bucket: (work, None) for RCCL's reduce-scatter into
@@ -218,6 +279,7 @@ class Exchange:
         # right behind its reduce-scatter, and each bucket's blend waits only
         # for its own all-gather, so blends overlap later buckets' transfers.
         # The reduce-scatter reads v before any blend of that bucket runs.
+        marks = self._marks()
         rs = []
         for i, b in enumerate(buckets):
             shard = self._workspace(("rs", i), b.numel() // self.world, b)
@@ -225,27 +287,35 @@ class Exchange:
         ags = []
         for i, (b, (shard, (w, recv))) in enumerate(zip(buckets, rs)):
             w.wait()
+            self._mark(marks, "reduce_scatter")
             if recv is not None:
                 self.epilogue.fold_(list(recv.chunk(self.world)), shard, OP.SUM, 0)
+                self._mark(marks, "epilogue")
             s = self._workspace(("sum", i), b.numel(), b)
             ags.append((s, dist.all_gather_into_tensor(s, shard, group=self.group,
                                                        async_op=True)))
         for b, (s, w) in zip(buckets, ags):
             w.wait()
+            self._mark(marks, "all_gather")
             self.epilogue.sma_blend_(b, s, self.world, alpha)
+            self._mark(marks, "blend")
         return buckets
 
 
 class _Handle:
     """Pending collectives of one start_() call."""
 
-    def __init__(self, works):
+    def __init__(self, works, on_done=None):
         self.works = works
+        self.on_done = on_done
 
     def wait(self):
         for w in self.works:
             w.wait()
         self.works = []
+        if self.on_done is not None:
+            self.on_done()
+            self.on_done = None
 
 
 class GradBuckets:

@@ -18,6 +18,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "kf_reduce_kernels.hpp"
 #include "kungfu_amd.h"
@@ -579,17 +580,24 @@ int host_grid()
     return g;
 }
 
-// Per-thread stream + HBM scratch for pageable buffers.
+// Stream + HBM scratch for pageable buffers, lent to one host-API call at a
+// time (std_transform_2 is called from many threads at once, session.go:317-
+// 323). No destructor releases them: a hipFree / hipStreamDestroy that runs
+// after main returns (a thread_local or static destructor) can reach a HIP
+// runtime that is already torn down. kf_shutdown() frees the idle ones while
+// the runtime is alive; whatever is left is the OS's at exit.
 struct Staging {
     hipStream_t s = nullptr;
     void *dev     = nullptr;  // 3 regions: x | y | z
     size_t cap    = 0;        // bytes per region
 
-    ~Staging()
+    void release()
     {
-        // Process teardown may have unloaded the runtime already; best effort.
         if (dev) (void)hipFree(dev);
         if (s) (void)hipStreamDestroy(s);
+        dev = nullptr;
+        s   = nullptr;
+        cap = 0;
     }
 
     int ensure_stream()
@@ -611,6 +619,7 @@ struct Staging {
         if (bytes > cap) {
             if (dev) KF_HIP(hipFree(dev));
             dev            = nullptr;
+            cap            = 0;
             size_t rounded = (bytes + 255) & ~static_cast<size_t>(255);
             KF_HIP(hipMalloc(&dev, 3 * rounded));
             cap = rounded;
@@ -619,7 +628,49 @@ struct Staging {
     }
 };
 
-thread_local Staging t_staging;
+struct StagingPool {
+    std::mutex mu;
+    std::vector<Staging *> idle;
+    size_t lent = 0;
+};
+
+// never destroyed (see Staging)
+StagingPool &staging_pool()
+{
+    static StagingPool *p = new StagingPool;
+    return *p;
+}
+
+// one call's Staging, back to the pool at the end of the call
+class StagingLease
+{
+  public:
+    StagingLease()
+    {
+        StagingPool &p = staging_pool();
+        std::lock_guard<std::mutex> l(p.mu);
+        if (!p.idle.empty()) {
+            st_ = p.idle.back();
+            p.idle.pop_back();
+        } else {
+            st_ = new Staging;
+        }
+        ++p.lent;
+    }
+    ~StagingLease()
+    {
+        StagingPool &p = staging_pool();
+        std::lock_guard<std::mutex> l(p.mu);
+        p.idle.push_back(st_);
+        --p.lent;
+    }
+    StagingLease(const StagingLease &)            = delete;
+    StagingLease &operator=(const StagingLease &) = delete;
+    Staging &operator*() const { return *st_; }
+
+  private:
+    Staging *st_;
+};
 
 // Where a host-API pointer lives: 0 pageable (or unknown to HIP), 1 page-locked
 // host memory (hipHostMalloc / kf_host_register), 2 device memory. `dev` is the
@@ -660,7 +711,8 @@ int transform2_host(const void *x, const void *y, void *out, size_t n,
     if (sz == 0 || dt == KungFu_BOOL) return KF_ERR_DTYPE;
     if (n == 0) return KF_OK;
     const size_t bytes = n * static_cast<size_t>(sz);
-    Staging &st        = t_staging;
+    StagingLease lease;
+    Staging &st = *lease;
     const void *gx = nullptr, *gy = nullptr, *gz = nullptr;
     const int kx = classify(x, bytes, &gx);
     const int ky = kx ? classify(y, bytes, &gy) : 0;
@@ -918,6 +970,22 @@ int kf_device_count(void)
 const char *kf_version(void) { return "kungfu_amd 0.1.0 (gfx950)"; }
 
 const char *kf_last_error(void) { return t_last_error.c_str(); }
+
+int kf_shutdown(void)
+{
+    StagingPool &p = staging_pool();
+    std::lock_guard<std::mutex> l(p.mu);
+    for (Staging *st : p.idle) {
+        st->release();
+        delete st;
+    }
+    p.idle.clear();
+    if (p.lent != 0) {
+        t_last_error = "kf_shutdown: " + std::to_string(p.lent) + " host-API call(s) still running";
+        return KF_ERR_ARG;
+    }
+    return KF_OK;
+}
 
 int kf_transform2_host(const void *x, const void *y, void *out, size_t n,
                        KungFu_Datatype dt, KungFu_Op op)

@@ -362,6 +362,21 @@ struct kf_exchange {
     hipStream_t comp   = nullptr;
     std::vector<hipEvent_t> pev;  // 3 per group
 
+    // opt-in per-phase timing (kf_exchange_set_timing): five timing events on
+    // the caller's stream at the phase boundaries of every un-pipelined batch
+    // call; the sums are taken when asked (kf_exchange_phase_times)
+    struct Marks {
+        hipEvent_t e[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    };
+    bool timing = false;
+    std::deque<Marks> marks_used;
+    std::vector<Marks> marks_free;
+    double phase_us[4]   = {0, 0, 0, 0};
+    int64_t timed_calls  = 0;
+    int64_t untimed_calls = 0;  // pipelined calls: their phases overlap
+    Marks *take_marks();
+    int harvest_marks();
+
     // NCCLScheduler / LinearExecutor
     std::mutex smu;
     std::condition_variable scv;
@@ -651,13 +666,23 @@ int kf_exchange::batch(const void *const *sends, void *const *recvs, const size_
 
     const int G = phases == 7 ? std::min(groups, nb) : 1;
     if (G <= 1) {
+        Marks *mk = timing ? take_marks() : nullptr;
+        auto mark = [&](int k) {
+            if (mk) (void)hipEventRecord(mk->e[k], s);
+        };
+        mark(0);
         if (phases & 1) rc = phase1(0, nb);
+        mark(1);
         if (rc == KF_OK && (phases & 2)) rc = phase2(0, nb, s);
+        mark(2);
         if (rc == KF_OK && (phases & 4)) rc = phase3(0, nb);
+        mark(3);
         if (rc == KF_OK && phases == 7) rc = blend(0, nb, s);
+        mark(4);
         if (need) release_ws(s);  // whatever ran reads the workspace in stream order
         return rc;
     }
+    if (timing) ++untimed_calls;
 
     // pipelined: groups of consecutive buckets with about equal bytes;
     //   caller stream s: p1(0) p1(1) [wait p2(0)] p3(0) p1(2) [wait p2(1)] p3(1) ...
@@ -688,33 +713,80 @@ int kf_exchange::batch(const void *const *sends, void *const *recvs, const size_
     auto e3 = [&](int g) { return pev[3 * g + 2]; };
     hipEvent_t e_end = pev[3 * ng];
     bool comp_used   = false;
+    // every failure below leaves through the same exit (no early return), so
+    // the folds already queued on comp are joined and the workspace released
+    auto hip_ok = [&](hipError_t e, const char *what) -> int {
+        return e == hipSuccess ? KF_OK : hip_fail(e, what);
+    };
     auto finish = [&](int g) -> int {  // gather group g, then blend it
-        KF_HIP(hipStreamWaitEvent(s, e2(g), 0));
-        int f = phase3(gb[g], gb[g + 1]);
+        int f = hip_ok(hipStreamWaitEvent(s, e2(g), 0), "hipStreamWaitEvent(p2)");
+        if (f == KF_OK) f = phase3(gb[g], gb[g + 1]);
         if (f != KF_OK || !sma) return f;
-        KF_HIP(hipEventRecord(e3(g), s));
-        KF_HIP(hipStreamWaitEvent(comp, e3(g), 0));
-        return blend(gb[g], gb[g + 1], comp);
+        f = hip_ok(hipEventRecord(e3(g), s), "hipEventRecord(p3)");
+        if (f == KF_OK) f = hip_ok(hipStreamWaitEvent(comp, e3(g), 0), "hipStreamWaitEvent(p3)");
+        if (f == KF_OK) f = blend(gb[g], gb[g + 1], comp);
+        return f;
     };
     for (int g = 0; g < ng && rc == KF_OK; ++g) {
         rc = phase1(gb[g], gb[g + 1]);
+        if (rc == KF_OK) rc = hip_ok(hipEventRecord(e1(g), s), "hipEventRecord(p1)");
+        if (rc == KF_OK) rc = hip_ok(hipStreamWaitEvent(comp, e1(g), 0), "hipStreamWaitEvent(p1)");
         if (rc != KF_OK) break;
-        KF_HIP(hipEventRecord(e1(g), s));
-        KF_HIP(hipStreamWaitEvent(comp, e1(g), 0));
         comp_used = true;
         rc = phase2(gb[g], gb[g + 1], comp);
-        if (rc != KF_OK) break;
-        KF_HIP(hipEventRecord(e2(g), comp));
-        if (g > 0) rc = finish(g - 1);
+        if (rc == KF_OK) rc = hip_ok(hipEventRecord(e2(g), comp), "hipEventRecord(p2)");
+        if (rc == KF_OK && g > 0) rc = finish(g - 1);
     }
     if (rc == KF_OK) rc = finish(ng - 1);
     // the caller's stream ends after everything queued on comp (the last
     // blend; after a failure, the folds already queued), so neither the
-    // workspace nor the buckets are reused under them
+    // workspace nor the buckets are reused under them; if even that join
+    // cannot be queued, wait for comp here
     if (comp_used && (sma || rc != KF_OK)) {
-        if (hipEventRecord(e_end, comp) == hipSuccess) (void)hipStreamWaitEvent(s, e_end, 0);
+        if (hipEventRecord(e_end, comp) != hipSuccess || hipStreamWaitEvent(s, e_end, 0) != hipSuccess) {
+            (void)hipStreamSynchronize(comp);
+        }
     }
     if (need) release_ws(s);
+    return rc;
+}
+
+kf_exchange::Marks *kf_exchange::take_marks()
+{
+    if (marks_free.empty()) {
+        Marks m;
+        for (auto &e : m.e) {
+            if (hipEventCreate(&e) != hipSuccess) {
+                for (auto &f : m.e)
+                    if (f) (void)hipEventDestroy(f);
+                return nullptr;  // this call goes untimed
+            }
+        }
+        marks_free.push_back(m);
+    }
+    marks_used.push_back(marks_free.back());
+    marks_free.pop_back();
+    return &marks_used.back();
+}
+
+// sum the finished calls' phase times (waits for the last one queued)
+int kf_exchange::harvest_marks()
+{
+    int rc = KF_OK;
+    while (!marks_used.empty()) {
+        Marks m = marks_used.front();
+        marks_used.pop_front();
+        if (rc == KF_OK && hipEventSynchronize(m.e[4]) == hipSuccess) {
+            for (int k = 0; k < 4; ++k) {
+                float ms = 0;
+                if (hipEventElapsedTime(&ms, m.e[k], m.e[k + 1]) == hipSuccess) phase_us[k] += 1e3 * ms;
+            }
+            ++timed_calls;
+        } else {
+            rc = fail(KF_ERR_HIP, "kf_exchange_phase_times: a timed call's events");
+        }
+        marks_free.push_back(m);
+    }
     return rc;
 }
 
@@ -1219,6 +1291,9 @@ kf_exchange::~kf_exchange()
     if (cdev) (void)hipFree(cdev);
     if (chost) (void)hipHostFree(chost);
     for (auto e : pev) (void)hipEventDestroy(e);
+    for (auto &m : marks_used) marks_free.push_back(m);
+    for (auto &m : marks_free)
+        for (auto e : m.e) (void)hipEventDestroy(e);
 }
 
 extern "C" {
@@ -1458,6 +1533,30 @@ int kf_exchange_set_pipeline(kf_exchange_t *ex, int groups)
     std::lock_guard<std::mutex> lk(ex->mu);
     ex->groups = groups;
     return KF_OK;
+}
+
+int kf_exchange_set_timing(kf_exchange_t *ex, int on)
+{
+    if (!ex) return fail(KF_ERR_ARG, "kf_exchange_set_timing: null exchange");
+    std::lock_guard<std::mutex> lk(ex->mu);
+    DeviceGuard g(ex->device);
+    const int rc = ex->harvest_marks();  // what was queued before counts for the old window
+    ex->timing   = on != 0;
+    for (double &v : ex->phase_us) v = 0;
+    ex->timed_calls = ex->untimed_calls = 0;
+    return rc;
+}
+
+int kf_exchange_phase_times(kf_exchange_t *ex, double *us, int64_t *calls, int64_t *untimed)
+{
+    if (!ex || !us) return fail(KF_ERR_ARG, "kf_exchange_phase_times: null argument");
+    std::lock_guard<std::mutex> lk(ex->mu);
+    DeviceGuard g(ex->device);
+    const int rc = ex->harvest_marks();
+    for (int k = 0; k < 4; ++k) us[k] = ex->phase_us[k];
+    if (calls) *calls = ex->timed_calls;
+    if (untimed) *untimed = ex->untimed_calls;
+    return rc;
 }
 
 int kf_exchange_begin_step(kf_exchange_t *ex, const char *const *names, int n, int auto_order)

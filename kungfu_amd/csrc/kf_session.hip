@@ -382,6 +382,22 @@ struct Lease {
     size_t cap = 0;
 };
 
+// Host mode: one received chunk body to fold into RecvBuf on a worker thread
+// (the reference's recvOnto runs on the chunk's own goroutine, session.go:317-
+// 323, execution.go:13-25), so the poll thread reads the next message while it
+// folds. Jobs of one chunk run one after another in arrival order (the lock of
+// recvOnto, session.go:258-259); `own` is chosen when the job starts.
+struct FoldJob {
+    SessOp *o = nullptr;
+    size_t i  = 0;
+    const char *own = nullptr;
+    char *dst       = nullptr;
+    size_t n        = 0;
+    std::vector<char> *body = nullptr;
+    int rc = KF_OK;
+    std::string err;
+};
+
 struct SessChunk {
     std::string name;
     const Strategy *st;
@@ -391,6 +407,7 @@ struct SessChunk {
     bool batched;              // stage the reduce arrivals, fold them in one launch
     std::vector<int> waiting;  // reduce predecessors not yet heard from
     hipEvent_t mirror_ev;      // device mode: the last fold went to the mirror (its end)
+    std::deque<FoldJob *> folds;  // host mode: received, not yet folded (front: running)
 };
 
 // One collective call (all-reduce, reduce, broadcast, subset all-reduce): the
@@ -420,6 +437,7 @@ struct SessOp {
     size_t remaining = 0;
     Lease stage, mir;
     size_t sends = 0;  // its chunks queued for the sender, not yet written (kf_session::mu)
+    size_t folds = 0;  // host mode: its fold jobs not yet retired by the poll thread
     int rc       = KF_OK;
     std::string err;
 };
@@ -448,7 +466,17 @@ struct kf_session {
     std::vector<hipEvent_t> ev_pool;  // free "chunk is final" events
     std::mutex ev_mu;
     kf_host_reduce_fn host_fn = nullptr;
-    std::vector<char> scratch;  // host-mode landing buffer (one chunk)
+    std::vector<char> scratch;  // host-mode landing buffer (one chunk, inline folds)
+    // host mode: fold workers (KUNGFU_AMD_HOST_FOLD_THREADS, 0 = fold inline
+    // on the poll thread); finished jobs go back to the poll thread, which
+    // alone touches the collectives' state, through fdone + wake()
+    int fold_threads = -1;  // -1: not decided yet
+    std::vector<std::thread> fold_workers;
+    std::mutex fmu;
+    std::condition_variable fcv;
+    std::deque<FoldJob *> fq, fdone;
+    bool fstop = false;
+    std::vector<std::vector<char> *> fbodies;  // free chunk bodies (poll thread)
     int batch_fold = 1;         // device mode: k-input fold at multi-predecessor nodes
     // per collective in flight, lent from these pools (device mode):
     //  * HBM staging for the k-input fold: [predecessor arrival][bucket bytes];
@@ -537,6 +565,15 @@ struct kf_session {
             wake();
             aworker.join();
         }
+        if (!fold_workers.empty()) {
+            {
+                std::lock_guard<std::mutex> l(fmu);
+                fstop = true;
+            }
+            fcv.notify_all();
+            for (auto &t : fold_workers) t.join();
+        }
+        for (auto *b : fbodies) delete b;
         if (sender.joinable()) {
             {
                 std::lock_guard<std::mutex> l(mu);
@@ -907,6 +944,10 @@ struct kf_session {
     void finish_reduce(SessOp &o, size_t i);
     int complete(SessOp &o);
     int run(SessOp *one);
+    bool fold_pool();
+    void fold_loop();
+    void start_fold(SessOp &o, size_t i);
+    void retire_folds();
     bool take(std::vector<Lease> &pool, size_t need, bool host, Lease *out);
     void give(std::vector<Lease> &pool, Lease &l);
 };
@@ -1193,6 +1234,33 @@ int kf_session::handle(SessOp &o, size_t i, uint32_t flags, int peer, int fd, co
             r = mirror_done(o, i, dst);
             if (r != KF_OK) return r;
         }
+    } else if (fold_pool()) {  // the fold runs on a worker; the poll thread reads on
+        auto *j = new FoldJob;
+        j->o    = &o;
+        j->i    = i;
+        j->dst  = dst;
+        j->n    = n;
+        if (fbodies.empty()) {
+            j->body = new std::vector<char>(kChunk + 64);
+        } else {
+            j->body = fbodies.back();
+            fbodies.pop_back();
+        }
+        if (j->body->size() < len) j->body->resize(len);
+        if (mem) {
+            std::memcpy(j->body->data(), mem, len);
+        } else {
+            r = kf_rch_recv_body(fd, j->body->data(), len);
+            if (r != KF_OK) {
+                fbodies.push_back(j->body);
+                delete j;
+                return fail(r, kf_ingest_last_error());
+            }
+        }
+        c.folds.push_back(j);
+        ++o.folds;
+        if (c.folds.size() == 1) start_fold(o, i);
+        return KF_OK;  // recv_count / pending_reduce move when it is retired
     } else {
         const char *pd = mem;
         if (!mem) {
@@ -1216,6 +1284,62 @@ int kf_session::handle(SessOp &o, size_t i, uint32_t flags, int peer, int fd, co
         if (c.bcast_done) --o.remaining;
     }
     return KF_OK;
+}
+
+// Host mode: whether chunk folds go to the worker pool (started on first use)
+bool kf_session::fold_pool()
+{
+    if (fold_threads < 0) {
+        const unsigned hw = std::thread::hardware_concurrency();
+        int t             = static_cast<int>(std::min(8u, std::max(1u, hw)));
+        if (const char *e = std::getenv("KUNGFU_AMD_HOST_FOLD_THREADS")) t = std::max(0, std::atoi(e));
+        fold_threads = t;
+        for (int k = 0; k < t; ++k) fold_workers.emplace_back([this] { fold_loop(); });
+    }
+    return fold_threads > 0;
+}
+
+void kf_session::fold_loop()
+{
+    for (;;) {
+        FoldJob *j = nullptr;
+        {
+            std::unique_lock<std::mutex> l(fmu);
+            fcv.wait(l, [&] { return fstop || !fq.empty(); });
+            if (fq.empty()) return;
+            j = fq.front();
+            fq.pop_front();
+        }
+        const KungFu_Datatype dt = j->o->dt;  // fixed for the collective's lifetime
+        const KungFu_Op op       = j->o->op;
+        if (host_fn) {
+            if (host_fn(j->own, j->body->data(), j->dst, static_cast<int64_t>(j->n),
+                        static_cast<int>(dt), static_cast<int>(op)) != 0) {
+                j->rc  = KF_ERR_OP;
+                j->err = "host reduce callback failed";
+            }
+        } else {
+            j->rc = kf_transform2_host(j->own, j->body->data(), j->dst, j->n, dt, op);
+            if (j->rc != KF_OK) j->err = kf_last_error();
+        }
+        {
+            std::lock_guard<std::mutex> l(fmu);
+            fdone.push_back(j);
+        }
+        wake();
+    }
+}
+
+// the chunk's oldest received body goes to a worker: RecvBuf = effective o body
+void kf_session::start_fold(SessOp &o, size_t i)
+{
+    FoldJob *j = o.chunks[i].folds.front();
+    j->own     = effective(o, i);
+    {
+        std::lock_guard<std::mutex> l(fmu);
+        fq.push_back(j);
+    }
+    fcv.notify_one();
 }
 
 // Every chunk received and every outgoing chunk written: the device work
@@ -1261,7 +1385,7 @@ int kf_session::run(SessOp *one)
         pfds.push_back({kv.second, POLLIN, 0});
         pfd_peer.push_back(kv.first);
     }
-    if (!one && wake_fd >= 0) {
+    if (wake_fd >= 0) {  // submissions, sends done, host folds done
         pfds.push_back({wake_fd, POLLIN, 0});
         pfd_peer.push_back(-1);
     }
@@ -1311,9 +1435,71 @@ int kf_session::run(SessOp *one)
     };
     if (one) start(one);
 
+    // host mode: the folds the workers finished, in the order they finished;
+    // a chunk's next body goes out once the one before it is folded
+    auto retire_folds = [&] {
+        std::deque<FoldJob *> done;
+        {
+            std::lock_guard<std::mutex> l(fmu);
+            done.swap(fdone);
+        }
+        for (FoldJob *j : done) {
+            SessOp &o    = *j->o;
+            const size_t i = j->i;
+            auto &c      = o.chunks[i];
+            c.folds.pop_front();  // j: one fold per chunk runs at a time
+            --o.folds;
+            fbodies.push_back(j->body);
+            if (j->rc != KF_OK && o.rc == KF_OK) {
+                o.rc  = j->rc;
+                o.err = j->err;
+            }
+            delete j;
+            if (o.rc != KF_OK) {  // failed (here or on a socket): its queued bodies go
+                while (!c.folds.empty()) {
+                    FoldJob *q = c.folds.front();
+                    c.folds.pop_front();
+                    --o.folds;
+                    fbodies.push_back(q->body);
+                    delete q;
+                }
+                if (o.remaining > 0) {
+                    o.remaining = 0;
+                    for (auto &ch : o.chunks) {
+                        auto f = index.find(ch.name);
+                        if (f != index.end() && f->second.first == &o) index.erase(f);
+                    }
+                }
+                continue;
+            }
+            ++c.recv_count;
+            if (--c.pending_reduce == 0) {
+                finish_reduce(o, i);
+                if (c.bcast_done) --o.remaining;
+            } else if (!c.folds.empty()) {
+                start_fold(o, i);
+            }
+        }
+    };
+
+    // a chunk of a call in flight still waits for a message (not only for its
+    // folds: a peer that sent its last chunk may close before they finish)
+    auto expecting_message = [&] {
+        for (SessOp *o : active) {
+            if (o->remaining == 0) continue;
+            for (auto &c : o->chunks) {
+                if (!c.waiting.empty() || (!c.bcast_done && !c.st->bcast.prev[rank].empty())) {
+                    return true;
+                }
+            }
+        }
+        return false;
+    };
+
     char hname[512];
     uint32_t flags = 0;
     for (;;) {
+        retire_folds();
         if (!one) {  // start what was submitted; a name in flight waits for its call
             std::vector<SessOp *> fresh;
             {
@@ -1333,6 +1519,7 @@ int kf_session::run(SessOp *one)
             for (SessOp *o : fresh) start(o);
         }
         // complete the collectives whose chunks are all in and all sent
+        bool retired = false;
         for (size_t a = 0; a < active.size();) {
             SessOp *o = active[a];
             bool sent = false;
@@ -1344,11 +1531,12 @@ int kf_session::run(SessOp *one)
                     o->err = "send: " + send_err;
                 }
             }
-            if (o->remaining > 0 || !sent) {
+            if (o->remaining > 0 || !sent || o->folds > 0) {
                 ++a;
                 continue;
             }
             active.erase(active.begin() + a);
+            retired = true;
             for (auto &c : o->chunks) {
                 auto f = index.find(c.name);
                 if (f != index.end() && f->second.first == o) index.erase(f);
@@ -1379,6 +1567,14 @@ int kf_session::run(SessOp *one)
                 if (--apending == 0) aidle.notify_all();
             }
         }
+        if (!one && retired) {  // a call waiting for the name just freed starts now,
+            bool queued = false;  // not after the next message: that message may
+            {                     // only come once the peer sees this call's chunks
+                std::lock_guard<std::mutex> l(amu);
+                queued = !aq.empty();
+            }
+            if (queued) continue;
+        }
         if (!one && active.empty()) {  // idle: wait for a submission, or the end;
             rl.unlock();               // blocking calls run their own loop meanwhile
             {
@@ -1389,9 +1585,12 @@ int kf_session::run(SessOp *one)
             rl.lock();
             continue;
         }
-        bool waiting_rx = false;  // anything still expected from the sockets?
-        for (SessOp *o : active) waiting_rx = waiting_rx || o->remaining > 0;
-        if (!waiting_rx && one) {  // only our own sends are left: the sender wakes no one here
+        bool waiting_rx = false, folding = false;  // anything still to come in?
+        for (SessOp *o : active) {
+            waiting_rx = waiting_rx || o->remaining > 0;
+            folding    = folding || o->folds > 0;
+        }
+        if (!waiting_rx && !folding && one) {  // only our own sends are left: the sender wakes no one here
             std::unique_lock<std::mutex> l(mu);
             cv_idle.wait(l, [&] { return one->sends == 0; });
             continue;
@@ -1401,7 +1600,7 @@ int kf_session::run(SessOp *one)
         // would otherwise wait for a message that cannot come
         size_t open_fds = 0;
         for (size_t q = 0; q < pfds.size(); ++q) open_fds += pfds[q].fd >= 0 && pfd_peer[q] >= 0;
-        if (open_fds == 0 && waiting_rx) {
+        if (open_fds == 0 && waiting_rx && expecting_message()) {
             fail_all(fail(KF_ERR_IO, "every peer connection closed before the all-reduce finished"));
             continue;
         }

@@ -29,6 +29,10 @@ from .base import OP, OP_NAMES
 from .ops import kungfu_dtype
 
 ALGOS = {"auto": 0, "rs": 1, "a2a": 2}
+# kf_exchange_phase_times' order: phase 1 (reduce-scatter, or all-to-all for
+# the rank-order fold), phase 2 (/np epilogue or the fold), phase 3
+# (all-gather), the SMA blend
+PHASES = ("reduce_scatter", "epilogue", "all_gather", "blend")
 _NO_DONE = _lib.DONE_FN()  # a NULL kf_done_fn
 
 
@@ -115,6 +119,24 @@ class NativeExchange:
                    "kf_exchange_set_pipeline")
         self.groups = int(groups)
         return self
+
+    def set_timing(self, on):
+        """kf_exchange_set_timing: start (zeroed) or stop the per-phase timing
+        window of the un-pipelined batch calls."""
+        _lib.check(self.lib.kf_exchange_set_timing(self._h, 1 if on else 0),
+                   "kf_exchange_set_timing")
+
+    def phase_times(self):
+        """kf_exchange_phase_times: the window's per-phase sums in us
+        (PHASES order) and the number of timed / pipelined (untimed) calls."""
+        us = (ctypes.c_double * 4)()
+        calls, untimed = ctypes.c_int64(), ctypes.c_int64()
+        _lib.check(self.lib.kf_exchange_phase_times(self._h, us, ctypes.byref(calls),
+                                                    ctypes.byref(untimed)),
+                   "kf_exchange_phase_times")
+        out = dict(zip(PHASES, (float(v) for v in us)))
+        out.update(calls=calls.value, untimed_calls=untimed.value)
+        return out
 
     # -- the optimizers' interface (collective.Exchange) --------------------
     def _check(self, buckets):

@@ -39,27 +39,73 @@ def _init_native():
         return None
     if dist.is_initialized() and dist.get_backend() != "nccl":
         return None
-    import sys
-    m, ok = None, True
-    try:
+
+    def load_module():
         from .. import kungfu_amd_torch_ops as m
-    except ImportError as e:
-        print("kungfu_amd.torch.ops: C++ op module unavailable: %r" % (e,), file=sys.stderr)
-        ok = False
-    if not _agree(ok):
-        return None
-    try:
-        from ..exchange import NativeExchange
-        uid = NativeExchange.shared_id()
-        rank = dist.get_rank() if dist.is_initialized() else 0
-        m.init_exchange(uid, rank, _world(), torch.cuda.current_device())
-    except RuntimeError as e:  # KungFuAMDError is one
-        print("kungfu_amd.torch.ops: exchange setup failed on rank %d: %r"
-              % (dist.get_rank() if dist.is_initialized() else 0, e), file=sys.stderr)
-        ok = False
-    if not _agree(ok):
+        return m
+
+    def make_uid():
+        import ctypes
+        from .. import _lib
+        uid = (ctypes.c_char * 128)()
+        _lib.check(_lib.load().kf_exchange_unique_id(uid), "kf_exchange_unique_id")
+        return bytes(uid)
+
+    def init(m, uid, rank, world):
+        m.init_exchange(uid, rank, world, torch.cuda.current_device())
+
+    def finalize(m):
         if m.initialized():
             m.finalize()
+
+    return bring_up(load_module, make_uid, init, finalize)
+
+
+def bring_up(load_module, make_uid, init, finalize):
+    """The native op's start-up, decided the same way on every rank. RCCL's
+    communicator init blocks until every rank has joined, so no rank may
+    enter it unless every rank is known to get there: each step that can
+    fail on one rank alone (the module import, rank 0's unique id, anything
+    before the init) is followed by an agreement (all_gather_object), and a
+    failure anywhere sends every rank to the torch.distributed path together.
+    The reference's init blocks the same way with no such check
+    (gpu_collective.cpp:105). Returns the module, or None."""
+    import sys
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    world = _world()
+    m, uid, ok = None, None, True
+
+    def say(what, e):
+        print("kungfu_amd.torch.ops: %s on rank %d: %r" % (what, rank, e), file=sys.stderr)
+
+    try:
+        m = load_module()
+    except ImportError as e:
+        say("C++ op module unavailable", e)
+        ok = False
+    if ok and rank == 0:
+        try:
+            uid = make_uid()
+        except RuntimeError as e:  # KungFuAMDError is one
+            say("unique id failed", e)
+            ok = False
+    # every rank is ready to join (and rank 0 has an id) before any shares it
+    if not _agree(ok):
+        return None
+    if world > 1:
+        box = [uid]
+        dist.broadcast_object_list(box, src=0)
+        uid = box[0]
+    try:
+        init(m, uid, rank, world)
+    except RuntimeError as e:
+        say("exchange setup failed", e)
+        ok = False
+    if not _agree(ok):
+        try:
+            finalize(m)
+        except RuntimeError as e:
+            say("finalize failed", e)
         return None
     return m
 

@@ -337,8 +337,9 @@ struct chunk_job {
     int64_t n;
     int dt, op;
     int64_t chunk_elems;
-    int64_t next; /* shared counter, guarded by mu */
-    pthread_mutex_t mu;
+    int64_t total; /* reps x chunks: chunk c is chunk c % nchunks of rep c / nchunks */
+    int64_t nchunks;
+    int64_t next;  /* shared counter (atomic fetch-add) */
     transform2_fn fn; /* 0: the restatement */
 };
 
@@ -351,16 +352,19 @@ static void run_span(const struct chunk_job *j, int64_t b, int64_t e, uint32_t s
     }
 }
 
+/* One OS thread of the pool (a Go P under GOMAXPROCS): takes the next chunk
+ * of the stream of all-reduces until every rep's chunks are taken, the way
+ * runStrategiesWithHash's goroutine-per-chunk fan-out (session.go:317-323)
+ * keeps every thread busy. The threads live for all reps: a goroutine costs
+ * no thread creation, so neither does a rep here. */
 static void *chunk_worker(void *arg)
 {
     struct chunk_job *j = (struct chunk_job *)arg;
     uint32_t sz = oracle_type_size(j->dt);
     for (;;) {
-        pthread_mutex_lock(&j->mu);
-        int64_t b = j->next;
-        j->next += j->chunk_elems;
-        pthread_mutex_unlock(&j->mu);
-        if (b >= j->n) break;
+        int64_t c = __atomic_fetch_add(&j->next, 1, __ATOMIC_RELAXED);
+        if (c >= j->total) break;
+        int64_t b = (c % j->nchunks) * j->chunk_elems;
         int64_t e = b + j->chunk_elems < j->n ? b + j->chunk_elems : j->n;
         run_span(j, b, e, sz);
     }
@@ -374,30 +378,34 @@ static double now_s(void)
     return ts.tv_sec + ts.tv_nsec * 1e-9;
 }
 
+#define MAX_POOL 1024
+
 static double bench(transform2_fn fn, const void *x, const void *y, void *z, int64_t n,
                     int dt, int op, int reps, int threads, int64_t chunk_bytes)
 {
     uint32_t sz = oracle_type_size(dt);
-    if (sz == 0 || threads < 1) return -1.0;
+    if (sz == 0 || threads < 1 || threads > MAX_POOL || n <= 0) return -1.0;
     if (fn && n > 2147483647) return -1.0; /* the reference's n is an int */
-    double t0 = now_s();
-    for (int r = 0; r < reps; ++r) {
-        struct chunk_job j;
-        j.x = (const char *)x; j.y = (const char *)y; j.z = (char *)z;
-        j.n = n; j.dt = dt; j.op = op; j.fn = fn;
-        if (threads == 1) {
-            run_span(&j, 0, n, sz);
-            continue;
-        }
-        j.chunk_elems = chunk_bytes / sz > 0 ? chunk_bytes / sz : 1;
-        j.next = 0;
-        pthread_mutex_init(&j.mu, 0);
-        pthread_t tid[256];
-        int t = threads > 256 ? 256 : threads;
-        for (int i = 0; i < t; ++i) pthread_create(&tid[i], 0, chunk_worker, &j);
-        for (int i = 0; i < t; ++i) pthread_join(tid[i], 0);
-        pthread_mutex_destroy(&j.mu);
+    struct chunk_job j;
+    j.x = (const char *)x; j.y = (const char *)y; j.z = (char *)z;
+    j.n = n; j.dt = dt; j.op = op; j.fn = fn;
+    if (threads == 1) {
+        double t0 = now_s();
+        for (int r = 0; r < reps; ++r) run_span(&j, 0, n, sz);
+        return now_s() - t0;
     }
+    j.chunk_elems = chunk_bytes / sz > 0 ? chunk_bytes / sz : 1;
+    j.nchunks = (n + j.chunk_elems - 1) / j.chunk_elems;
+    j.total = j.nchunks * reps;
+    j.next = 0;
+    pthread_t tid[MAX_POOL];
+    double t0 = now_s(); /* one pool for all reps: its start-up is amortised */
+    int started = 0;
+    for (; started < threads; ++started) {
+        if (pthread_create(&tid[started], 0, chunk_worker, &j) != 0) break;
+    }
+    for (int i = 0; i < started; ++i) pthread_join(tid[i], 0);
+    if (started == 0) return -1.0;
     return now_s() - t0;
 }
 

@@ -23,7 +23,7 @@ thread_local std::string t_err;
 // ---------------------------------------------------------------------------
 // loopback: every collective is a rendezvous of the group's threads
 // ---------------------------------------------------------------------------
-enum { LB_OK = 0, LB_HIP = 1, LB_DTYPE = 2, LB_ARG = 3 };
+enum { LB_OK = 0, LB_HIP = 1, LB_DTYPE = 2, LB_ARG = 3, LB_INJECTED = 4 };
 
 struct LoopSlot {
     int arrived = 0, left = 0;
@@ -34,6 +34,7 @@ struct LoopSlot {
 
 struct LoopGroup {
     int world;
+    int64_t fail_at = -1;  // kf_loopback_fail_at: this call index of every rank fails
     std::mutex mu;
     std::condition_variable cv;
     std::map<uint64_t, LoopSlot> slots;
@@ -44,7 +45,8 @@ struct LoopGroup {
 struct LoopComm {
     LoopGroup *g;
     int rank;
-    uint64_t seq = 0;
+    uint64_t seq   = 0;
+    int64_t calls  = 0;  // collective calls made (injection counter)
 };
 
 size_t dsize(KungFu_Datatype dt)
@@ -80,6 +82,8 @@ template <typename F>
 int loop_collective(void *comm, const void *send, void *recv, void *stream, F move)
 {
     auto *c = static_cast<LoopComm *>(comm);
+    // every rank fails the same call before its rendezvous, so none waits
+    if (c->calls++ == c->g->fail_at) return LB_INJECTED;
     if (stream && hipStreamSynchronize(static_cast<hipStream_t>(stream)) != hipSuccess) return LB_HIP;
     LoopGroup *g = c->g;
     std::unique_lock<std::mutex> lk(g->mu);
@@ -223,6 +227,7 @@ const char *lb_error_string(int code)
     switch (code) {
     case LB_HIP: return "loopback: a HIP copy failed";
     case LB_DTYPE: return "loopback: no reduce-scatter for this dtype";
+    case LB_INJECTED: return "loopback: injected failure";
     default: return "loopback transport error";
     }
 }
@@ -355,6 +360,11 @@ kf_loopback_t *kf_loopback_create(int world)
 }
 
 void kf_loopback_destroy(kf_loopback_t *g) { delete g; }
+
+void kf_loopback_fail_at(kf_loopback_t *g, int64_t call)
+{
+    if (g) g->g.fail_at = call;
+}
 
 kf_exchange_t *kf_exchange_create_loopback(kf_loopback_t *g, int rank, int device)
 {

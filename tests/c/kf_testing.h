@@ -27,6 +27,10 @@ kf_loopback_t *kf_loopback_create(int world);
 /* after every exchange of the group (and of its splits) was destroyed */
 void kf_loopback_destroy(kf_loopback_t *g);
 kf_exchange_t *kf_exchange_create_loopback(kf_loopback_t *g, int rank, int device);
+/* every rank's collective call number `call` (0-based, counted per rank's
+ * communicator since its creation) fails with "injected failure" before its
+ * rendezvous; -1 = none. Set before the ranks call. */
+void kf_loopback_fail_at(kf_loopback_t *g, int64_t call);
 /* NULL on failure (kf_testing_last_error) */
 kf_exchange_t *kf_exchange_create_rccl1(int device);
 const char *kf_testing_last_error(void);

@@ -55,6 +55,7 @@ int main(void)
     free(a);
     free(b);
     free(c);
+    CHECK(kf_shutdown() == KF_OK); /* HIP resources back while the runtime is up */
     printf("ok\n");
     return 0;
 }

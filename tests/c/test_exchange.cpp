@@ -252,6 +252,7 @@ int main()
     CHECK(hipStreamDestroy(s) == hipSuccess);
     CHECK(multi_rank_loopback(3) == 0);
     CHECK(multi_rank_named(3) == 0);
+    CHECK(kf_shutdown() == KF_OK);  // HIP resources back while the runtime is up
     std::printf("exchange ok\n");
     return 0;
 }

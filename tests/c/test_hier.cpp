@@ -177,6 +177,7 @@ int main(int argc, char **argv)
     std::printf("2 + 1 ranks ok\n");
     CHECK(run_layout({{0}, {1}}, port + 20, argv[2], true) == 0);
     std::printf("2 hosts x 1 rank (kf_exchange_create_local) ok\n");
+    CHECK(kf_shutdown() == KF_OK);  // HIP resources back while the runtime is up
     std::printf("hier ok\n");
     return 0;
 }

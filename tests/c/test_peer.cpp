@@ -96,8 +96,16 @@ int main(int argc, char **argv)
     }
     const int rank = std::atoi(argv[1]), size = std::atoi(argv[2]);
     const bool device = argc > 4 && std::strcmp(argv[4], "dev") == 0;
-    Peer world(rank, size, device ? Peer::Device : Peer::Host, argv[3]);
-    if (test_AllReduce(world, size, device)) return 1;
+    {
+        Peer world(rank, size, device ? Peer::Device : Peer::Host, argv[3]);
+        if (test_AllReduce(world, size, device)) return 1;
+    }
+    // the session is gone; the drop-in's HIP resources go back while the
+    // runtime is up (no library destructor touches HIP at exit)
+    if (kf_shutdown() != KF_OK) {
+        std::printf("kf_shutdown: %s\n", kf_last_error());
+        return 1;
+    }
     std::printf("peer ok (%d of %d, %s)\n", rank, size, device ? "device" : "host");
     return 0;
 }

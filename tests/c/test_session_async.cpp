@@ -140,6 +140,10 @@ int main(int argc, char **argv)
         std::printf("FAIL %d\n", g_failures.load());
         return 1;
     }
+    if (kf_shutdown() != KF_OK) {
+        std::printf("kf_shutdown: %s\n", kf_last_error());
+        return 1;
+    }
     std::printf("OK np=%d steps=%d\n", np, steps);
     return 0;
 }

@@ -27,6 +27,8 @@ def load():
         lib.kf_loopback_create.restype = ctypes.c_void_p
         lib.kf_loopback_destroy.argtypes = [ctypes.c_void_p]
         lib.kf_loopback_destroy.restype = None
+        lib.kf_loopback_fail_at.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+        lib.kf_loopback_fail_at.restype = None
         lib.kf_exchange_create_loopback.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
         lib.kf_exchange_create_loopback.restype = ctypes.c_void_p
         lib.kf_exchange_create_rccl1.argtypes = [ctypes.c_int]
@@ -51,6 +53,10 @@ class LoopbackGroup:
         assert h, self.lib.kf_testing_last_error().decode()
         return NativeExchange.from_handle(h, algo)
 
+    def fail_at(self, call):
+        """kf_loopback_fail_at: every rank's collective call #call fails."""
+        self.lib.kf_loopback_fail_at(self._h, int(call))
+
     def close(self):
         if self._h:
             self.lib.kf_loopback_destroy(self._h)
@@ -66,11 +72,11 @@ def rccl1_exchange(algo="auto", device=0):
     return NativeExchange.from_handle(h, algo)
 
 
-def loop_ranks(world, body, timeout=300):
+def loop_ranks(world, body, timeout=300, group=None):
     """Run body(rank, ex) on `world` threads, each with its own exchange of
-    one loopback group; re-raise the first failure."""
+    one loopback group (`group`, or a new one); re-raise the first failure."""
     import torch
-    g = LoopbackGroup(world)
+    g = group if group is not None else LoopbackGroup(world)
     errs = []
 
     def run(r):

@@ -1,0 +1,45 @@
+"""bench.py's launch contract, checked without a GPU: a WORLD_SIZE that
+disagrees with --gpus is an error (non-zero exit before anything touches the
+GPU), and `--gpus N` with no launcher around it starts the N ranks itself
+under torch.distributed.run (the reference's `kungfu-run -np N`,
+srcs/go/kungfu/runner/flags.go:73) and relays their exit status."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _env(**kw):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(kw)
+    return env
+
+
+@pytest.mark.parametrize("gpus,world", [(2, "1"), (1, "2"), (8, "4")])
+def test_world_size_mismatch_exits_nonzero(gpus, world):
+    r = subprocess.run([sys.executable, BENCH, "--gpus", str(gpus), "--steps", "1"],
+                       env=_env(WORLD_SIZE=world, RANK="0", LOCAL_RANK="0"),
+                       capture_output=True, text=True, timeout=120, cwd=ROOT)
+    assert r.returncode != 0
+    assert "WORLD_SIZE" in r.stderr, r.stderr[-2000:]
+    assert r.stdout.strip() == ""
+
+
+def test_self_launch_starts_n_ranks_and_relays_status():
+    """No GPU here: each of the 2 ranks the launcher starts fails at its
+    first device call, so the parent must come back non-zero, having started
+    torch.distributed.run with 2 ranks (its per-rank failure report names
+    both local ranks)."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("CPU-only check (the GPU variant is in test_bench_gpu.py)")
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--steps", "1", "--warmup", "0"],
+                       env=_env(), capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode != 0
+    assert "the 2 ranks ended with status" in r.stderr, r.stderr[-3000:]
+    assert "(local_rank: 0)" in r.stderr and "(local_rank: 1)" in r.stderr, r.stderr[-3000:]

@@ -45,6 +45,29 @@ def test_bench_n2_rehearsal_with_p2p_children():
     assert d["p2p_children"]["all_ok"] is True
 
 
+def test_bench_gpus2_starts_its_own_ranks():
+    """`bench.py --gpus 2` with no launcher: bench.py starts the two ranks
+    itself (torch.distributed.run as a child) and relays rank 0's line."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+           "--device-index", "0", "--steps", "3", "--warmup", "1", "--elems", str(4 << 20),
+           "--extras", ""]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and "collective" in d and d["value"] > 0, d
+    # the per-phase split of the timed step (RS / epilogue / AG)
+    ph = d["collective"]["phase_us"]
+    total = sum(v for k, v in ph.items() if k in ("reduce_scatter", "epilogue", "all_gather"))
+    assert abs(total - d["ms_per_step"] * 1e3) <= 0.1 * d["ms_per_step"] * 1e3, (ph, d["ms_per_step"])
+
+
 _NATIVE_CHILD = r"""
 import os, sys
 sys.path[:0] = [%r, %r]

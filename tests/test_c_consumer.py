@@ -134,13 +134,21 @@ def hier_binary(tmp_path_factory):
 
 
 def _hier_args():
-    import socket
+    """test_hier's base port: every TCP address its three layouts bind
+    (main(): base + rank, base + 10 + rank, base + 20 + rank on 127.0.0.1 /
+    127.0.0.2) bindable now (tests/ports.py)."""
+    import sys
     import tempfile
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return [str(20000 + port % 12000), tempfile.mkdtemp(prefix="kfh")]  # below the ephemeral range
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from ports import draw_block
+
+    def addrs(b):
+        out = []
+        for off, hosts in ((0, [[0, 1], [2, 3]]), (10, [[0, 1], [2]]), (20, [[0], [1]])):
+            for h, ranks in enumerate(hosts):
+                out += [("127.0.0.%d" % (h + 1), b + off + g) for g in ranks]
+        return out
+    return [str(draw_block(addrs)), tempfile.mkdtemp(prefix="kfh")]
 
 
 def test_cpp_hier_host_builds(hier_binary):

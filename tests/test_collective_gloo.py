@@ -655,3 +655,60 @@ def body_auto_exchange_past_16_ranks(rank, world, use_gpu):
 
 def test_auto_exchange_past_16_ranks():
     run_world("body_auto_exchange_past_16_ranks", 17)
+
+
+def body_native_bring_up(rank, world, use_gpu):
+    """kungfu_amd.torch.ops.bring_up over gloo with injected failures: a
+    failure on ONE rank at any step sends every rank to the torch path
+    (None), nobody enters the (blocking) communicator init unless every rank
+    got ready, and nobody hangs; no failure: every rank gets the module."""
+    from kungfu_amd.torch import ops as tops
+
+    class Mod:
+        def __init__(self):
+            self.inits, self.finals = [], 0
+
+        def initialized(self):
+            return bool(self.inits)
+
+    def run(fail_where, fail_rank):
+        mod = Mod()
+
+        def load_module():
+            if fail_where == "import" and rank == fail_rank:
+                raise ImportError("injected")
+            return mod
+
+        def make_uid():
+            if fail_where == "uid":
+                raise RuntimeError("injected")
+            return b"u" * 128
+
+        def init(m, uid, r, w):
+            assert uid == b"u" * 128 and r == rank and w == world
+            m.inits.append(uid)
+            if fail_where == "init" and rank == fail_rank:
+                raise RuntimeError("injected")
+
+        def finalize(m):
+            m.finals += 1
+
+        got = tops.bring_up(load_module, make_uid, init, finalize)
+        return got, mod
+
+    for where in ("import", "uid", "init"):
+        for fail_rank in range(world):
+            if where == "uid" and fail_rank != 0:
+                continue  # only rank 0 makes the id
+            got, mod = run(where, fail_rank)
+            assert got is None, (where, fail_rank)
+            # the blocking init only after every rank got ready
+            assert bool(mod.inits) == (where == "init"), (where, fail_rank, mod.inits)
+            assert mod.finals == (1 if where == "init" else 0)
+    got, mod = run(None, -1)
+    assert got is mod and len(mod.inits) == 1 and mod.finals == 0
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_native_bring_up_agrees_before_init(world):
+    run_world("body_native_bring_up", world)

@@ -258,6 +258,53 @@ def _loop_ranks(world, body):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("algo", ["rs", "a2a"])
+def test_pipelined_failure_at_every_call_then_reusable(algo):
+    """a transport failure at ANY collective of the
+    pipelined schedule (3 groups of 2 buckets: p1(0) p1(1) p3(0) p1(2) p3(1)
+    p3(2), 12 calls) comes back as the call's error on every rank, with the
+    folds already queued on the exchange's second stream joined and the
+    workspace released: the next call on the same exchange is bit-exact."""
+    import threading
+    import torch
+    from loopback import LoopbackGroup, loop_ranks
+    from oracle import oracle
+    from kungfu_amd._lib import KungFuAMDError
+    dev = _gpu()
+    world, nb = 2, 6
+    counts = [world * (40000 + 1000 * b) for b in range(nb)]  # no tails
+    g = LoopbackGroup(world)
+    bar = threading.Barrier(world)
+    per_call = 2 * nb  # one phase-1 and one phase-3 collective per bucket
+
+    def body(rank, ex):
+        ex.set_pipeline(3)
+        ex.algo = algo
+        done = 0  # collective calls made so far (the same on every rank)
+        for k in range(per_call):
+            hs = [[_rand("f32", n, 100 * r + b + k) for b, n in enumerate(counts)]
+                  for r in range(world)]
+            bufs = [_to_dev(hs[rank][b], "f32", dev) for b in range(nb)]
+            bar.wait()
+            if rank == 0:
+                g.fail_at(done + k)
+            bar.wait()
+            with pytest.raises(KungFuAMDError, match="injected failure"):
+                ex.all_reduce_(bufs, average=True, coalesce=False)
+            done += k + 1
+            # the same exchange, workspace and streams: bit-exact next call
+            bufs = [_to_dev(hs[rank][b], "f32", dev) for b in range(nb)]
+            ex.all_reduce_(bufs, average=True, coalesce=False)
+            torch.cuda.synchronize()
+            done += per_call
+            for b in range(nb):
+                want = oracle.reduce_avg([hs[r][b] for r in range(world)], "f32", world)
+                assert np.array_equal(_to_np(bufs[b], "f32"), want), (k, b)
+
+    loop_ranks(world, body, group=g)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("world,groups", [(2, 1), (3, 1), (4, 1), (8, 1), (2, 3), (3, 2),
                                           (8, 4)])
 def test_exchange_multi_rank_loopback(world, groups):

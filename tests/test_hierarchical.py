@@ -8,7 +8,6 @@ np·x / iota·np, fake_agent.cpp:15-44); float averages within the order bound
 (np-1)·2^-24·Σ|x| + one rounding for the division."""
 import ctypes
 import os
-import random
 import socket
 import sys
 import tempfile
@@ -39,17 +38,28 @@ def _peers(hosts_sizes, base):
     return out
 
 
+def _addr(peer):
+    ip, port = peer.rsplit(":", 1)
+    return ip, int(port)
+
+
 def _x(rank, n):
     return np.random.default_rng(300 + rank).standard_normal(n).astype(np.float32)
 
 
-def _body(rank, peers, port, sock_dir, errq, use_gpu):
+def _body(rank, hosts_sizes, port, sock_dir, errq, use_gpu, first=None):
     import faulthandler
     faulthandler.dump_traceback_later(100, exit=True)  # a hung rank dies loudly
     sys.path[:0] = [ROOT, HERE]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     try:
-        dist.init_process_group("gloo", rank=rank, world_size=len(peers))
+        dist.init_process_group("gloo", rank=rank, world_size=sum(hosts_sizes))
+        # the session ports: a block every rank could bind, agreed over gloo
+        from ports import agreed_block
+        base, rounds = agreed_block(lambda b: [_addr(_peers(hosts_sizes, b)[rank])], first=first)
+        if first is not None:  # the test holds rank 0's first port: redrawn
+            assert rounds >= 2 and base != first, (rounds, base, first)
+        peers = _peers(hosts_sizes, base)
         from cpu_epilogue import CpuEpilogue
         from kungfu_amd.hierarchical import HierarchicalExchange
         from oracle import oracle
@@ -108,14 +118,13 @@ def _body(rank, peers, port, sock_dir, errq, use_gpu):
             dist.destroy_process_group()
 
 
-def _run(hosts_sizes, use_gpu=False):
-    peers = _peers(hosts_sizes, random.Random().randrange(20000, 32000, 16))  # below the ephemeral range (32768+), where gloo's own connections live
+def _run(hosts_sizes, use_gpu=False, first=None):
     ctx = mp.get_context("spawn")
     errq = ctx.SimpleQueue()
     port = _free_port()
     with tempfile.TemporaryDirectory() as d:
-        ps = [ctx.Process(target=_body, args=(r, peers, port, d, errq, use_gpu))
-              for r in range(len(peers))]
+        ps = [ctx.Process(target=_body, args=(r, hosts_sizes, port, d, errq, use_gpu, first))
+              for r in range(sum(hosts_sizes))]
         for p in ps:
             p.start()
         for p in ps:
@@ -147,6 +156,19 @@ def test_uneven_hosts_via_master():
 def test_one_rank_per_host():
     # every host one rank: the whole exchange is the cross-host session
     _run([1, 1, 1])
+
+
+def test_session_port_taken_is_redrawn():
+    """Another process listens on the first port chosen for rank 0's session:
+    the ranks see it in their bind check, agree to redraw, and the run
+    passes."""
+    sys.path[:0] = [HERE]
+    from ports import taken_port
+    s, p = taken_port()
+    try:
+        _run([1, 1], first=p)
+    finally:
+        s.close()
 
 
 @pytest.mark.gpu
@@ -191,12 +213,12 @@ def test_native_hierarchical_threads_two_hosts_two_ranks():
     from kungfu_amd.hierarchical import NativeHierarchicalExchange
     from kungfu_amd.session import Session
     from oracle import oracle
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    base = 20000 + s.getsockname()[1] % 12000  # below the ephemeral range (32768+)
-    s.close()
+    from ports import draw_block
     hosts = [[0, 1], [2, 3]]
-    peers = ["127.0.0.%d:%d" % (h + 1, base + g) for h, hs in enumerate(hosts) for g in hs]
+
+    def mk(base):
+        return ["127.0.0.%d:%d" % (h + 1, base + g) for h, hs in enumerate(hosts) for g in hs]
+    peers = mk(draw_block(lambda b: [_addr(p) for p in mk(b)]))  # all bindable now
     groups = [LoopbackGroup(2), LoopbackGroup(2)]
     d = tempfile.mkdtemp(prefix="kfnh")
     dev = torch.device("cuda:0")

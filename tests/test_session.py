@@ -137,6 +137,16 @@ def test_session_host_mode(size, kind, n):
     run(size, "host", kind, n)
 
 
+@pytest.mark.parametrize("threads", ["0", "1", "3"])
+@pytest.mark.parametrize("strategy", ["STAR", "RING", "BINARY_TREE"])
+def test_session_host_fold_workers(threads, strategy):
+    """Host mode folds each received chunk on a worker (the goroutine per
+    chunk) while the poll thread reads the next one; 0 folds inline on the
+    poll thread. Same schedule, same bits, at 4 peers and several chunks."""
+    run(4, "host", "rand", (5 << 20) // 4 + 7, strategy=strategy,
+        env={"KUNGFU_AMD_HOST_FOLD_THREADS": threads})
+
+
 @pytest.mark.parametrize("strategy", ["RING", "CLIQUE", "BINARY_TREE", "STAR",
                                       "BINARY_TREE_STAR", "AUTO"])
 @pytest.mark.parametrize("size", [2, 3, 4])
@@ -502,12 +512,109 @@ def test_session_async_any_order_host(size, strategy):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("size,strategy", [(3, None), (4, "RING")])
+@pytest.mark.parametrize("size,strategy", [(3, None), (4, "RING"), (4, "BINARY_TREE"),
+                                           (3, "CLIQUE")])
 def test_session_async_any_order_device(size, strategy):
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     _run_any_order(size, "device", strategy)
+
+
+def _names_with_roots(n, want):
+    """Bucket names whose single chunk a 2-peer CLIQUE roots at want[0],
+    want[1], ... (strategy index = nameBasedHash % 2, shard.go:17-23)."""
+    from oracle import schedule
+    out = []
+    for r in want:
+        for j in range(1000):
+            name = "g%d" % j
+            if name not in out and schedule.chunk_roots(n, 4, 2, "CLIQUE", name)[0][2] == r:
+                out.append(name)
+                break
+    return out
+
+
+def _next_call_body(rank, sock_dir, mode, errq):
+    """X is rooted at rank 1, Z at rank 0. Rank 0 queues
+    X(0), Z(0), X(1), Z(1) at once; rank 1 queues X(0), X(1), waits for X(1)
+    and only then queues Z(0), Z(1). Rank 0's X(0) completes on rank 1's
+    bcast while Z(0) is still in flight; rank 1 then sends nothing until it
+    has rank 0's X(1) chunk. So rank 0 must start X(1) as soon as X(0)
+    completes, not after its next socket message (which never comes)."""
+    sys.path[:0] = [ROOT, HERE]
+    os.environ["KUNGFU_ALLREDUCE_STRATEGY"] = "CLIQUE"
+    try:
+        from kungfu_amd.session import Session
+        n = 1000
+        X, Z = _names_with_roots(n, (1, 0))
+        if mode == "device":
+            import torch
+            dev = torch.device("cuda:0")
+            s = Session(rank, 2, sock_dir, mode="device")
+            mk = lambda v: torch.full((n,), float(v), device=dev)  # noqa: E731
+        else:
+            s = Session(rank, 2, sock_dir, mode="host", host_reduce_fn=oracle_reduce_fn())
+            mk = lambda v: np.full(n, float(v), dtype=np.float32)  # noqa: E731
+        want = {}
+        hs = {}
+
+        def go(name, step):
+            x = mk((rank + 1) * (step + 1) + (name == Z))
+            hs[(name, step)] = s.all_reduce_async(x, mk(0), name)
+            want[(name, step)] = 3.0 * (step + 1) + 2 * (name == Z)
+
+        if rank == 0:
+            for step in (0, 1):
+                go(X, step)
+                go(Z, step)
+        else:
+            go(X, 0)
+            go(X, 1)
+            hs[(X, 1)].wait()
+            go(Z, 0)
+            go(Z, 1)
+        s.wait_all()
+        for key, h in hs.items():
+            got = h.wait()
+            got = got.cpu().numpy() if mode == "device" else got
+            assert np.all(got == want[key]), (rank, key, got[:3])
+        s.close()
+    except Exception:
+        errq.put("rank %d: %s" % (rank, traceback.format_exc()))
+
+
+def _run_next_call(mode):
+    ctx = mp.get_context("spawn")
+    errq = ctx.SimpleQueue()
+    with tempfile.TemporaryDirectory() as d:
+        ps = [ctx.Process(target=_next_call_body, args=(r, d, mode, errq)) for r in range(2)]
+        for p in ps:
+            p.start()
+        for p in ps:
+            p.join(timeout=60)
+        hung = [p.exitcode is None for p in ps]
+        for p in ps:
+            if p.exitcode is None:
+                p.kill()
+    errs = []
+    while not errq.empty():
+        errs.append(errq.get())
+    assert not any(hung), "hung: a queued call was not started after its name freed"
+    assert not errs, "\n".join(errs)
+    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+
+
+def test_session_async_next_call_starts_on_completion_host():
+    _run_next_call("host")
+
+
+@pytest.mark.gpu
+def test_session_async_next_call_starts_on_completion_device():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _run_next_call("device")
 
 
 def _dead_peer_body(rank, sock_dir, errq):

@@ -7,9 +7,9 @@ MULTI_BINARY_TREE_STAR, AUTO -> BINARY_TREE_STAR) is checked against the
 oracle schedule (oracle/schedule.py) built on the same host layout."""
 import itertools
 import os
-import random
 import sys
 import tempfile
+import time
 import traceback
 
 import numpy as np
@@ -18,6 +18,9 @@ import torch.multiprocessing as mp
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
+sys.path.insert(0, HERE)
+from ports import draw_block, taken_port  # noqa: E402
+
 NAME = "NegotiatedGrad_0/AllReduce"
 
 
@@ -90,22 +93,49 @@ def check(peers, kind, n, strategy, got):
         assert any(np.array_equal(got[b:e], o[b:e]) for o in outs), (strategy, b, e)
 
 
-def run(hosts_sizes, kind, n, strategy, mode="host"):
-    peers = layout(hosts_sizes, random.Random().randrange(20000, 32000, 16))  # below the ephemeral range (32768+), where gloo's own connections live
+def _addrs(peers):
+    return [(p.rsplit(":", 1)[0], int(p.rsplit(":", 1)[1])) for p in peers]
+
+
+def run(hosts_sizes, kind, n, strategy, mode="host", first=None, attempts=3):
+    """The peers on a port block every address of which could be bound just
+    before (tests/ports.py); if a rank still loses its port to another
+    process ('Address already in use' at session creation), every rank is
+    stopped and the run starts over on a new block. Returns the blocks used."""
     ctx = mp.get_context("spawn")
-    errq = ctx.SimpleQueue()
-    with tempfile.TemporaryDirectory() as d:
-        ps = [ctx.Process(target=_body, args=(r, peers, d, kind, n, strategy, errq, mode))
-              for r in range(len(peers))]
-        for p in ps:
-            p.start()
-        for p in ps:
-            p.join(timeout=300)
-    errs = []
-    while not errq.empty():
-        errs.append(errq.get())
-    assert not errs, "\n".join(errs)
-    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+    used = []
+    for attempt in range(attempts):
+        if attempt == 0 and first is not None:
+            base = first  # a test forces a taken block here
+        else:
+            base = draw_block(lambda b: _addrs(layout(hosts_sizes, b)))
+        used.append(base)
+        peers = layout(hosts_sizes, base)
+        errq = ctx.SimpleQueue()
+        with tempfile.TemporaryDirectory() as d:
+            ps = [ctx.Process(target=_body, args=(r, peers, d, kind, n, strategy, errq, mode))
+                  for r in range(len(peers))]
+            for p in ps:
+                p.start()
+            errs, taken = [], False
+            deadline = time.monotonic() + 300
+            while any(p.is_alive() for p in ps) and time.monotonic() < deadline and not taken:
+                while not errq.empty():
+                    errs.append(errq.get())
+                taken = any("Address already in use" in e for e in errs)
+                time.sleep(0.05)
+            for p in ps:
+                if taken or p.is_alive():
+                    p.kill()
+                p.join()
+        while not errq.empty():
+            errs.append(errq.get())
+        if any("Address already in use" in e for e in errs):
+            continue  # the peers dialling it would wait for it: start over
+        assert not errs, "\n".join(errs)
+        assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+        return used
+    raise AssertionError("every port block was taken: %r" % used)
 
 
 STRATEGIES = ["STAR", "MULTI_STAR", "CLIQUE", "RING", "TREE", "BINARY_TREE",
@@ -128,6 +158,18 @@ def test_three_uneven_hosts_iota(strategy):
 def test_default_strategy_is_binary_tree_star():
     # no KUNGFU_ALLREDUCE_STRATEGY: kungfu-run's default BINARY_TREE_STAR
     run([1, 2], "rand", 1 << 18, None)
+
+
+def test_taken_port_restarts_on_a_new_block():
+    """The first block's rank-0 port is held by another listener: that rank's
+    session cannot bind ('Address already in use'), the run stops every rank
+    and starts over on a new block, and passes."""
+    s, p = taken_port()
+    try:
+        used = run([1, 1], "iota", 1000, "STAR", first=p)
+    finally:
+        s.close()
+    assert used[0] == p and len(used) == 2, used
 
 
 def test_bad_peer_specs():

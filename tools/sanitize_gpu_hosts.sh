@@ -33,32 +33,44 @@ build)
     echo "built $D"
     ;;
 run)
-    # A host passes when it printed its ok line and ASan reported no error.
-    # ASan's device-allocator CHECK ("dev_runtime_unloaded_") can fire inside
-    # the ROCm runtime's own teardown in __cxa_finalize, after main returned;
-    # that is recorded (the exit status is printed) but is not a report about
-    # this code.
+    # A host passes when it printed its ok line, exited 0 and the sanitizer
+    # reported nothing; any other exit fails the run (an ASan CHECK at exit
+    # included: the library no longer calls HIP from a destructor, and the
+    # hosts call kf_shutdown() before main returns). The raw log of every
+    # failing host is kept under gpurun_out/sanitize_logs/.
     export ASAN_OPTIONS="detect_leaks=0 halt_on_error=1 protect_shadow_gap=0"
     export TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1 suppressions=$ROOT/tools/tsan_rocm.supp"
+    KEEP="$ROOT/gpurun_out/sanitize_logs"
     cd "$D"
-    check() {  # check <log> <ok-pattern> <status>
+    check() {  # check <log> <ok-pattern> <status> <name>
         cat "$1"
         echo "   exit status $3"
-        case $3 in 124|134|137|139) echo "stopping: abort, fault or time limit"; exit 1 ;; esac
-        if grep -q "ERROR: AddressSanitizer\|WARNING: ThreadSanitizer" "$1"; then
-            echo "SANITIZER REPORT"; exit 1
+        local bad=""
+        case $3 in
+        0) ;;
+        124|134|137|139) bad="abort, fault or time limit (status $3)" ;;
+        *) bad="exit status $3" ;;
+        esac
+        if [ -z "$bad" ] && grep -q "ERROR: AddressSanitizer\|WARNING: ThreadSanitizer\|CHECK failed" "$1"; then
+            bad="sanitizer report"
         fi
-        grep -q "$2" "$1" || { echo "no '$2' line"; exit 1; }
+        if [ -z "$bad" ] && ! grep -q "$2" "$1"; then bad="no '$2' line"; fi
+        if [ -n "$bad" ]; then
+            mkdir -p "$KEEP"
+            cp "$1" "$KEEP/$SAN-$4.log"
+            echo "FAIL: $bad (raw log: gpurun_out/sanitize_logs/$SAN-$4.log)"
+            exit 1
+        fi
     }
     L=$(mktemp)
     echo "== test_exchange"
     st=0; timeout -k 10 240 ./test_exchange > "$L" 2>&1 || st=$?
-    check "$L" "exchange ok" $st
+    check "$L" "exchange ok" $st test_exchange
     echo "== test_hier"
     P=$((20000 + RANDOM % 12000))  # below the ephemeral range
     H=$(mktemp -d)
     st=0; timeout -k 10 240 ./test_hier $P "$H" > "$L" 2>&1 || st=$?
-    check "$L" "hier ok" $st
+    check "$L" "hier ok" $st test_hier
     for np in 2 3 4; do
         echo "== test_peer np=$np dev"
         S=$(mktemp -d)
@@ -67,9 +79,10 @@ run)
             timeout -k 10 120 ./test_peer $r $np "$S" dev > "$S/out.$r" 2>&1 &
             pids="$pids $!"
         done
-        st=0
-        for p in $pids; do wait $p || st=$?; done
-        for r in $(seq 0 $((np - 1))); do check "$S/out.$r" "peer ok" $st; done
+        sts=""
+        for p in $pids; do st=0; wait $p || st=$?; sts="$sts $st"; done
+        r=0
+        for st in $sts; do check "$S/out.$r" "peer ok" $st "test_peer_np${np}_r$r"; r=$((r + 1)); done
     done
     echo "$SAN sanitizer, gpu hosts: no report"
     ;;
