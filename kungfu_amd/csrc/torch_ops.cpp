@@ -39,6 +39,7 @@
 #include <hip/hip_runtime_api.h>
 #include <torch/extension.h>
 
+#include <atomic>
 #include <condition_variable>
 #include <map>
 #include <memory>
@@ -66,6 +67,7 @@ struct Pending {
 };
 std::map<int, std::shared_ptr<Pending>> g_handles;
 int g_next = 0;
+std::atomic<int> g_algo{KF_ALGO_AUTO};  // set_algo: the exchange schedule of every op
 
 void check(int rc, const char *what)
 {
@@ -156,7 +158,7 @@ std::shared_ptr<Pending> start(const torch::Tensor &input, torch::Tensor &output
         // (other ranks in a test, the training loop) keep running
         py::gil_scoped_release nogil;
         rc = kf_exchange_all_reduce_named(ex, name.c_str(), in_ptr, out_ptr, n, dt, op, 0,
-                                          KF_ALGO_AUTO, s, on_done, ref);
+                                          g_algo.load(), s, on_done, ref);
     }
     if (rc != KF_OK) {
         delete ref;
@@ -210,6 +212,17 @@ bool initialized() { return g_ex != nullptr; }
 // this thread's ops use `handle` (a kf_exchange_t* as an integer; 0 = back to
 // the process exchange); the caller keeps it alive while bound
 void bind_exchange(uintptr_t handle) { t_ex = reinterpret_cast<kf_exchange_t *>(handle); }
+
+// the schedule of every later op: "auto" (the exchange's choice, default),
+// "rs" (RCCL reduce-scatter), "a2a" (all-to-all + the HIP rank-order fold)
+void set_algo(const std::string &algo)
+{
+    static const std::map<std::string, int> m = {
+        {"auto", KF_ALGO_AUTO}, {"rs", KF_ALGO_REDUCE_SCATTER}, {"a2a", KF_ALGO_ALL_TO_ALL}};
+    auto it = m.find(algo);
+    if (it == m.end()) throw std::runtime_error("kungfu_amd: algo must be auto, rs or a2a");
+    g_algo = it->second;
+}
 
 void finalize()
 {
@@ -277,6 +290,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m)
     m.def("initialized", &initialized);
     m.def("bind_exchange", &bind_exchange);
     m.def("finalize", &finalize);
+    m.def("set_algo", &set_algo);
     m.def("all_reduce_cuda", &all_reduce_cuda);
     m.def("all_reduce_cuda_async", &all_reduce_cuda_async);
     m.def("wait_handle", &wait_handle);

@@ -839,15 +839,19 @@ def test_sma_blend_batch_matches_single(name, np_):
 # ---- name-keyed all-reduce and splits ----------------------------------------
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("algo", ["auto", "a2a"])
 @pytest.mark.parametrize("world", [2, 3, 4])
-def test_named_all_reduce_any_order(world):
+def test_named_all_reduce_any_order(world, algo):
     """kf_exchange_all_reduce_named: every rank starts the step's names in its
     own random order, with random gaps, from its own thread; tensors pair by
     name (the reference's per-name mailbox, handler/collective.go:48-64), so
     each result is the oracle's rank-order fold of that name's buffers on
     every rank. Three steps reuse the names; f32 /np, bf16, i32 MAX and a u16
     SUM (all-to-all fold) are mixed, so one cycle can complete names of
-    different kinds (one batched call per kind)."""
+    different kinds (one batched call per kind). algo "a2a": the f32 and i32
+    names go through the all-to-all and the HIP rank-order fold too (under
+    "auto" they take the transport's reduce-scatter, which the loopback does
+    on the host), so the product's fold is what is checked at world > 1."""
     import time
     import torch
     from oracle import oracle
@@ -867,6 +871,7 @@ def test_named_all_reduce_any_order(world):
 
     def body(rank, ex):
         import torch
+        ex.algo = algo
         s = torch.cuda.Stream()
         for step in range(3):
             rng = np.random.default_rng(31 * rank + step)
@@ -889,7 +894,8 @@ def test_named_all_reduce_any_order(world):
                         ex._named_keep = getattr(ex, "_named_keep", []) + [cb]
                         _lib.check(ex.lib.kf_exchange_all_reduce_named(
                             ex._h, names[i].encode(), bufs[i].data_ptr(), bufs[i].data_ptr(),
-                            bufs[i].numel(), 0x00208, 0, 0, 0, s.cuda_stream, cb, None), "u16")
+                            bufs[i].numel(), 0x00208, 0, 0, 2 if algo == "a2a" else 0,
+                            s.cuda_stream, cb, None), "u16")
                     else:
                         ex.all_reduce_named(names[i], bufs[i], op=op, average=avg,
                                             callback=lambda n, st: seen.append(st))

@@ -72,8 +72,9 @@ def test_cuda_ops_world1():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("algo", ["auto", "a2a"])
 @pytest.mark.parametrize("world", [2, 4])
-def test_cuda_ops_multi_rank_by_name(world):
+def test_cuda_ops_multi_rank_by_name(world, algo):
     """all_reduce_cuda_async pairs tensors by NAME across ranks, as the
     reference's does (collective.cpp:32-55 hands tensor_name to
     Peer::AllReduce, whose messages pair by name): `world` ranks (threads,
@@ -82,7 +83,10 @@ def test_cuda_ops_multi_rank_by_name(world):
     random orders with random gaps; every result equals the oracle's
     rank-order fold of that name's tensors — f32 sum, i32 max, bf16 sum. Then
     the blocking all_reduce_cuda in one order, and the kungfu.torch.ops mirror
-    (inplace_all_reduce_async_op) over the same binding."""
+    (inplace_all_reduce_async_op) over the same binding. algo "a2a"
+    (set_algo): the f32 and i32 names too go through the all-to-all and the
+    HIP rank-order fold, not the loopback's host reduce-scatter, so the
+    product's arithmetic is what is compared at world > 1."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     import time
@@ -155,4 +159,8 @@ def test_cuda_ops_multi_rank_by_name(world):
         finally:
             m.bind_exchange(0)
 
-    loop_ranks(world, body)
+    m.set_algo(algo)
+    try:
+        loop_ranks(world, body)
+    finally:
+        m.set_algo("auto")

@@ -1,0 +1,58 @@
+#!/usr/bin/env bash
+# Round-4 GPU sessions, one stage per call. Every GPU step runs under its own
+# time limit; an abort, fault or time limit stops the script there.
+#   bash tools/gpu_r04.sh <tag> new       # the tests this round added/changed
+#   bash tools/gpu_r04.sh <tag> suite     # the whole -m gpu suite + smoke
+#   bash tools/gpu_r04.sh <tag> bench     # bench.py N=1 (default line)
+#   bash tools/gpu_r04.sh <tag> bench2    # bench.py --gpus 2 rehearsal (self-launch, gloo)
+#   bash tools/gpu_r04.sh <tag> asan      # host-code ASan of the C++ hosts
+set -u
+TAG=${1:?tag}
+shift
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+
+step() {  # step <name> <timeout> <cmd...>
+    local name=$1 t=$2
+    shift 2
+    echo "== $name ($(date +%T))"
+    timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    echo "   rc=$rc"
+    tail -5 "$OUT/$name.log"
+    return $rc
+}
+
+fatal() {  # a crash, abort or time limit: nothing more on the GPU
+    case $1 in 0|1) return 1 ;; *) echo "stopping: status $1"; exit "$1" ;; esac
+}
+
+PYT="python -u -m pytest -x -v -p no:cacheprovider --timeout 120 --timeout-method thread -m gpu"
+for stage in "$@"; do
+  case $stage in
+  new)
+    step new_tests 900 $PYT tests/test_bench_gpu.py tests/test_session.py \
+        tests/test_exchange.py tests/test_torch_ops_native.py tests/test_hierarchical.py \
+        tests/test_c_consumer.py -k "gpus2 or next_call or any_order_device or pipelined_failure \
+or named_all_reduce_any_order or multi_rank_by_name or cross_host or two_hosts or native_hier \
+or hier_all_reduce or fake_agent or rehearsal or branch_single_rank"
+    fatal $? ;;
+  suite)
+    step pytest_gpu 1100 $PYT tests
+    fatal $?
+    step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
+  bench)
+    step bench 900 python bench.py --steps 20 --warmup 5 || exit $?
+    tail -1 "$OUT/bench.log" > "$OUT/bench.json" ;;
+  bench2)
+    step bench2 300 python bench.py --gpus 2 --dist-backend gloo --device-index 0 --steps 5 \
+        --warmup 2 --elems $((16 << 20)) --extras c4_torch,c5_torch --extras-timeout 200 || exit $?
+    tail -1 "$OUT/bench2.log" > "$OUT/bench2.json" ;;
+  asan)
+    step asan_build 600 bash tools/sanitize_gpu_hosts.sh build || exit $?
+    step asan 900 bash tools/sanitize_gpu_hosts.sh run || exit $? ;;
+  *) echo "unknown stage $stage"; exit 2 ;;
+  esac
+done
+echo "all stages done"
