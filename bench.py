@@ -84,7 +84,7 @@ def parse():
                     help="rehearsal only: put every rank on this GPU")
     ap.add_argument("--no-extra", action="store_true",
                     help="N>1: skip the C4/C5/P2P sub-benchmarks")
-    ap.add_argument("--extras", default="c4,c5,c5_pipe,c5_overlap,c4_overlap,c4_pipe,c4_named,c3_pipe,c3_a2a,c3_fused,c3_torch_fused,c3_per_bucket,c4_torch,"
+    ap.add_argument("--extras", default="c4,c5,c5_pipe,c5_overlap,c4_overlap,c4_pipe,c4_rs_avg,c4_named,c3_pipe,c3_a2a,c3_fused,c3_torch_fused,c3_per_bucket,c4_torch,"
                                         "c5_torch,c3_ar,c3_p2p,c3_p2p_push,c3_p2p_hostbar,"
                                         "c4_p2p,c5_p2p",
                     help="N>1: which sub-benchmarks to run (comma list)")
@@ -95,9 +95,9 @@ def parse():
                     help="N>1: seconds for the native exchange's communicator to come up "
                          "before the torch.distributed path is used instead")
     ap.add_argument("--c3-schedule", default="auto",
-                    choices=["auto", "grouped", "fused", "a2a", "pipelined"],
+                    choices=["auto", "grouped", "fused", "a2a", "pipelined", "rs_avg"],
                     help="N>1, native exchange: the C3 schedule timed as `value` (auto: "
-                         "the fastest of a short parity-checked trial of all four)")
+                         "the fastest of a short parity-checked trial of all five)")
     ap.add_argument("--no-c1", action="store_true",
                     help="N=1: skip the C1 (np=2 localhost) sub-object")
     ap.add_argument("--config", default="default", choices=["default", "c1"],
@@ -923,6 +923,10 @@ def main():
                               "native C-ABI exchange: per bucket RCCL reduce-scatter -> HIP /np "
                               "-> RCCL all-gather, pipelined in %d groups (HIP /np on a second "
                               "stream between the groups' collectives)" % PIPE_GROUPS),
+                "rs_avg": (_AlgoView(prim_ex, "rs_avg"), False,
+                           "native C-ABI exchange: per bucket RCCL reduce-scatter with ncclAvg "
+                           "(the /np inside the collective, no HIP epilogue) -> RCCL all-gather, "
+                           "the buckets of a step in one call"),
             }
             if args.c3_schedule != "auto":
                 cands = {args.c3_schedule: cands[args.c3_schedule]}
@@ -984,6 +988,8 @@ def main():
                  ("c4_overlap", lambda: bench_c4_overlap(world, rank, dev, min(steps_x, 20), 3)),
                  ("c4_pipe", lambda: bench_c4(world, rank, dev, steps_x, 5,
                                               exchange="native_pipe")),
+                 ("c4_rs_avg", lambda: bench_c4(world, rank, dev, steps_x, 5,
+                                                exchange="native_rs_avg")),
                  ("c3_pipe", lambda: bench_c3_native(world, rank, dev, steps_x, 5, n, x, "rs",
                                                      args.buckets, pipe=True)),
                  ("c3_a2a", lambda: bench_c3_native(world, rank, dev, steps_x, 5, n, x,
@@ -1431,10 +1437,12 @@ def _exchange(kind):
     if kind == "p2p":
         from kungfu_amd.p2p import PeerExchange
         return PeerExchange(timeout_s=5.0)
-    if kind in ("native", "native_pipe"):
+    if kind in ("native", "native_pipe", "native_rs_avg"):
         ex = _NATIVE.get("ex")
         if ex is None:
             raise RuntimeError("native exchange unavailable (see collective.native_exchange_error)")
+        if kind == "native_rs_avg":
+            return _AlgoView(ex, "rs_avg")
         return _AlgoView(ex, "auto", PIPE_GROUPS if kind == "native_pipe" else 1)
     from kungfu_amd.collective import Exchange
     return Exchange()
@@ -1591,6 +1599,8 @@ def bench_c4(world, rank, dev, steps, warmup, exchange="native"):
            "native_pipe": "native C-ABI exchange: RCCL RS -> HIP /np -> RCCL AG, 16 buckets "
                           "in one call pipelined in %d groups (HIP /np on a second stream "
                           "between the groups' collectives)" % PIPE_GROUPS,
+           "native_rs_avg": "native C-ABI exchange: RCCL RS with ncclAvg (no HIP epilogue) -> "
+                            "RCCL AG, 16 buckets in one call",
            "torch": "torch.distributed RCCL RS -> HIP /np -> RCCL AG",
            "p2p": "xGMI P2P pull: rank-order shard fold from peers' HBM + gather, "
                   "device barriers"}[exchange]

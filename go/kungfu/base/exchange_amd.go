@@ -28,9 +28,10 @@ const ExchangeIDBytes = C.KF_UNIQUE_ID_BYTES
 
 // Exchange algorithms (enum KF_ExchangeAlgo).
 const (
-	AlgoAuto          = int(C.KF_ALGO_AUTO)
-	AlgoReduceScatter = int(C.KF_ALGO_REDUCE_SCATTER)
-	AlgoAllToAll      = int(C.KF_ALGO_ALL_TO_ALL)
+	AlgoAuto             = int(C.KF_ALGO_AUTO)
+	AlgoReduceScatter    = int(C.KF_ALGO_REDUCE_SCATTER)
+	AlgoAllToAll         = int(C.KF_ALGO_ALL_TO_ALL)
+	AlgoReduceScatterAvg = int(C.KF_ALGO_REDUCE_SCATTER_AVG)
 )
 
 type Exchange struct {

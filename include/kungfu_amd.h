@@ -438,6 +438,17 @@ const char *kf_p2p_last_error(void);
  *                           bf16 with fp32 accumulation and one rounding,
  *                           fp16 rounded per hop — equal to the P2P path;
  *                           same xGMI bytes as the reduce-scatter.
+ *   KF_ALGO_REDUCE_SCATTER_AVG
+ *                           for average calls: ncclReduceScatter with
+ *                           ncclAvg (each input scaled by 1/world inside the
+ *                           collective) -> in-place ncclAllGather, no HIP
+ *                           epilogue launch. Opt-in: for f32/f64 the bits
+ *                           equal KF_ALGO_REDUCE_SCATTER's (sum, then /np)
+ *                           when world is a power of two and no x / world is
+ *                           subnormal (scaling by 2^-k commutes with every
+ *                           rounding of the sum); otherwise each input adds
+ *                           one rounding. Calls without average: as
+ *                           KF_ALGO_REDUCE_SCATTER.
  *   KF_ALGO_AUTO            reduce-scatter for integers and f32/f64
  *                           (RCCL's own order; integers exact; float MIN/MAX
  *                           differ from std::min/max only on NaN inputs),
@@ -454,7 +465,12 @@ enum KF_ExchangeAlgo {
     KF_ALGO_AUTO           = 0,
     KF_ALGO_REDUCE_SCATTER = 1,
     KF_ALGO_ALL_TO_ALL     = 2,
+    KF_ALGO_REDUCE_SCATTER_AVG = 3,
 };
+/* the reduce_scatter op a transport is asked for under
+ * KF_ALGO_REDUCE_SCATTER_AVG: the sum of the inputs each scaled by 1/world
+ * (ncclAvg); a transport without it returns a non-zero code */
+#define KF_TRANSPORT_OP_AVG 4
 #pragma GCC visibility pop
 typedef struct kf_exchange kf_exchange_t; /* opaque */
 #pragma GCC visibility push(default)
@@ -550,8 +566,11 @@ const char *kf_exchange_last_error(void);
  * runs once the all-reduce finished on the device (kf_exchange_last_error
  * inside done gives a failure's message). A name may be outstanding once per
  * rank; count, dtype, op and average must agree across ranks (a mismatch
- * fails that name with KF_ERR_ARG on every rank). Do not interleave these
- * with the ordered calls above on one exchange. */
+ * fails that name with KF_ERR_ARG on every rank). An empty name is the
+ * anonymous call of a blocking op (the reference's all_reduce_cuda): the
+ * exchange names it from its own counter, so such calls pair across ranks by
+ * their order on each rank's exchange. Do not interleave these with the
+ * ordered calls above on one exchange. */
 int kf_exchange_all_reduce_named(kf_exchange_t *ex, const char *name, const void *send, void *recv,
                                  size_t count, KungFu_Datatype dt, KungFu_Op op, int average,
                                  int algo, void *stream, kf_done_fn done, void *arg);
@@ -571,7 +590,8 @@ int kf_exchange_wait_named(kf_exchange_t *ex);
  * returns 0, or a transport code that error_string explains. The calls
  * between group_start and group_end belong to one phase and may be fused.
  * reduce_scatter sums count elements per rank (op, dt as the exchange's own
- * kernels define them) and may refuse a dtype with a non-zero code; the
+ * kernels define them, or KF_TRANSPORT_OP_AVG) and may refuse a dtype or op
+ * with a non-zero code; the
  * AUTO algo never asks for an f16 / bf16 / u16 / i16 reduce-scatter. split
  * (ncclCommSplit's contract: collective over comm; ranks of one color form a
  * communicator ordered by key) is needed by kf_exchange_split and the named

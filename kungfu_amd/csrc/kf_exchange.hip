@@ -209,7 +209,8 @@ bool nccl_type(KungFu_Datatype dt, ncclDataType_t *t)
 
 ncclRedOp_t nccl_op(KungFu_Op op)
 {
-    switch (op) {
+    switch (static_cast<int>(op)) {
+    case KF_TRANSPORT_OP_AVG: return ncclAvg;
     case KungFu_MIN: return ncclMin;
     case KungFu_MAX: return ncclMax;
     case KungFu_PROD: return ncclProd;
@@ -398,6 +399,7 @@ struct kf_exchange {
     std::deque<std::string> nfresh;          // started, not yet reported to the peers
     std::map<std::pair<uint64_t, uint64_t>, std::string> nhash;  // outstanding names
     size_t nstarted = 0, nfinished = 0;
+    uint64_t anon_seq = 0;  // names of the anonymous (empty-name) calls, in call order
     int nstatus      = KF_OK;
     std::string nerr;
     bool nstop = false, nbroken = false, nready = false;
@@ -489,7 +491,7 @@ static int resolve_algo(int algo, KungFu_Datatype dt, KungFu_Op op, int world, i
 {
     ncclDataType_t t;
     const bool rs_ok = nccl_type(dt, &t);
-    if (algo == KF_ALGO_REDUCE_SCATTER) {
+    if (algo == KF_ALGO_REDUCE_SCATTER || algo == KF_ALGO_REDUCE_SCATTER_AVG) {
         if (!rs_ok) return fail(KF_ERR_DTYPE, "no reduce-scatter type for this dtype");
         *out = algo;
         return KF_OK;
@@ -539,6 +541,10 @@ int kf_exchange::batch(const void *const *sends, void *const *recvs, const size_
     int a  = 0;
     int rc = resolve_algo(algo, dt, op, W, &a);
     if (rc != KF_OK) return rc;
+    if (a == KF_ALGO_REDUCE_SCATTER_AVG && !average) a = KF_ALGO_REDUCE_SCATTER;
+    // the /np inside the collective (ncclAvg): no shard epilogue
+    const KungFu_Op rs_op =
+        a == KF_ALGO_REDUCE_SCATTER_AVG ? static_cast<KungFu_Op>(KF_TRANSPORT_OP_AVG) : op;
 
     // workspace: received shards (all-to-all) and gathered tails
     std::vector<size_t> wsoff(nb, 0), toff(nb, 0);
@@ -577,8 +583,8 @@ int kf_exchange::batch(const void *const *sends, void *const *recvs, const size_
             const char *snd = static_cast<const char *>(sends[b]);
             char *rcv       = static_cast<char *>(recvs[b]);
             int e           = 0;
-            if (q && a == KF_ALGO_REDUCE_SCATTER) {
-                e = T->reduce_scatter(snd, rcv + r * q * sz, q, dt, op, comm, s);
+            if (q && (a == KF_ALGO_REDUCE_SCATTER || a == KF_ALGO_REDUCE_SCATTER_AVG)) {
+                e = T->reduce_scatter(snd, rcv + r * q * sz, q, dt, rs_op, comm, s);
             } else if (q) {
                 e = T->all_to_all(snd, wsp + wsoff[b], q * sz, comm, s);
             }
@@ -1422,13 +1428,19 @@ kf_exchange_t *kf_exchange_create_local(kf_session_t *s, int device)
     }
     std::vector<int> host(size);
     (void)kf_session_hosts_internal(s, host.data());
-    const size_t bytes = static_cast<size_t>(hosts) * KF_UNIQUE_ID_BYTES;
+    // [every host's id][one status byte per host]: the host's first rank
+    // writes its host's id, or 1 in its host's status byte if it could not
+    // make one, so every rank of that host fails with the reason instead of
+    // calling the communicator init with an id that is all zeros
+    const size_t idbytes = static_cast<size_t>(hosts) * KF_UNIQUE_ID_BYTES;
+    const size_t bytes   = idbytes + static_cast<size_t>(hosts);
     std::vector<unsigned char> ids(bytes, 0);
     int rc = KF_OK;
     std::string why;
     if (lr == 0 && kf_exchange_unique_id(ids.data() + host[rank] * KF_UNIQUE_ID_BYTES) != KF_OK) {
-        why = t_ex_error;  // the host's peers still take part: they get zeros and fail in init
+        why = t_ex_error;
         rc  = KF_ERR_RCCL;
+        ids[idbytes + host[rank]] = 1;
     }
     // every host's id in one all-reduce: one contributor per slot, so the sum is the id
     int e = KF_OK;
@@ -1458,6 +1470,11 @@ kf_exchange_t *kf_exchange_create_local(kf_session_t *s, int device)
     }
     if (rc != KF_OK) {
         fail(rc, why);
+        return nullptr;
+    }
+    if (ids[idbytes + host[rank]] != 0) {
+        fail(KF_ERR_RCCL, "kf_exchange_create_local: this host's first rank could not create "
+                          "the RCCL id (its own error says why)");
         return nullptr;
     }
     return kf_exchange_create(ids.data() + host[rank] * KF_UNIQUE_ID_BYTES, lr, ls, device);
@@ -1657,7 +1674,7 @@ int kf_exchange_all_reduce_named(kf_exchange_t *ex, const char *name, const void
     size_t c = count;
     int rc   = check_bucket_args(ex, &send, &recv, &c, 1, dt, op, average);
     if (rc != KF_OK) return rc;
-    if (algo < KF_ALGO_AUTO || algo > KF_ALGO_ALL_TO_ALL) return fail(KF_ERR_ARG, "unknown algo");
+    if (algo < KF_ALGO_AUTO || algo > KF_ALGO_REDUCE_SCATTER_AVG) return fail(KF_ERR_ARG, "unknown algo");
     DeviceGuard g(ex->device);
     {
         std::lock_guard<std::mutex> lk(ex->mu);
@@ -1665,9 +1682,13 @@ int kf_exchange_all_reduce_named(kf_exchange_t *ex, const char *name, const void
         if (rc != KF_OK) return rc;
     }
     NamedTask t;
-    t.name    = name;
-    t.h1      = fnv1a(name, 0xcbf29ce484222325ull);
-    t.h2      = fnv1a(name, 0x6c62272e07bb0142ull) ^ (t.name.size() * 0x9e3779b97f4a7c15ull);
+    t.name = name;
+    if (t.name.empty()) {  // the blocking op's anonymous call: paired by call order
+        std::lock_guard<std::mutex> lk(ex->nmu);
+        t.name = "::anon::" + std::to_string(ex->anon_seq++);
+    }
+    t.h1 = fnv1a(t.name.c_str(), 0xcbf29ce484222325ull);
+    t.h2 = fnv1a(t.name.c_str(), 0x6c62272e07bb0142ull) ^ (t.name.size() * 0x9e3779b97f4a7c15ull);
     t.send    = send;
     t.recv    = recv;
     t.count   = count;
@@ -1688,9 +1709,9 @@ int kf_exchange_all_reduce_named(kf_exchange_t *ex, const char *name, const void
     if (ex->nbroken) {
         rc = fail(KF_ERR_RCCL, "the name negotiation has failed on this exchange");
     } else if (ex->nwait.count(t.name)) {
-        rc = fail(KF_ERR_ARG, std::string("name already outstanding: ") + name);
+        rc = fail(KF_ERR_ARG, "name already outstanding: " + t.name);
     } else if (ex->nhash.count({t.h1, t.h2})) {
-        rc = fail(KF_ERR_ARG, std::string("name hash collides with an outstanding name: ") + name);
+        rc = fail(KF_ERR_ARG, "name hash collides with an outstanding name: " + t.name);
     }
     if (rc != KF_OK) {
         (void)hipEventDestroy(t.ready);

@@ -382,6 +382,17 @@ struct Lease {
     size_t cap = 0;
 };
 
+// The leases of one kind: the idle ones, and how many bytes are lent out. The
+// pool never holds more than `cap` bytes (idle + lent): a call that would
+// need more goes without (the k-input fold falls back to the chain of
+// 2-input folds, the mirror to the D2H send), so memory does not grow with the
+// number of calls in flight (KUNGFU_AMD_STAGE_CAP_MB, KUNGFU_AMD_MIRROR_CAP_MB).
+struct LeasePool {
+    std::vector<Lease> idle;
+    size_t lent = 0, idle_bytes = 0;
+    size_t cap  = 0;
+};
+
 // Host mode: one received chunk body to fold into RecvBuf on a worker thread
 // (the reference's recvOnto runs on the chunk's own goroutine, session.go:317-
 // 323, execution.go:13-25), so the poll thread reads the next message while it
@@ -486,7 +497,7 @@ struct kf_session {
     //    over PCIe while it reads — so the sender has no D2H to wait for; the
     //    node's own HBM copy follows as an H2D off the critical path.
     //    KUNGFU_AMD_ROOT_MIRROR=0 turns it off (A/B).
-    std::vector<Lease> stage_pool, mirror_pool;
+    LeasePool stage_pool, mirror_pool;
     bool mirror        = true;
     int device         = 0;        // device mode: the GPU the session was created on
     char *barrier_dev  = nullptr;  // device mode: the barrier's zeroed u8 workspace
@@ -594,8 +605,8 @@ struct kf_session {
         for (auto e : tx_done) (void)hipEventDestroy(e);
         for (auto e : ev_pool) (void)hipEventDestroy(e);
         if (tx_stream) (void)hipStreamDestroy(tx_stream);
-        for (auto &l : stage_pool) (void)hipFree(l.p);
-        for (auto &l : mirror_pool) (void)hipHostFree(l.p);
+        for (auto &l : stage_pool.idle) (void)hipFree(l.p);
+        for (auto &l : mirror_pool.idle) (void)hipHostFree(l.p);
         if (barrier_dev) (void)hipFree(barrier_dev);
         if (wake_fd >= 0) ::close(wake_fd);
     }
@@ -948,30 +959,41 @@ struct kf_session {
     void fold_loop();
     void start_fold(SessOp &o, size_t i);
     void retire_folds();
-    bool take(std::vector<Lease> &pool, size_t need, bool host, Lease *out);
-    void give(std::vector<Lease> &pool, Lease &l);
+    bool take(LeasePool &pool, size_t need, bool host, Lease *out);
+    void give(LeasePool &pool, Lease &l);
 };
 
 enum { kAllReduce = 0, kReduce = 1, kBroadcast = 2 };
 
-// A buffer of at least `need` bytes from the pool (the smallest that fits); if
-// none fits, the idle ones are freed (their collectives completed, streams
-// synchronized) and one of exactly `need` bytes is allocated.
-bool kf_session::take(std::vector<Lease> &pool, size_t need, bool host, Lease *out)
+// A buffer of at least `need` bytes from the pool: the smallest idle one that
+// fits; else a new one of exactly `need` bytes, after freeing idle ones
+// (largest first) only as far as the pool's cap requires. false: no buffer
+// within the cap, or the allocation failed — the caller goes without.
+bool kf_session::take(LeasePool &pool, size_t need, bool host, Lease *out)
 {
     int best = -1;
-    for (size_t i = 0; i < pool.size(); ++i) {
-        if (pool[i].cap >= need && (best < 0 || pool[i].cap < pool[best].cap)) {
+    for (size_t i = 0; i < pool.idle.size(); ++i) {
+        if (pool.idle[i].cap >= need && (best < 0 || pool.idle[i].cap < pool.idle[best].cap)) {
             best = static_cast<int>(i);
         }
     }
     if (best >= 0) {
-        *out = pool[best];
-        pool.erase(pool.begin() + best);
+        *out = pool.idle[best];
+        pool.idle.erase(pool.idle.begin() + best);
+        pool.idle_bytes -= out->cap;
+        pool.lent += out->cap;
         return true;
     }
-    for (auto &l : pool) host ? (void)hipHostFree(l.p) : (void)hipFree(l.p);
-    pool.clear();
+    if (need > pool.cap || pool.lent + need > pool.cap) return false;
+    // idle buffers are too small: free the largest until the new one fits
+    std::sort(pool.idle.begin(), pool.idle.end(),
+              [](const Lease &a, const Lease &b) { return a.cap < b.cap; });
+    while (!pool.idle.empty() && pool.lent + pool.idle_bytes + need > pool.cap) {
+        Lease &l = pool.idle.back();
+        host ? (void)hipHostFree(l.p) : (void)hipFree(l.p);
+        pool.idle_bytes -= l.cap;
+        pool.idle.pop_back();
+    }
     Lease l;
     if (host) {
         void *dv = nullptr;
@@ -988,13 +1010,18 @@ bool kf_session::take(std::vector<Lease> &pool, size_t need, bool host, Lease *o
         l.dev = l.p;
     }
     l.cap = need;
-    *out  = l;
+    pool.lent += need;
+    *out = l;
     return true;
 }
 
-void kf_session::give(std::vector<Lease> &pool, Lease &l)
+void kf_session::give(LeasePool &pool, Lease &l)
 {
-    if (l.p) pool.push_back(l);
+    if (l.p) {
+        pool.idle.push_back(l);
+        pool.idle_bytes += l.cap;
+        pool.lent -= l.cap;
+    }
     l = Lease{};
 }
 
@@ -1056,7 +1083,9 @@ int kf_session::plan(SessOp &o)
         if (c.batched && c.pending_reduce * o.bytes > need_stage) need_stage = c.pending_reduce * o.bytes;
     }
     if (need_stage > 0 && !take(stage_pool, need_stage, false, &o.stage)) {
-        return fail(KF_ERR_HIP, "hipMalloc staging for the k-input fold");
+        // no staging within the cap: this call folds chunk by chunk as the
+        // reference does (recvOnto per predecessor), same bits
+        for (auto &c : o.chunks) c.batched = false;
     }
     // the fold that completes a chunk goes to the page-locked mirror when the
     // chunk then leaves this node (reduce successors, or bcast successors of a
@@ -1698,6 +1727,14 @@ kf_session_t *create_session(int rank, std::vector<PeerAddr> peers, const char *
         s->strategy = st;
     }
     if (const char *e = std::getenv("KUNGFU_AMD_BATCH_FOLD")) s->batch_fold = std::atoi(e) != 0;
+    s->stage_pool.cap  = size_t(8) << 30;  // HBM staging for k-input folds
+    s->mirror_pool.cap = size_t(2) << 30;  // page-locked mirrors
+    if (const char *e = std::getenv("KUNGFU_AMD_STAGE_CAP_MB")) {
+        s->stage_pool.cap = static_cast<size_t>(std::max(0L, std::atol(e))) << 20;
+    }
+    if (const char *e = std::getenv("KUNGFU_AMD_MIRROR_CAP_MB")) {
+        s->mirror_pool.cap = static_cast<size_t>(std::max(0L, std::atol(e))) << 20;
+    }
     if (const char *e = std::getenv("KUNGFU_CONFIG_STRATEGY_HASH_METHOD")) {
         s->hash_name = std::strcmp(e, "NAME") == 0 || std::strcmp(e, "name") == 0;
     }

@@ -55,7 +55,6 @@ namespace
 kf_exchange_t *g_ex = nullptr;              // init_exchange's (Peer::GetDefault)
 thread_local kf_exchange_t *t_ex = nullptr; // bind_exchange's, this thread only
 std::mutex g_mu;
-std::map<kf_exchange_t *, uint64_t> g_sync_seq;
 
 struct Pending {
     std::mutex m;
@@ -218,9 +217,10 @@ void bind_exchange(uintptr_t handle) { t_ex = reinterpret_cast<kf_exchange_t *>(
 void set_algo(const std::string &algo)
 {
     static const std::map<std::string, int> m = {
-        {"auto", KF_ALGO_AUTO}, {"rs", KF_ALGO_REDUCE_SCATTER}, {"a2a", KF_ALGO_ALL_TO_ALL}};
+        {"auto", KF_ALGO_AUTO}, {"rs", KF_ALGO_REDUCE_SCATTER}, {"a2a", KF_ALGO_ALL_TO_ALL},
+        {"rs_avg", KF_ALGO_REDUCE_SCATTER_AVG}};
     auto it = m.find(algo);
-    if (it == m.end()) throw std::runtime_error("kungfu_amd: algo must be auto, rs or a2a");
+    if (it == m.end()) throw std::runtime_error("kungfu_amd: algo must be auto, rs, a2a or rs_avg");
     g_algo = it->second;
 }
 
@@ -232,19 +232,16 @@ void finalize()
         (void)kf_exchange_wait_named(g_ex);
         kf_exchange_destroy(g_ex);
     }
-    g_sync_seq.erase(g_ex);
     g_ex = nullptr;
 }
 
+// the blocking op: an anonymous call, named by the exchange's own counter
+// (kf_exchange_all_reduce_named with ""), so the calls pair by their order on
+// every rank's exchange and a new exchange starts its count at zero
 void all_reduce_cuda(torch::Tensor input, torch::Tensor output, const std::string &type,
                      const std::string &op_name)
 {
-    std::string name;
-    {
-        std::lock_guard<std::mutex> lk(g_mu);
-        name = "::sync::" + std::to_string(g_sync_seq[current()]++);
-    }
-    wait(start(input, output, type, op_name, name));
+    wait(start(input, output, type, op_name, ""));
 }
 
 int all_reduce_cuda_async(torch::Tensor input, torch::Tensor output, const std::string &type,

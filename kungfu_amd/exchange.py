@@ -13,6 +13,9 @@ buckets to ONE native call:
   algo="auto" rs for integers and f32/f64, a2a for f16/bf16 (the build's
               defined semantics: bf16 accumulates in fp32 and rounds once,
               bit-identical to the P2P exchange and the oracle)
+  algo="rs_avg" (opt-in) average calls as ncclReduceScatter(ncclAvg) ->
+              ncclAllGather, no HIP epilogue: rs's bits when the world is a
+              power of two and no x / world is subnormal
 
 Each phase of a call is one grouped RCCL launch and all shard epilogues one
 batched HIP launch, so a step of 64 buckets costs 3 launches whatever the
@@ -28,7 +31,7 @@ from . import _lib
 from .base import OP, OP_NAMES
 from .ops import kungfu_dtype
 
-ALGOS = {"auto": 0, "rs": 1, "a2a": 2}
+ALGOS = {"auto": 0, "rs": 1, "a2a": 2, "rs_avg": 3}
 # kf_exchange_phase_times' order: phase 1 (reduce-scatter, or all-to-all for
 # the rank-order fold), phase 2 (/np epilogue or the fold), phase 3
 # (all-gather), the SMA blend

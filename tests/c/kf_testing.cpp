@@ -63,6 +63,17 @@ template <typename T>
 void host_fold(const std::vector<std::vector<char>> &in, size_t off, size_t n, KungFu_Op op,
                char *out)
 {
+    if (static_cast<int>(op) == KF_TRANSPORT_OP_AVG) {  // ncclAvg's float form: premultiply
+        const T w = static_cast<T>(1) / static_cast<T>(in.size());
+        for (size_t i = 0; i < n; ++i) {
+            T a = reinterpret_cast<const T *>(in[0].data() + off)[i] * w;
+            for (size_t j = 1; j < in.size(); ++j) {
+                a = static_cast<T>(a + reinterpret_cast<const T *>(in[j].data() + off)[i] * w);
+            }
+            reinterpret_cast<T *>(out)[i] = a;
+        }
+        return;
+    }
     for (size_t i = 0; i < n; ++i) {
         T a = reinterpret_cast<const T *>(in[0].data() + off)[i];
         for (size_t j = 1; j < in.size(); ++j) {
@@ -119,6 +130,9 @@ int lb_reduce_scatter(const void *send, void *recv, size_t count, KungFu_Datatyp
         if (dt == KungFu_FLOAT16 || dt == KungFu_BFLOAT16 || dt == KungFu_UINT16 ||
             dt == KungFu_INT16) {
             return int(LB_DTYPE);
+        }
+        if (static_cast<int>(op) == KF_TRANSPORT_OP_AVG && dt != KungFu_FLOAT && dt != KungFu_DOUBLE) {
+            return int(LB_DTYPE);  // the loopback averages floats only
         }
         const size_t sz = dsize(dt), W = sd.size();
         std::vector<std::vector<char>> in(W, std::vector<char>(count * W * sz));
@@ -309,7 +323,8 @@ int r1_rs(const void *s, void *r, size_t n, KungFu_Datatype dt, KungFu_Op op, vo
 {
     ncclDataType_t t;
     if (!ntype(dt, &t)) return ncclInvalidArgument;
-    const ncclRedOp_t o = op == KungFu_MIN ? ncclMin : op == KungFu_MAX ? ncclMax
+    const ncclRedOp_t o = static_cast<int>(op) == KF_TRANSPORT_OP_AVG ? ncclAvg
+                          : op == KungFu_MIN ? ncclMin : op == KungFu_MAX ? ncclMax
                           : op == KungFu_PROD ? ncclProd : ncclSum;
     return rcl()->ReduceScatter(s, r, n, t, o, C(c), S(st));
 }

@@ -84,6 +84,7 @@ x = torch.randn(n, device=dev, generator=torch.Generator(device=dev).manual_seed
 res = {
     "c4": bench.bench_c4(1, 0, dev, 3, 1, exchange="native"),
     "c4_pipe": bench.bench_c4(1, 0, dev, 3, 1, exchange="native_pipe"),
+    "c4_rs_avg": bench.bench_c4(1, 0, dev, 3, 1, exchange="native_rs_avg"),
     "c5": bench.bench_c5(1, 0, dev, 3, 1, exchange="native"),
     "c5_pipe": bench.bench_c5(1, 0, dev, 3, 1, exchange="native_pipe"),
     "c5_overlap": bench.bench_c5_overlap(1, 0, dev, 3, 1),
@@ -140,7 +141,8 @@ def test_bench_exchange_branch_single_rank_rccl():
         pytest.skip("no GPU")
     env = dict(os.environ, MASTER_ADDR="127.0.0.1",
                MASTER_PORT=str(_port()), RANK="0", LOCAL_RANK="0", WORLD_SIZE="1")
-    extras = "c4,c5,c5_pipe,c5_overlap,c4_overlap,c4_pipe,c4_named,c3_pipe,c3_a2a,c3_fused,c4_torch,c5_torch"
+    extras = ("c4,c5,c5_pipe,c5_overlap,c4_overlap,c4_pipe,c4_rs_avg,c4_named,c3_pipe,c3_a2a,"
+              "c3_fused,c4_torch,c5_torch")
     argv = ["--rehearse-exchange", "--steps", "3", "--warmup", "1", "--elems", str(4 << 20),
             "--extras", extras, "--extras-timeout", "200"]
     code = _BRANCH_CHILD % (ROOT, os.path.join(ROOT, "tests"), argv)
@@ -156,7 +158,10 @@ def test_bench_exchange_branch_single_rank_rccl():
     assert d["value"] == d["collective"]["algbw_GiBps_per_gpu"]
     # the primary's schedule trial: every schedule parity-checked and timed
     trial = d["collective"]["schedule_trial_ms"]
-    assert sorted(trial) == ["a2a", "fused", "grouped", "pipelined"], trial
+    assert sorted(trial) == ["a2a", "fused", "grouped", "pipelined", "rs_avg"], trial
+    # the per-phase split of the timed step on the native exchange
+    ph = d["collective"]["phase_us"]
+    assert ph["timed_calls_per_step"] > 0 or ph.get("pipelined_calls_untimed"), ph
     assert all(v is not None and v > 0 for v in trial.values()), trial
     assert abs(d["value_aggregate"] - d["n_gpus"] * d["value"]) < 1e-2
     for k in extras.split(","):

@@ -258,6 +258,54 @@ def _loop_ranks(world, body):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("world,groups", [(2, 1), (4, 1), (4, 2), (3, 1)])
+def test_rs_avg_folds_the_division_into_the_collective(world, groups):
+    """KF_ALGO_REDUCE_SCATTER_AVG: the average's /np inside the reduce-scatter
+    (ncclAvg; the loopback premultiplies by 1/world and sums in rank order)
+    and no shard epilogue. At a power-of-two world it has the bits of the
+    rank-order sum then /np (the oracle's reduce_avg) for normal inputs; at
+    world 3 each input adds one rounding (|err| <= world * u * sum|x|/world
+    + u*|avg|). Tails (count % world) still take the rank-order fold with /np.
+    Non-average calls under it are plain reduce-scatters."""
+    import torch
+    from oracle import oracle
+    dev = _gpu()
+    counts = [world * 5000, world * 777 + 2, 1, world * 65536]
+
+    def body(rank, ex):
+        ex.set_pipeline(groups)
+        ex.algo = "rs_avg"
+        hs = [[_rand("f32", n, 40 * r + b) for b, n in enumerate(counts)] for r in range(world)]
+        bufs = [_to_dev(hs[rank][b], "f32", dev) for b in range(len(counts))]
+        ex.set_timing(True)
+        ex.all_reduce_(bufs, average=True, coalesce=False)
+        torch.cuda.synchronize()
+        ph = ex.phase_times()
+        ex.set_timing(False)
+        for b, n in enumerate(counts):
+            ins = [hs[r][b] for r in range(world)]
+            want = oracle.reduce_avg(ins, "f32", world)
+            got = _to_np(bufs[b], "f32")
+            if world & (world - 1) == 0:
+                assert np.array_equal(got, want), (b, n)
+            else:
+                u = 2.0 ** -24
+                absum = np.sum([np.abs(x.astype(np.float64)) for x in ins], axis=0)
+                bound = 2 * world * u * absum / world + 2 * u * np.abs(want.astype(np.float64))
+                assert np.all(np.abs(got.astype(np.float64) - want) <= bound + 1e-38), (b, n)
+        if groups == 1:
+            assert ph["calls"] == 1, ph
+        # a plain sum under rs_avg is the reduce-scatter's
+        xi = [_rand("i32", world * 999, 7 + r) for r in range(world)]
+        bi = _to_dev(xi[rank], "i32", dev)
+        ex.all_reduce_([bi], average=False)
+        torch.cuda.synchronize()
+        assert np.array_equal(_to_np(bi, "i32"), oracle.reduce_k(xi, "i32", "sum"))
+
+    _loop_ranks(world, body)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("algo", ["rs", "a2a"])
 def test_pipelined_failure_at_every_call_then_reusable(algo):
     """a transport failure at ANY collective of the

@@ -198,6 +198,31 @@ def test_session_device_strategies(strategy, size, batch_fold):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("strategy", ["STAR", "BINARY_TREE", "CLIQUE"])
+def test_session_device_lease_caps(strategy):
+    """HBM staging and page-locked mirrors come from
+    pools capped in bytes; a call that would pass the cap goes without (the
+    chain of 2-input folds, the D2H send) instead of failing. Caps of 1 MiB
+    refuse every lease of a 5 MiB bucket: same schedule, same bits."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    run(4, "device", "rand", (5 << 20) // 4 + 17, strategy=strategy,
+        env={"KUNGFU_AMD_STAGE_CAP_MB": "1", "KUNGFU_AMD_MIRROR_CAP_MB": "1"})
+
+
+@pytest.mark.gpu
+def test_session_async_any_order_device_capped():
+    """Calls in flight at once share the capped pools: some get staging and a
+    mirror, the rest fall back (12 MiB caps, six names of 1-6 chunks)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _run_any_order(3, "device", None, env={"KUNGFU_AMD_STAGE_CAP_MB": "12",
+                                           "KUNGFU_AMD_MIRROR_CAP_MB": "6"})
+
+
+@pytest.mark.gpu
 def test_session_device_batched_iota():
     # fake_agent.cpp:15-44 KAT (iota * np) through the k-input fold at np=4
     import torch
@@ -436,7 +461,7 @@ def test_session_async_device():
     _run_async(3, "device")
 
 
-def _any_order_body(rank, size, sock_dir, mode, strategy, errq, steps=2):
+def _any_order_body(rank, size, sock_dir, mode, strategy, errq, steps=2, env=None):
     """Every peer starts the same named all-reduces in its OWN random order,
     two steps of them back to back (a name's second call waits for its
     first; the peers' step-2 chunks wait in the stash meanwhile), as the
@@ -444,6 +469,7 @@ def _any_order_body(rank, size, sock_dir, mode, strategy, errq, steps=2):
     messages pair by name (handler/collective.go:48-64). Exact inputs (ints,
     and the C1 floats whose sums are exact in any order)."""
     sys.path[:0] = [ROOT, HERE]
+    os.environ.update(env or {})
     try:
         import time
         if strategy is not None:
@@ -485,11 +511,12 @@ def _any_order_body(rank, size, sock_dir, mode, strategy, errq, steps=2):
         errq.put("rank %d: %s" % (rank, traceback.format_exc()))
 
 
-def _run_any_order(size, mode, strategy=None, steps=2):
+def _run_any_order(size, mode, strategy=None, steps=2, env=None):
     ctx = mp.get_context("spawn")
     errq = ctx.SimpleQueue()
     with tempfile.TemporaryDirectory() as d:
-        ps = [ctx.Process(target=_any_order_body, args=(r, size, d, mode, strategy, errq, steps))
+        ps = [ctx.Process(target=_any_order_body,
+                          args=(r, size, d, mode, strategy, errq, steps, env))
               for r in range(size)]
         for p in ps:
             p.start()
