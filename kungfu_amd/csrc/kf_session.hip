@@ -50,6 +50,7 @@
 
 #include <algorithm>
 #include <cerrno>
+#include <chrono>
 #include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
@@ -372,6 +373,23 @@ struct SendItem {  // one chunk to every fd in `fds` (the node's successors)
                            // (the root's fold wrote it there): no D2H, send once
                            // `ready` has completed
     SessOp *owner = nullptr;  // the collective whose chunk this is
+    int chunk     = -1;       // its index in the collective (trace only)
+};
+
+// KUNGFU_AMD_SESSION_TRACE=<path>: every step of every chunk, timestamped,
+// written to <path>.<rank> as JSON lines when the session is destroyed
+// (tools/c1_trace.py reads them). Off: one branch per step.
+enum TraceTag {
+    TR_OP_START, TR_OP_DONE, TR_RX_HDR, TR_RX_DONE, TR_TX_QUEUED, TR_TX_STAGED, TR_TX_READY,
+    TR_TX_DONE, TR_FOLD_BEGIN, TR_FOLD_END, TR_NTAGS
+};
+const char *const kTraceNames[TR_NTAGS] = {"op_start", "op_done",  "rx_hdr",     "rx_done",
+                                           "tx_queued", "tx_staged", "tx_ready",  "tx_done",
+                                           "fold_begin", "fold_end"};
+struct TraceRec {
+    int64_t ns;
+    int tag, chunk, arg;
+    unsigned thr;  // 0 poll loop, 1 sender, 2 fold worker
 };
 
 // A buffer lent to one collective in flight: HBM staging for the k-input fold,
@@ -501,6 +519,31 @@ struct kf_session {
     bool mirror        = true;
     int device         = 0;        // device mode: the GPU the session was created on
     char *barrier_dev  = nullptr;  // device mode: the barrier's zeroed u8 workspace
+    // KUNGFU_AMD_SESSION_TRACE (see TraceRec)
+    std::string trace_path;
+    std::mutex tmu;
+    std::vector<TraceRec> trec;
+    void tr(int tag, int chunk, int arg, unsigned thr)
+    {
+        if (trace_path.empty()) return;
+        // CLOCK_MONOTONIC: one clock for every peer process on the host
+        const int64_t ns = std::chrono::duration_cast<std::chrono::nanoseconds>(
+                               std::chrono::steady_clock::now().time_since_epoch())
+                               .count();
+        std::lock_guard<std::mutex> l(tmu);
+        trec.push_back({ns, tag, chunk, arg, thr});
+    }
+    void dump_trace()
+    {
+        if (trace_path.empty()) return;
+        FILE *f = std::fopen((trace_path + "." + std::to_string(rank)).c_str(), "w");
+        if (!f) return;
+        for (const auto &r : trec) {
+            std::fprintf(f, "{\"t_us\": %.3f, \"ev\": \"%s\", \"chunk\": %d, \"arg\": %d, \"thr\": %u}\n",
+                         r.ns / 1e3, kTraceNames[r.tag], r.chunk, r.arg, r.thr);
+        }
+        std::fclose(f);
+    }
     std::deque<Stashed> stash;  // per-name mailbox for early messages
     std::mutex run_mu;          // one poll loop over the sockets at a time
     int wake_fd = -1;           // eventfd: a submission, or an op's last chunk sent
@@ -593,6 +636,7 @@ struct kf_session {
             cv_work.notify_all();
             sender.join();
         }
+        dump_trace();
         for (auto &kv : out_fd) ::close(kv.second);
         for (auto &kv : in_fd) ::close(kv.second);
         if (listen_unix >= 0) {
@@ -630,6 +674,7 @@ struct kf_session {
                     l.unlock();
                     const size_t slot = (first_slot + staged.size()) % nslot;
                     q.slot_ok = send_rc == KF_OK && stage_d2h(q, slot);
+                    tr(TR_TX_STAGED, q.chunk, static_cast<int>(q.flags), 1);
                     staged.push_back(std::move(q));
                     l.lock();
                 }
@@ -650,6 +695,7 @@ struct kf_session {
             } else if (send_rc == KF_OK) {
                 rc = send_item(it, &err);
             }
+            tr(TR_TX_DONE, it.chunk, static_cast<int>(it.flags), 1);
             bool last = false;
             {
                 std::lock_guard<std::mutex> l(mu);
@@ -699,6 +745,7 @@ struct kf_session {
             *err = "D2H of an outgoing chunk failed";
             return KF_ERR_HIP;
         }
+        tr(TR_TX_READY, it.chunk, static_cast<int>(it.flags), 1);
         const char *data = it.host ? it.ptr : static_cast<const char *>(tx[slot]);
         for (int fd : it.fds) {
             const int rc = kf_rch_send(fd, it.name.c_str(), it.flags, data,
@@ -750,6 +797,7 @@ struct kf_session {
 
     void enqueue(SendItem it)
     {
+        tr(TR_TX_QUEUED, it.chunk, static_cast<int>(it.flags), 0);
         {
             std::lock_guard<std::mutex> l(mu);
             if (it.owner) ++it.owner->sends;
@@ -1130,6 +1178,7 @@ void kf_session::send_chunk(SessOp &o, size_t i, std::vector<int> fds, uint32_t 
         SendItem it{fds, c.name, fl, cptr(o, o.mir.p, i), clen(o, i), o.stream, c.mirror_ev};
         it.host     = true;
         it.owner    = &o;
+        it.chunk    = static_cast<int>(i);
         c.mirror_ev = nullptr;
         enqueue(std::move(it));
         return;
@@ -1137,6 +1186,7 @@ void kf_session::send_chunk(SessOp &o, size_t i, std::vector<int> fds, uint32_t 
     SendItem it{fds, c.name, fl, effective(o, i), clen(o, i), o.stream,
                 device_mode ? chunk_ready(o.stream) : nullptr};
     it.owner = &o;
+    it.chunk = static_cast<int>(i);
     enqueue(std::move(it));
 }
 
@@ -1341,6 +1391,7 @@ void kf_session::fold_loop()
         }
         const KungFu_Datatype dt = j->o->dt;  // fixed for the collective's lifetime
         const KungFu_Op op       = j->o->op;
+        tr(TR_FOLD_BEGIN, static_cast<int>(j->i), 0, 2);
         if (host_fn) {
             if (host_fn(j->own, j->body->data(), j->dst, static_cast<int64_t>(j->n),
                         static_cast<int>(dt), static_cast<int>(op)) != 0) {
@@ -1351,6 +1402,7 @@ void kf_session::fold_loop()
             j->rc = kf_transform2_host(j->own, j->body->data(), j->dst, j->n, dt, op);
             if (j->rc != KF_OK) j->err = kf_last_error();
         }
+        tr(TR_FOLD_END, static_cast<int>(j->i), j->rc, 2);
         {
             std::lock_guard<std::mutex> l(fmu);
             fdone.push_back(j);
@@ -1434,6 +1486,7 @@ int kf_session::run(SessOp *one)
         }
     };
     auto start = [&](SessOp *o) {
+        tr(TR_OP_START, -1, static_cast<int>(o->count), 0);
         t_sess_error.clear();
         o->rc = plan(*o);
         if (o->rc != KF_OK) {
@@ -1577,6 +1630,7 @@ int kf_session::run(SessOp *one)
             }
             t_sess_error = o->err;
             const int rc = complete(*o);
+            tr(TR_OP_DONE, -1, rc, 0);
             if (o == one) {
                 if (rc != KF_OK) t_sess_error = o->err;
                 return rc;
@@ -1665,7 +1719,10 @@ int kf_session::run(SessOp *one)
             const int peer = pfd_peer[q];
             auto it        = index.find(hname);
             if (it != index.end() && expects(*it->second.first, it->second.second, flags, peer)) {
+                const int ci = static_cast<int>(it->second.second);
+                tr(TR_RX_HDR, ci, static_cast<int>(flags), 0);
                 rc = handle(*it->second.first, it->second.second, flags, peer, fd, nullptr);
+                tr(TR_RX_DONE, ci, static_cast<int>(flags), 0);
                 continue;
             }
             // not ours (yet): keep it for the call it belongs to
@@ -1727,6 +1784,7 @@ kf_session_t *create_session(int rank, std::vector<PeerAddr> peers, const char *
         s->strategy = st;
     }
     if (const char *e = std::getenv("KUNGFU_AMD_BATCH_FOLD")) s->batch_fold = std::atoi(e) != 0;
+    if (const char *e = std::getenv("KUNGFU_AMD_SESSION_TRACE")) s->trace_path = e;
     s->stage_pool.cap  = size_t(8) << 30;  // HBM staging for k-input folds
     s->mirror_pool.cap = size_t(2) << 30;  // page-locked mirrors
     if (const char *e = std::getenv("KUNGFU_AMD_STAGE_CAP_MB")) {

@@ -6,6 +6,7 @@
 #   bash tools/gpu_r04.sh <tag> bench     # bench.py N=1 (default line)
 #   bash tools/gpu_r04.sh <tag> bench2    # bench.py --gpus 2 rehearsal (self-launch, gloo)
 #   bash tools/gpu_r04.sh <tag> asan      # host-code ASan of the C++ hosts
+#   bash tools/gpu_r04.sh <tag> c1trace   # C1 np=2 per-chunk timelines (device, cpu)
 set -u
 TAG=${1:?tag}
 shift
@@ -52,6 +53,9 @@ or hier_all_reduce or fake_agent or rehearsal or branch_single_rank"
   asan)
     step asan_build 600 bash tools/sanitize_gpu_hosts.sh build || exit $?
     step asan 900 bash tools/sanitize_gpu_hosts.sh run || exit $? ;;
+  c1trace)
+    step c1trace 600 python tools/c1_trace.py --modes device,cpu --steps 60 \
+        --out "$OUT/c1_trace.json" || exit $? ;;
   *) echo "unknown stage $stage"; exit 2 ;;
   esac
 done
