@@ -18,7 +18,10 @@ package base
 // #include "kungfu_amd.h"
 import "C"
 
-import "unsafe"
+import (
+	"fmt"
+	"unsafe"
+)
 
 type OP C.KungFu_Op
 
@@ -49,4 +52,16 @@ func Transform2(z, x, y *Vector, op OP) {
 		unsafe.Pointer(&y.Data[0]),
 		unsafe.Pointer(&z.Data[0]),
 		C.int(z.Count), C.KungFu_Datatype(z.Type), C.KungFu_Op(op))
+}
+
+// Shutdown gives the library's HIP resources (the scratch and streams that
+// Transform2 borrows per call) back while the HIP runtime is still up; call
+// it once no Transform2 is running, e.g. before main returns. No library
+// destructor calls HIP at exit, so a program that never calls it leaves them
+// to the OS (include/kungfu_amd.h kf_shutdown).
+func Shutdown() error {
+	if rc := C.kf_shutdown(); rc != C.KF_OK {
+		return fmt.Errorf("kf_shutdown: %s", C.GoString(C.kf_last_error()))
+	}
+	return nil
 }
