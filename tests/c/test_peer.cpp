@@ -16,7 +16,6 @@
 #include <numeric>
 #include <vector>
 
-#include "asan_drain.h"
 #include "kungfu_amd.hpp"
 
 using kungfu_amd::Peer;
@@ -107,7 +106,6 @@ int main(int argc, char **argv)
         std::printf("kf_shutdown: %s\n", kf_last_error());
         return 1;
     }
-    kf_asan_drain_quarantine();
     std::printf("peer ok (%d of %d, %s)\n", rank, size, device ? "device" : "host");
     return 0;
 }

@@ -38,7 +38,17 @@ run)
     # included: the library no longer calls HIP from a destructor, and the
     # hosts call kf_shutdown() before main returns). The raw log of every
     # failing host is kept under gpurun_out/sanitize_logs/.
-    export ASAN_OPTIONS="detect_leaks=0 halt_on_error=1 protect_shadow_gap=0"
+    # quarantine_size_mb=0: ASan's quarantine also holds the chunks of its
+    # DEVICE allocator (every hipFree of the run); the HIP runtime's own
+    # teardown in libamdhip64's __cxa_finalize unloads HSA and then frees host
+    # objects, and a device chunk pushed out of the quarantine by such a free
+    # trips "CHECK !dev_runtime_unloaded_" with no frame of this project on
+    # the stack (raw logs: profiles/r04/asan_check_r04c.log,
+    # asan_check_r04d_test_hier.log — the second after the hosts had cycled
+    # the quarantine themselves before returning). Without a quarantine every
+    # free is final at once, while the runtime is up; freed memory stays
+    # poisoned until it is reused.
+    export ASAN_OPTIONS="detect_leaks=0 halt_on_error=1 protect_shadow_gap=0 quarantine_size_mb=0 thread_local_quarantine_size_kb=0"
     export TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1 suppressions=$ROOT/tools/tsan_rocm.supp"
     KEEP="$ROOT/gpurun_out/sanitize_logs"
     cd "$D"
