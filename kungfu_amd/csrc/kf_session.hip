@@ -460,6 +460,7 @@ struct SessOp {
     const std::vector<Strategy> *L = nullptr;
     size_t isz = 0, bytes = 0;
     bool inplace = false, may_forward = true, use_mirror = false, trivial = false;
+    bool mir_side = false;  // a mirror's copy to HBM went to the session's side stream
     Strategy single{Graph(0), Graph(0)};
     std::vector<std::pair<size_t, size_t>> parts;
     std::vector<SessChunk> chunks;
@@ -491,7 +492,9 @@ struct kf_session {
     // path of the one before it (KUNGFU_AMD_TX_SLOTS, 1 = copy, send, copy...)
     std::vector<void *> tx;
     std::vector<hipEvent_t> tx_done;  // one per slot: its D2H has landed
-    hipStream_t tx_stream = nullptr;  // sender's D2H stream
+    size_t tx_ahead = 2;              // D2H issued ahead of the write (KUNGFU_AMD_TX_AHEAD)
+    hipStream_t tx_stream  = nullptr;  // sender's D2H stream
+    hipStream_t mir_stream = nullptr;  // the bcast root's mirror -> HBM copies
     std::vector<hipEvent_t> ev_pool;  // free "chunk is final" events
     std::mutex ev_mu;
     kf_host_reduce_fn host_fn = nullptr;
@@ -649,6 +652,7 @@ struct kf_session {
         for (auto e : tx_done) (void)hipEventDestroy(e);
         for (auto e : ev_pool) (void)hipEventDestroy(e);
         if (tx_stream) (void)hipStreamDestroy(tx_stream);
+        if (mir_stream) (void)hipStreamDestroy(mir_stream);
         for (auto &l : stage_pool.idle) (void)hipFree(l.p);
         for (auto &l : mirror_pool.idle) (void)hipHostFree(l.p);
         if (barrier_dev) (void)hipFree(barrier_dev);
@@ -667,8 +671,11 @@ struct kf_session {
             {
                 std::unique_lock<std::mutex> l(mu);
                 if (staged.empty()) cv_work.wait(l, [&] { return stopping || !queue.empty(); });
-                // issue the D2H of every queued chunk that has a free slot
-                while (device_mode && staged.size() < nslot && !queue.empty()) {
+                // issue the D2H of queued chunks into free slots, at most
+                // tx_ahead of them before the oldest is written: a D2H takes a
+                // fraction of a socket write, and every D2H issued first delays
+                // the first write by its host-side cost
+                while (device_mode && staged.size() < std::min(nslot, tx_ahead) && !queue.empty()) {
                     SendItem q = queue.front();
                     queue.pop_front();
                     l.unlock();
@@ -1191,16 +1198,23 @@ void kf_session::send_chunk(SessOp &o, size_t i, std::vector<int> fds, uint32_t 
 }
 
 // after the completing fold into the mirror: its end marks the chunk final
-// for the sender; then this node's own copy of it goes to HBM
+// for the sender; then this node's own copy of it goes to HBM. At the bcast
+// root nothing writes that chunk of dst again in this call, so the copy runs
+// on the session's side stream: the next chunk's fold on the caller's stream
+// does not queue behind it (complete() waits for both streams)
 int kf_session::mirror_done(SessOp &o, size_t i, char *dst)
 {
     auto &c     = o.chunks[i];
     c.mirror_ev = chunk_ready(o.stream);
-    if (!c.mirror_ev ||
-        hipMemcpyAsync(dst, cptr(o, o.mir.p, i), clen(o, i), hipMemcpyHostToDevice,
-                       static_cast<hipStream_t>(o.stream)) != hipSuccess) {
+    if (!c.mirror_ev) return fail(KF_ERR_HIP, "mirror event");
+    const bool side = mir_stream && c.st->bcast.prev[rank].empty();
+    hipStream_t hs  = side ? mir_stream : static_cast<hipStream_t>(o.stream);
+    if ((side && hipStreamWaitEvent(mir_stream, c.mirror_ev, 0) != hipSuccess) ||
+        hipMemcpyAsync(dst, cptr(o, o.mir.p, i), clen(o, i), hipMemcpyHostToDevice, hs) !=
+            hipSuccess) {
         return fail(KF_ERR_HIP, "mirror copy to HBM");
     }
+    if (side) o.mir_side = true;
     return KF_OK;
 }
 
@@ -1433,6 +1447,9 @@ int kf_session::complete(SessOp &o)
         if (irc != KF_OK && rc == KF_OK) rc = fail(irc, kf_ingest_last_error());
         if (hipStreamSynchronize(static_cast<hipStream_t>(o.stream)) != hipSuccess && rc == KF_OK) {
             rc = fail(KF_ERR_HIP, "stream sync");
+        }
+        if (o.mir_side && hipStreamSynchronize(mir_stream) != hipSuccess && rc == KF_OK) {
+            rc = fail(KF_ERR_HIP, "mirror stream sync");
         }
     }
     for (auto &c : o.chunks) {  // a failed collective may leave a mirror event unsent
@@ -1809,6 +1826,9 @@ kf_session_t *create_session(int rank, std::vector<PeerAddr> peers, const char *
         int nslot = 4;
         if (const char *e = std::getenv("KUNGFU_AMD_TX_SLOTS")) nslot = std::max(1, std::atoi(e));
         if (const char *e = std::getenv("KUNGFU_AMD_ROOT_MIRROR")) s->mirror = std::atoi(e) != 0;
+        if (const char *e = std::getenv("KUNGFU_AMD_TX_AHEAD")) {
+            s->tx_ahead = static_cast<size_t>(std::max(1, std::atoi(e)));
+        }
         bool tx_ok = true;
         for (int i = 0; i < nslot && tx_ok; ++i) {
             void *p      = nullptr;
@@ -1820,6 +1840,9 @@ kf_session_t *create_session(int rank, std::vector<PeerAddr> peers, const char *
         }
         if (hipStreamCreateWithFlags(&s->tx_stream, hipStreamNonBlocking) != hipSuccess) {
             s->tx_stream = nullptr;
+        }
+        if (hipStreamCreateWithFlags(&s->mir_stream, hipStreamNonBlocking) != hipSuccess) {
+            s->mir_stream = nullptr;  // the copies stay on the caller's stream
         }
         if (!s->ingest || !tx_ok || !s->tx_stream) {
             t_sess_error = "kf_ingest_create failed";

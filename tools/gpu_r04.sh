@@ -53,6 +53,14 @@ or hier_all_reduce or fake_agent or rehearsal or branch_single_rank"
   asan)
     step asan_build 600 bash tools/sanitize_gpu_hosts.sh build || exit $?
     step asan 900 bash tools/sanitize_gpu_hosts.sh run || exit $? ;;
+  session)
+    step session_tests 900 $PYT tests/test_session.py tests/test_session_multihost.py \
+        tests/test_hierarchical.py tests/test_c_consumer.py
+    fatal $? ;;
+  c1)
+    step c1 600 python bench.py --config c1 --c1-modes device,cpu,cpu_dev --c1-repeats 5 \
+        --steps 100 --warmup 10 || exit $?
+    tail -1 "$OUT/c1.log" > "$OUT/c1.json" ;;
   c1trace)
     step c1trace 600 python tools/c1_trace.py --modes device,cpu --steps 60 \
         --out "$OUT/c1_trace.json" || exit $? ;;
