@@ -1841,7 +1841,9 @@ kf_session_t *create_session(int rank, std::vector<PeerAddr> peers, const char *
         if (hipStreamCreateWithFlags(&s->tx_stream, hipStreamNonBlocking) != hipSuccess) {
             s->tx_stream = nullptr;
         }
-        if (hipStreamCreateWithFlags(&s->mir_stream, hipStreamNonBlocking) != hipSuccess) {
+        const char *ms = std::getenv("KUNGFU_AMD_MIRROR_SIDE");  // 0: A/B, caller's stream
+        if ((!ms || std::atoi(ms) != 0) &&
+            hipStreamCreateWithFlags(&s->mir_stream, hipStreamNonBlocking) != hipSuccess) {
             s->mir_stream = nullptr;  // the copies stay on the caller's stream
         }
         if (!s->ingest || !tx_ok || !s->tx_stream) {
