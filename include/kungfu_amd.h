@@ -261,6 +261,18 @@ int kf_ingest_recv_onto(kf_ingest_t *g, int fd, uint32_t len, void *dev_acc,
  * page-locked slot and queue its copy into dev_dst on `stream`. */
 int kf_ingest_recv_into(kf_ingest_t *g, int fd, uint32_t len, void *dev_dst,
                         void *stream);
+/* The same two steps with the body read in pieces of piece_bytes (a multiple
+ * of the element size): each piece's fold (or copy) is queued on `stream` as
+ * soon as that piece has been read, so the device work of a chunk overlaps
+ * the rest of its socket read. piece_events (hipEvent_t handles, may be NULL;
+ * at least ceil(len / piece_bytes) of them) gets event k recorded after piece
+ * k's fold. Element-wise, so the bits equal the whole-chunk call's. */
+int kf_ingest_recv_onto_pieces(kf_ingest_t *g, int fd, uint32_t len, void *dev_acc,
+                               const void *dev_own, size_t count, KungFu_Datatype dt,
+                               KungFu_Op op, void *stream, uint32_t piece_bytes,
+                               void *const *piece_events, int n_events);
+int kf_ingest_recv_into_pieces(kf_ingest_t *g, int fd, uint32_t len, void *dev_dst,
+                               void *stream, uint32_t piece_bytes);
 /* sendOnto/sendInto from the device: copy bytes of dev_src (after the work
  * queued on `stream`) to a page-locked slot and send it as one message. */
 int kf_ingest_send_from_device(kf_ingest_t *g, int fd, const char *name,

@@ -38,6 +38,8 @@ EXPORTED = (
     "kf_ingest_destroy",
     "kf_ingest_recv_onto",
     "kf_ingest_recv_into",
+    "kf_ingest_recv_onto_pieces",
+    "kf_ingest_recv_into_pieces",
     "kf_ingest_send_from_device",
     "kf_ingest_fold_host",
     "kf_ingest_copy_host",

@@ -26,6 +26,7 @@
 #include <sys/uio.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -300,6 +301,83 @@ int kf_ingest_recv_into(kf_ingest_t *g, int fd, uint32_t len, void *dev_dst,
     if (rc != KF_OK || len == 0) return rc;
     hipStream_t s = static_cast<hipStream_t>(stream);
     ING_HIP(hipMemcpyAsync(dev_dst, g->host[slot], len, hipMemcpyHostToDevice, s));
+    ING_HIP(hipEventRecord(g->done[slot], s));
+    {
+        std::lock_guard<std::mutex> lock(g->mu);
+        g->armed[slot] = true;
+    }
+    return KF_OK;
+}
+
+// The body in pieces: piece k's device work is queued as soon as it is read,
+// so a chunk's fold / copy overlaps the rest of its socket read; the last
+// piece's work ends shortly after the last byte instead of a whole chunk's
+// work after it. The operation is element-wise, so the bits are those of one
+// launch over the chunk.
+int kf_ingest_recv_onto_pieces(kf_ingest_t *g, int fd, uint32_t len, void *dev_acc,
+                               const void *dev_own, size_t count, KungFu_Datatype dt,
+                               KungFu_Op op, void *stream, uint32_t piece_bytes,
+                               void *const *piece_events, int n_events)
+{
+    if (!g || !dev_acc) return KF_ERR_ARG;
+    if (len > g->slot_bytes) return proto_fail("chunk larger than ingest slot");
+    const uint32_t sz = kungfu_type_size(dt);
+    if (static_cast<size_t>(len) != count * sz) return proto_fail("chunk length != count * type size");
+    if (piece_bytes == 0 || piece_bytes % sz) return KF_ERR_ARG;
+    const uint32_t npieces = len == 0 ? 0 : (len + piece_bytes - 1) / piece_bytes;
+    if (piece_events && static_cast<uint32_t>(n_events) < npieces) return KF_ERR_ARG;
+    int slot;
+    int rc = g->take(&slot);
+    if (rc != KF_OK) return rc;
+    unsigned char a[4];
+    rc = read_full(fd, a, 4);
+    if (rc != KF_OK) return rc;
+    if (get_u32(a) != len) return proto_fail("unexpected message length");
+    hipStream_t s   = static_cast<hipStream_t>(stream);
+    char *host      = static_cast<char *>(g->host[slot]);
+    const char *dev = static_cast<const char *>(g->hmap[slot]);
+    const char *own = static_cast<const char *>(dev_own ? dev_own : dev_acc);
+    char *acc       = static_cast<char *>(dev_acc);
+    for (uint32_t k = 0; k < npieces; ++k) {
+        const uint32_t off = k * piece_bytes;
+        const uint32_t pl  = std::min(piece_bytes, len - off);
+        rc = read_full(fd, host + off, pl);
+        if (rc != KF_OK) return rc;
+        const void *ins[2] = {own + off, dev + off};
+        rc = kf_bucket_reduce(ins, 2, acc + off, pl / sz, dt, op, stream);
+        if (rc != KF_OK) return rc;
+        if (piece_events) ING_HIP(hipEventRecord(static_cast<hipEvent_t>(piece_events[k]), s));
+    }
+    ING_HIP(hipEventRecord(g->done[slot], s));
+    {
+        std::lock_guard<std::mutex> lock(g->mu);
+        g->armed[slot] = true;
+    }
+    return KF_OK;
+}
+
+int kf_ingest_recv_into_pieces(kf_ingest_t *g, int fd, uint32_t len, void *dev_dst,
+                               void *stream, uint32_t piece_bytes)
+{
+    if (!g || (!dev_dst && len > 0) || piece_bytes == 0) return KF_ERR_ARG;
+    if (len > g->slot_bytes) return proto_fail("chunk larger than ingest slot");
+    int slot;
+    int rc = g->take(&slot);
+    if (rc != KF_OK) return rc;
+    unsigned char a[4];
+    rc = read_full(fd, a, 4);
+    if (rc != KF_OK) return rc;
+    if (get_u32(a) != len) return proto_fail("unexpected message length");
+    if (len == 0) return KF_OK;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    char *host    = static_cast<char *>(g->host[slot]);
+    char *dst     = static_cast<char *>(dev_dst);
+    for (uint32_t off = 0; off < len; off += piece_bytes) {
+        const uint32_t pl = std::min(piece_bytes, len - off);
+        rc = read_full(fd, host + off, pl);
+        if (rc != KF_OK) return rc;
+        ING_HIP(hipMemcpyAsync(dst + off, host + off, pl, hipMemcpyHostToDevice, s));
+    }
     ING_HIP(hipEventRecord(g->done[slot], s));
     {
         std::lock_guard<std::mutex> lock(g->mu);

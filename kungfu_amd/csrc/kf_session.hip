@@ -45,6 +45,7 @@
 #include <poll.h>
 #include <sys/eventfd.h>
 #include <sys/socket.h>
+#include <sys/uio.h>
 #include <sys/un.h>
 #include <unistd.h>
 
@@ -56,6 +57,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -358,6 +360,55 @@ int read_exact(int fd, void *buf, size_t n)
     return KF_OK;
 }
 
+int write_all(int fd, struct iovec *iov, int cnt)
+{
+    while (cnt > 0) {
+        ssize_t w = ::writev(fd, iov, cnt);
+        if (w < 0) {
+            if (errno == EINTR) continue;
+            return fail(KF_ERR_IO, std::string("writev: ") + strerror(errno));
+        }
+        size_t left = static_cast<size_t>(w);
+        while (cnt > 0 && left >= iov->iov_len) {
+            left -= iov->iov_len;
+            ++iov;
+            --cnt;
+        }
+        if (cnt > 0) {
+            iov->iov_base = static_cast<char *>(iov->iov_base) + left;
+            iov->iov_len -= left;
+        }
+    }
+    return KF_OK;
+}
+
+inline void put_le32(unsigned char *p, uint32_t v)
+{
+    p[0] = v & 0xff;
+    p[1] = (v >> 8) & 0xff;
+    p[2] = (v >> 16) & 0xff;
+    p[3] = (v >> 24) & 0xff;
+}
+
+// One rchannel message written in parts (the framing of kf_rch_send,
+// message.go:90-101,160-198): the header and the body length first, then the
+// body as its pieces become ready. The receiver sees one message.
+int write_msg_header(int fd, const std::string &name, uint32_t flags, uint32_t len)
+{
+    unsigned char a[4], b[4], c[4];
+    put_le32(a, static_cast<uint32_t>(name.size()));
+    put_le32(b, flags);
+    put_le32(c, len);
+    struct iovec iov[4] = {{a, 4}, {const_cast<char *>(name.data()), name.size()}, {b, 4}, {c, 4}};
+    return write_all(fd, iov, 4);
+}
+
+int write_bytes(int fd, const char *p, size_t n)
+{
+    struct iovec iov = {const_cast<char *>(p), n};
+    return write_all(fd, &iov, 1);
+}
+
 struct SessOp;
 
 struct SendItem {  // one chunk to every fd in `fds` (the node's successors)
@@ -374,6 +425,10 @@ struct SendItem {  // one chunk to every fd in `fds` (the node's successors)
                            // `ready` has completed
     SessOp *owner = nullptr;  // the collective whose chunk this is
     int chunk     = -1;       // its index in the collective (trace only)
+    // host items folded piece by piece: one event per piece (its fold's end),
+    // so the sender writes each piece once it is final
+    std::vector<hipEvent_t> pieces;
+    int staged_pieces = 0;    // device items: the D2H went out in this many pieces
 };
 
 // KUNGFU_AMD_SESSION_TRACE=<path>: every step of every chunk, timestamped,
@@ -436,6 +491,7 @@ struct SessChunk {
     bool batched;              // stage the reduce arrivals, fold them in one launch
     std::vector<int> waiting;  // reduce predecessors not yet heard from
     hipEvent_t mirror_ev;      // device mode: the last fold went to the mirror (its end)
+    std::vector<hipEvent_t> piece_ev;  // ... and each of its pieces' ends (streamed send)
     std::deque<FoldJob *> folds;  // host mode: received, not yet folded (front: running)
 };
 
@@ -493,6 +549,13 @@ struct kf_session {
     std::vector<void *> tx;
     std::vector<hipEvent_t> tx_done;  // one per slot: its D2H has landed
     size_t tx_ahead = 2;              // D2H issued ahead of the write (KUNGFU_AMD_TX_AHEAD)
+    // device mode: a chunk moves through each stage in pieces of this many
+    // bytes (KUNGFU_AMD_PIECE_KB; 0 = whole chunks): the D2H before a send,
+    // the fold or copy after a receive, the send of a fold's result, so a
+    // chunk's GPU and socket stages overlap instead of running in series
+    uint32_t piece = 256u << 10;
+    std::vector<hipEvent_t> tx_piece_ev;  // [slot][piece]: that piece's D2H landed
+    size_t max_pieces = 0;
     hipStream_t tx_stream  = nullptr;  // sender's D2H stream
     hipStream_t mir_stream = nullptr;  // the bcast root's mirror -> HBM copies
     std::vector<hipEvent_t> ev_pool;  // free "chunk is final" events
@@ -650,6 +713,7 @@ struct kf_session {
         if (ingest) kf_ingest_destroy(ingest);
         for (auto p : tx) (void)hipHostFree(p);
         for (auto e : tx_done) (void)hipEventDestroy(e);
+        for (auto e : tx_piece_ev) (void)hipEventDestroy(e);
         for (auto e : ev_pool) (void)hipEventDestroy(e);
         if (tx_stream) (void)hipStreamDestroy(tx_stream);
         if (mir_stream) (void)hipStreamDestroy(mir_stream);
@@ -723,10 +787,22 @@ struct kf_session {
     {
         if (it.host) return it.ready != nullptr;  // synced at send time
         bool ok = it.ready && it.bytes <= kChunk + 4096 &&
-                  hipStreamWaitEvent(tx_stream, it.ready, 0) == hipSuccess &&
-                  hipMemcpyAsync(tx[slot], it.ptr, it.bytes, hipMemcpyDeviceToHost, tx_stream) ==
-                      hipSuccess &&
-                  hipEventRecord(tx_done[slot], tx_stream) == hipSuccess;
+                  hipStreamWaitEvent(tx_stream, it.ready, 0) == hipSuccess;
+        const size_t np = piece ? (it.bytes + piece - 1) / piece : 0;
+        if (ok && np >= 2 && np <= max_pieces) {  // piece by piece, an event each
+            for (size_t k = 0; k < np && ok; ++k) {
+                const size_t off = k * piece, pl = std::min<size_t>(piece, it.bytes - off);
+                ok = hipMemcpyAsync(static_cast<char *>(tx[slot]) + off, it.ptr + off, pl,
+                                    hipMemcpyDeviceToHost, tx_stream) == hipSuccess &&
+                     hipEventRecord(tx_piece_ev[slot * max_pieces + k], tx_stream) == hipSuccess;
+            }
+            it.staged_pieces = static_cast<int>(np);
+        } else {
+            ok = ok &&
+                 hipMemcpyAsync(tx[slot], it.ptr, it.bytes, hipMemcpyDeviceToHost, tx_stream) ==
+                     hipSuccess;
+        }
+        ok = ok && hipEventRecord(tx_done[slot], tx_stream) == hipSuccess;
         if (it.ready) {
             std::lock_guard<std::mutex> l(ev_mu);
             ev_pool.push_back(it.ready);
@@ -735,8 +811,69 @@ struct kf_session {
         return ok;
     }
 
+    // the message header to every successor, then each piece once `ready(k)`
+    int send_pieces(const SendItem &it, const char *data, size_t np,
+                    const std::function<bool(size_t)> &ready, std::string *err)
+    {
+        for (int fd : it.fds) {
+            if (write_msg_header(fd, it.name, it.flags, static_cast<uint32_t>(it.bytes)) != KF_OK) {
+                *err = t_sess_error;
+                return KF_ERR_IO;
+            }
+        }
+        for (size_t k = 0; k < np; ++k) {
+            if (!ready(k)) {
+                *err = "a piece of an outgoing chunk did not land";
+                return KF_ERR_HIP;
+            }
+            const size_t off = k * piece, pl = std::min<size_t>(piece, it.bytes - off);
+            for (int fd : it.fds) {
+                if (write_bytes(fd, data + off, pl) != KF_OK) {
+                    *err = t_sess_error;
+                    return KF_ERR_IO;
+                }
+            }
+        }
+        return KF_OK;
+    }
+
     int send_staged(SendItem &it, size_t slot, std::string *err)
     {
+        if (it.host && !it.pieces.empty()) {  // the fold writes the mirror piece by piece
+            int rc = KF_ERR_HIP;
+            if (it.slot_ok) {
+                tr(TR_TX_READY, it.chunk, static_cast<int>(it.flags), 1);
+                rc = send_pieces(it, it.ptr, it.pieces.size(), [&](size_t k) {
+                    return hipEventSynchronize(it.pieces[k]) == hipSuccess;
+                }, err);
+            }
+            const bool synced = hipEventSynchronize(it.ready) == hipSuccess;
+            {
+                std::lock_guard<std::mutex> l(ev_mu);
+                ev_pool.push_back(it.ready);
+                it.ready = nullptr;
+                for (auto e : it.pieces) ev_pool.push_back(e);
+                it.pieces.clear();
+            }
+            if (rc == KF_OK && !synced) {
+                *err = "the fold of an outgoing chunk failed";
+                rc   = KF_ERR_HIP;
+            }
+            if (!it.slot_ok) *err = "the fold of an outgoing chunk failed";
+            return rc;
+        }
+        if (!it.host && it.slot_ok && it.staged_pieces >= 2) {  // D2H landing piece by piece
+            tr(TR_TX_READY, it.chunk, static_cast<int>(it.flags), 1);
+            const int rc = send_pieces(it, static_cast<const char *>(tx[slot]),
+                                       static_cast<size_t>(it.staged_pieces), [&](size_t k) {
+                return hipEventSynchronize(tx_piece_ev[slot * max_pieces + k]) == hipSuccess;
+            }, err);
+            if (rc == KF_OK && hipEventSynchronize(tx_done[slot]) != hipSuccess) {
+                *err = "D2H of an outgoing chunk failed";
+                return KF_ERR_HIP;
+            }
+            return rc;
+        }
         if (it.host) {  // the fold wrote the chunk to host memory: wait for it
             const bool ok = it.slot_ok && hipEventSynchronize(it.ready) == hipSuccess;
             {
@@ -787,6 +924,35 @@ struct kf_session {
             return nullptr;
         }
         return e;
+    }
+
+    // n events from the pool (new ones if it runs dry)
+    bool take_events(size_t n, std::vector<hipEvent_t> *out)
+    {
+        out->clear();
+        {
+            std::lock_guard<std::mutex> l(ev_mu);
+            while (out->size() < n && !ev_pool.empty()) {
+                out->push_back(ev_pool.back());
+                ev_pool.pop_back();
+            }
+        }
+        while (out->size() < n) {
+            hipEvent_t e = nullptr;
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+                give_events(*out);
+                return false;
+            }
+            out->push_back(e);
+        }
+        return true;
+    }
+
+    void give_events(std::vector<hipEvent_t> &evs)
+    {
+        std::lock_guard<std::mutex> l(ev_mu);
+        for (auto e : evs) ev_pool.push_back(e);
+        evs.clear();
     }
 
     int send_item(const SendItem &it, std::string *err)  // host mode
@@ -1186,6 +1352,8 @@ void kf_session::send_chunk(SessOp &o, size_t i, std::vector<int> fds, uint32_t 
         it.host     = true;
         it.owner    = &o;
         it.chunk    = static_cast<int>(i);
+        it.pieces   = std::move(c.piece_ev);
+        c.piece_ev.clear();
         c.mirror_ev = nullptr;
         enqueue(std::move(it));
         return;
@@ -1273,10 +1441,12 @@ int kf_session::handle(SessOp &o, size_t i, uint32_t flags, int peer, int fd, co
     const uint32_t len = static_cast<uint32_t>(clen(o, i));
     void *stream       = o.stream;
     int r              = KF_OK;
+    const bool pieces = device_mode && !mem && piece && len > piece;
     if (flags & KF_RCH_WAIT_RECV_BUF) {  // bcast: recvInto RecvBuf
         if (device_mode) {
-            r = mem ? kf_ingest_copy_host(ingest, mem, len, dst, stream)
-                    : kf_ingest_recv_into(ingest, fd, len, dst, stream);
+            r = mem      ? kf_ingest_copy_host(ingest, mem, len, dst, stream)
+                : pieces ? kf_ingest_recv_into_pieces(ingest, fd, len, dst, stream, piece)
+                         : kf_ingest_recv_into(ingest, fd, len, dst, stream);
         } else if (mem) {
             std::memcpy(dst, mem, len);
         } else {
@@ -1290,8 +1460,9 @@ int kf_session::handle(SessOp &o, size_t i, uint32_t flags, int peer, int fd, co
     }
     if (c.batched) {  // stage arrival #recv_count; fold once all are in
         char *slot = o.stage.p + static_cast<size_t>(c.recv_count) * o.bytes + o.parts[i].first * o.isz;
-        r = mem ? kf_ingest_copy_host(ingest, mem, len, slot, stream)
-                : kf_ingest_recv_into(ingest, fd, len, slot, stream);
+        r = mem      ? kf_ingest_copy_host(ingest, mem, len, slot, stream)
+            : pieces ? kf_ingest_recv_into_pieces(ingest, fd, len, slot, stream, piece)
+                     : kf_ingest_recv_into(ingest, fd, len, slot, stream);
         if (r != KF_OK) return fail(r, kf_ingest_last_error());
         ++c.recv_count;
         if (--c.pending_reduce > 0) return KF_OK;
@@ -1320,8 +1491,26 @@ int kf_session::handle(SessOp &o, size_t i, uint32_t flags, int peer, int fd, co
         // the completing fold of a chunk that leaves this node goes to the mirror
         const bool to_mirror = o.use_mirror && c.pending_reduce == 1 && sends_onward(o, i, rank);
         char *out            = to_mirror ? const_cast<char *>(cptr(o, o.mir.dev, i)) : dst;
-        r = mem ? kf_ingest_fold_host(ingest, mem, len, out, own, n, o.dt, o.op, stream)
-                : kf_ingest_recv_onto(ingest, fd, len, out, own, n, o.dt, o.op, stream);
+        if (pieces) {
+            // the completing fold into the mirror marks each piece, so the
+            // sender can write it while the next pieces are read and folded
+            std::vector<hipEvent_t> pev;
+            if (to_mirror && !take_events((len + piece - 1) / piece, &pev)) {
+                return fail(KF_ERR_HIP, "piece events");
+            }
+            r = kf_ingest_recv_onto_pieces(
+                ingest, fd, len, out, own, n, o.dt, o.op, stream, piece,
+                pev.empty() ? nullptr : reinterpret_cast<void *const *>(pev.data()),
+                static_cast<int>(pev.size()));
+            if (r != KF_OK) {
+                give_events(pev);
+                return fail(r, kf_ingest_last_error());
+            }
+            c.piece_ev = std::move(pev);
+        } else {
+            r = mem ? kf_ingest_fold_host(ingest, mem, len, out, own, n, o.dt, o.op, stream)
+                    : kf_ingest_recv_onto(ingest, fd, len, out, own, n, o.dt, o.op, stream);
+        }
         if (r != KF_OK) return fail(r, kf_ingest_last_error());
         if (to_mirror) {
             r = mirror_done(o, i, dst);
@@ -1453,11 +1642,13 @@ int kf_session::complete(SessOp &o)
         }
     }
     for (auto &c : o.chunks) {  // a failed collective may leave a mirror event unsent
+        std::lock_guard<std::mutex> l(ev_mu);
         if (c.mirror_ev) {
-            std::lock_guard<std::mutex> l(ev_mu);
             ev_pool.push_back(c.mirror_ev);
             c.mirror_ev = nullptr;
         }
+        for (auto e : c.piece_ev) ev_pool.push_back(e);
+        c.piece_ev.clear();
     }
     give(stage_pool, o.stage);
     give(mirror_pool, o.mir);
@@ -1829,6 +2020,10 @@ kf_session_t *create_session(int rank, std::vector<PeerAddr> peers, const char *
         if (const char *e = std::getenv("KUNGFU_AMD_TX_AHEAD")) {
             s->tx_ahead = static_cast<size_t>(std::max(1, std::atoi(e)));
         }
+        if (const char *e = std::getenv("KUNGFU_AMD_PIECE_KB")) {
+            s->piece = static_cast<uint32_t>(std::max(0, std::atoi(e))) << 10;
+        }
+        s->piece &= ~0xFFFu;  // whole 4 KiB: every dtype's elements, aligned pieces
         bool tx_ok = true;
         for (int i = 0; i < nslot && tx_ok; ++i) {
             void *p      = nullptr;
@@ -1845,6 +2040,14 @@ kf_session_t *create_session(int rank, std::vector<PeerAddr> peers, const char *
         if ((!ms || std::atoi(ms) != 0) &&
             hipStreamCreateWithFlags(&s->mir_stream, hipStreamNonBlocking) != hipSuccess) {
             s->mir_stream = nullptr;  // the copies stay on the caller's stream
+        }
+        if (s->piece) {
+            s->max_pieces = (kChunk + 4096 + s->piece - 1) / s->piece;
+            for (size_t k = 0; k < s->tx.size() * s->max_pieces && tx_ok; ++k) {
+                hipEvent_t e = nullptr;
+                tx_ok = hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+                if (tx_ok) s->tx_piece_ev.push_back(e);
+            }
         }
         if (!s->ingest || !tx_ok || !s->tx_stream) {
             t_sess_error = "kf_ingest_create failed";

@@ -54,17 +54,18 @@ or hier_all_reduce or fake_agent or rehearsal or branch_single_rank"
     step asan_build 600 bash tools/sanitize_gpu_hosts.sh build || exit $?
     step asan 900 bash tools/sanitize_gpu_hosts.sh run || exit $? ;;
   session)
-    step session_tests 900 $PYT tests/test_session.py tests/test_session_multihost.py \
-        tests/test_hierarchical.py tests/test_c_consumer.py
+    step session_tests 1000 $PYT tests/test_session.py tests/test_session_multihost.py \
+        tests/test_hierarchical.py tests/test_c_consumer.py tests/test_torch_ops_native.py
     fatal $? ;;
   c1)
     step c1 600 python bench.py --config c1 --c1-modes device,cpu,cpu_dev --c1-repeats 5 \
         --steps 100 --warmup 10 || exit $?
     tail -1 "$OUT/c1.log" > "$OUT/c1.json" ;;
   c1ab)
-    step c1ab 900 python tools/c1_ab.py device device:KUNGFU_AMD_TX_AHEAD=4 \
-        device:KUNGFU_AMD_MIRROR_SIDE=0 device:KUNGFU_AMD_TX_AHEAD=4,KUNGFU_AMD_MIRROR_SIDE=0 \
-        cpu --repeats 5 --out "$OUT/c1_ab.json" || exit $? ;;
+    step c1ab 900 python tools/c1_ab.py device device:KUNGFU_AMD_PIECE_KB=0 \
+        device:KUNGFU_AMD_PIECE_KB=128 device:KUNGFU_AMD_PIECE_KB=512 \
+        device:KUNGFU_AMD_TX_AHEAD=4 device:KUNGFU_AMD_MIRROR_SIDE=0 \
+        cpu cpu_dev --repeats 5 --out "$OUT/c1_ab.json" || exit $? ;;
   c1trace)
     step c1trace 600 python tools/c1_trace.py --modes device,cpu --steps 60 \
         --out "$OUT/c1_trace.json" || exit $? ;;
