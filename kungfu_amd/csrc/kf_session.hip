@@ -550,10 +550,14 @@ struct kf_session {
     std::vector<hipEvent_t> tx_done;  // one per slot: its D2H has landed
     size_t tx_ahead = 2;              // D2H issued ahead of the write (KUNGFU_AMD_TX_AHEAD)
     // device mode: a chunk moves through each stage in pieces of this many
-    // bytes (KUNGFU_AMD_PIECE_KB; 0 = whole chunks): the D2H before a send,
-    // the fold or copy after a receive, the send of a fold's result, so a
-    // chunk's GPU and socket stages overlap instead of running in series
-    uint32_t piece = 256u << 10;
+    // bytes (KUNGFU_AMD_PIECE_KB; 0 = whole chunks, the default): the D2H
+    // before a send, the fold or copy after a receive, the send of a fold's
+    // result, so a chunk's GPU and socket stages overlap instead of running in
+    // series. Every piece costs a launch or copy plus an event on the thread
+    // that reads the socket; over unix sockets that loses (C1 np = 2: 0.78 ms
+    // at 256 KiB, 1.01 at 128, 0.69 at 512, 0.66 whole), so it
+    // is for links slow enough to hide a launch per piece (TCP between hosts)
+    uint32_t piece = 0;
     std::vector<hipEvent_t> tx_piece_ev;  // [slot][piece]: that piece's D2H landed
     size_t max_pieces = 0;
     hipStream_t tx_stream  = nullptr;  // sender's D2H stream
@@ -811,23 +815,30 @@ struct kf_session {
         return ok;
     }
 
-    // the message header to every successor, then each piece once `ready(k)`
+    // One whole message per successor in turn: the header, then each piece
+    // once `ready(k)` (for the first successor; the later ones find every
+    // piece landed). A message is never interleaved with another: a peer
+    // that has started reading it blocks until it ends, so a sender that
+    // moved on to a second socket midway could wait on a peer that waits on
+    // it (three peers, each stuck in the middle of another's message).
     int send_pieces(const SendItem &it, const char *data, size_t np,
                     const std::function<bool(size_t)> &ready, std::string *err)
     {
+        size_t landed = 0;
         for (int fd : it.fds) {
             if (write_msg_header(fd, it.name, it.flags, static_cast<uint32_t>(it.bytes)) != KF_OK) {
                 *err = t_sess_error;
                 return KF_ERR_IO;
             }
-        }
-        for (size_t k = 0; k < np; ++k) {
-            if (!ready(k)) {
-                *err = "a piece of an outgoing chunk did not land";
-                return KF_ERR_HIP;
-            }
-            const size_t off = k * piece, pl = std::min<size_t>(piece, it.bytes - off);
-            for (int fd : it.fds) {
+            for (size_t k = 0; k < np; ++k) {
+                if (k >= landed) {
+                    if (!ready(k)) {
+                        *err = "a piece of an outgoing chunk did not land";
+                        return KF_ERR_HIP;
+                    }
+                    landed = k + 1;
+                }
+                const size_t off = k * piece, pl = std::min<size_t>(piece, it.bytes - off);
                 if (write_bytes(fd, data + off, pl) != KF_OK) {
                     *err = t_sess_error;
                     return KF_ERR_IO;

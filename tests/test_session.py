@@ -198,16 +198,18 @@ def test_session_device_strategies(strategy, size, batch_fold):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("piece_kb", ["0", "64", "300"])
+@pytest.mark.parametrize("piece_kb", ["256", "64", "300"])
 @pytest.mark.parametrize("strategy,size", [("STAR", 2), ("RING", 3), ("BINARY_TREE", 4),
                                            ("CLIQUE", 3)])
 def test_session_device_pieces(strategy, size, piece_kb):
-    """Device mode moves a chunk through each stage in pieces
-    (KUNGFU_AMD_PIECE_KB, default 256): the D2H before a send, the fold or
-    copy after a receive, the send of a fold's result written piece by piece
-    as each piece's fold ends. 0 = whole chunks; 300 KiB (rounded down to
-    296 KiB, whole 4 KiB) leaves a ragged last piece in every chunk of the
-    ragged bucket. Same schedule, same bits."""
+    """Device mode can move a chunk through each stage in pieces
+    (KUNGFU_AMD_PIECE_KB; default 0 = whole chunks): the D2H before a send,
+    the fold or copy after a receive, the send of a fold's result written
+    piece by piece as each piece's fold ends, one whole message per successor
+    at a time (CLIQUE at np = 3 deadlocked when a root interleaved two
+    successors' messages). 300 KiB (rounded down to 296 KiB, whole 4 KiB)
+    leaves a ragged last piece in every chunk of the ragged bucket. Same
+    schedule, same bits."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")

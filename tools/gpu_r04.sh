@@ -62,10 +62,9 @@ or hier_all_reduce or fake_agent or rehearsal or branch_single_rank"
         --steps 100 --warmup 10 || exit $?
     tail -1 "$OUT/c1.log" > "$OUT/c1.json" ;;
   c1ab)
-    step c1ab 900 python tools/c1_ab.py device device:KUNGFU_AMD_PIECE_KB=0 \
-        device:KUNGFU_AMD_PIECE_KB=128 device:KUNGFU_AMD_PIECE_KB=512 \
+    step c1ab 900 python tools/c1_ab.py device device:KUNGFU_AMD_PIECE_KB=512 \
         device:KUNGFU_AMD_TX_AHEAD=4 device:KUNGFU_AMD_MIRROR_SIDE=0 \
-        cpu cpu_dev --repeats 5 --out "$OUT/c1_ab.json" || exit $? ;;
+        device:KUNGFU_AMD_ROOT_MIRROR=0 cpu cpu_dev --repeats 5 --out "$OUT/c1_ab.json" || exit $? ;;
   c1trace)
     step c1trace 600 python tools/c1_trace.py --modes device,cpu --steps 60 \
         --out "$OUT/c1_trace.json" || exit $? ;;
