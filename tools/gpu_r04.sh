@@ -7,6 +7,9 @@
 #   bash tools/gpu_r04.sh <tag> bench2    # bench.py --gpus 2 rehearsal (self-launch, gloo)
 #   bash tools/gpu_r04.sh <tag> asan      # host-code ASan of the C++ hosts
 #   bash tools/gpu_r04.sh <tag> c1trace   # C1 np=2 per-chunk timelines (device, cpu)
+#   bash tools/gpu_r04.sh <tag> c1ab      # C1 session settings, interleaved A/B
+#   bash tools/gpu_r04.sh <tag> session   # the session / hierarchical / C-host GPU tests
+#   bash tools/gpu_r04.sh <tag> prof      # rocprofv3 stats + PMC traffic of the C2 kernel
 set -u
 TAG=${1:?tag}
 shift
@@ -61,6 +64,16 @@ or hier_all_reduce or fake_agent or rehearsal or branch_single_rank"
     step c1 600 python bench.py --config c1 --c1-modes device,cpu,cpu_dev --c1-repeats 5 \
         --steps 100 --warmup 10 || exit $?
     tail -1 "$OUT/c1.log" > "$OUT/c1.json" ;;
+  prof)
+    # the C2 kernel's rocprofv3 summary and PMC traffic for this round
+    step rocprof_trace 600 rocprofv3 --kernel-trace --stats -T -d "$OUT/prof" -o trace \
+        --output-format csv -- python3 bench.py --profile-only --steps 200 --warmup 20 || exit $?
+    for c in FETCH_SIZE WRITE_SIZE; do
+      step pmc_$c 300 rocprofv3 --pmc $c -T -d "$OUT/pmc_$c" -o pmc --output-format csv -- \
+          python3 bench.py --profile-only --steps 20 --warmup 2 || exit $?
+    done
+    python tools/pmc_traffic.py "$OUT/pmc_FETCH_SIZE" "$OUT/pmc_WRITE_SIZE" \
+        "$OUT/traffic.json" > /dev/null ;;
   c1ab)
     step c1ab 900 python tools/c1_ab.py device device:KUNGFU_AMD_PIECE_KB=512 \
         device:KUNGFU_AMD_TX_AHEAD=4 device:KUNGFU_AMD_MIRROR_SIDE=0 \
