@@ -1413,12 +1413,13 @@ def _primary_exchange(args, rank, world, dev):
     if uid is not None:
         def make():
             try:
-                box["ex"] = NativeExchange(algo="rs", device=dev, uid=uid)
+                box["ex"] = NativeExchange(algo="rs", device=dev, uid=uid,
+                                           timeout_s=args.native_timeout)
             except Exception as e:
                 box["err"] = repr(e)[:300]
         th = threading.Thread(target=make, daemon=True)
         th.start()
-        th.join(args.native_timeout)
+        th.join(args.native_timeout + 15)
     ex = box.get("ex")
     if _agree(ex is not None, dev):
         _NATIVE["ex"] = ex

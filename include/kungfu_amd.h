@@ -495,6 +495,12 @@ int kf_exchange_share_id(kf_session_t *s, void *id);
 /* ncclCommInitRank on HIP device `device` (the caller's current device is
  * restored). NULL on failure (kf_exchange_last_error). */
 kf_exchange_t *kf_exchange_create(const void *id, int rank, int world, int device);
+/* kf_exchange_create that gives up after timeout_ms (< 0: wait as long as it
+ * takes) with KF_ERR_TIMEOUT in kf_exchange_last_error, when not every rank
+ * joined the communicator's init in time. The init it abandons keeps waiting
+ * on a helper thread (a late completion releases its communicator). */
+kf_exchange_t *kf_exchange_create_timeout(const void *id, int rank, int world, int device,
+                                          int timeout_ms);
 /* gpu_collective::new_global: id from rank 0, shared over the session, then
  * kf_exchange_create(id, rank, size, device). */
 kf_exchange_t *kf_exchange_create_session(kf_session_t *s, int rank, int world, int device);

@@ -71,6 +71,7 @@ EXPORTED = (
     "kf_exchange_unique_id",
     "kf_exchange_share_id",
     "kf_exchange_create",
+    "kf_exchange_create_timeout",
     "kf_exchange_create_session",
     "kf_exchange_all_reduce",
     "kf_exchange_all_reduce_batch",
@@ -281,6 +282,8 @@ def load():
     lib.kf_exchange_share_id.restype = c_int
     lib.kf_exchange_create.argtypes = [c_void_p, c_int, c_int, c_int]
     lib.kf_exchange_create.restype = c_void_p
+    lib.kf_exchange_create_timeout.argtypes = [c_void_p, c_int, c_int, c_int, c_int]
+    lib.kf_exchange_create_timeout.restype = c_void_p
     lib.kf_exchange_create_session.argtypes = [c_void_p, c_int, c_int, c_int]
     lib.kf_exchange_create_session.restype = c_void_p
     lib.kf_exchange_all_reduce.argtypes = [c_void_p, c_void_p, c_void_p, c_size_t, c_int, c_int,

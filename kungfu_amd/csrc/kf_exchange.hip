@@ -1351,6 +1351,18 @@ static bool device_ok(int device)
 
 kf_exchange_t *kf_exchange_create(const void *id, int rank, int world, int device)
 {
+    return kf_exchange_create_timeout(id, rank, world, device, -1);
+}
+
+// ncclCommInitRank blocks until every rank has joined. With a timeout it runs
+// on a helper thread; if the time passes first the call fails with
+// KF_ERR_TIMEOUT and the helper is abandoned: it stays in the init until the
+// missing ranks come (then it releases the communicator it got) or the
+// process ends. RCCL's non-blocking init would make every later call of the
+// communicator non-blocking as well, so it is not used.
+kf_exchange_t *kf_exchange_create_timeout(const void *id, int rank, int world, int device,
+                                          int timeout_ms)
+{
     if (!id || world < 1 || rank < 0 || rank >= world || device < 0) {
         fail(KF_ERR_ARG, "kf_exchange_create: bad arguments");
         return nullptr;
@@ -1360,7 +1372,42 @@ kf_exchange_t *kf_exchange_create(const void *id, int rank, int world, int devic
     ncclUniqueId u;
     std::memcpy(&u, id, sizeof(u));
     ncclComm_t comm = nullptr;
-    ncclResult_t e  = rccl().CommInitRank(&comm, world, u, rank);
+    ncclResult_t e  = ncclSuccess;
+    if (timeout_ms < 0) {
+        e = rccl().CommInitRank(&comm, world, u, rank);
+    } else {
+        struct Init {
+            std::mutex m;
+            std::condition_variable cv;
+            bool done = false, abandoned = false;
+            ncclComm_t comm = nullptr;
+            ncclResult_t e  = ncclSuccess;
+        };
+        auto job = std::make_shared<Init>();
+        std::thread([job, u, world, rank, device] {
+            (void)hipSetDevice(device);
+            ncclComm_t c     = nullptr;
+            ncclResult_t r   = rccl().CommInitRank(&c, world, u, rank);
+            std::lock_guard<std::mutex> l(job->m);
+            if (job->abandoned) {  // nobody waits for it any more
+                if (r == ncclSuccess && c) (void)rccl().CommDestroy(c);
+                return;
+            }
+            job->comm = c;
+            job->e    = r;
+            job->done = true;
+            job->cv.notify_all();
+        }).detach();
+        std::unique_lock<std::mutex> l(job->m);
+        if (!job->cv.wait_for(l, std::chrono::milliseconds(timeout_ms), [&] { return job->done; })) {
+            job->abandoned = true;
+            fail(KF_ERR_TIMEOUT, "ncclCommInitRank: not every rank joined within " +
+                                     std::to_string(timeout_ms) + " ms");
+            return nullptr;
+        }
+        comm = job->comm;
+        e    = job->e;
+    }
     if (e != ncclSuccess) {
         nccl_fail(e, "ncclCommInitRank");
         return nullptr;

@@ -41,6 +41,7 @@
 
 #include <atomic>
 #include <condition_variable>
+#include <cstdlib>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -195,7 +196,15 @@ void init_exchange(py::bytes uid, int rank, int size, int device)
         (void)kf_exchange_wait_named(g_ex);
         kf_exchange_destroy(g_ex);
     }
-    g_ex = kf_exchange_create(id.data(), rank, size, device);
+    // a rank that never joins costs KUNGFU_AMD_INIT_TIMEOUT_S (default 300 s),
+    // then every rank learns it in ops.bring_up's agreement and takes the
+    // torch.distributed path
+    int timeout_ms = 300 * 1000;
+    if (const char *e = std::getenv("KUNGFU_AMD_INIT_TIMEOUT_S")) timeout_ms = 1000 * std::atoi(e);
+    {
+        py::gil_scoped_release nogil;
+        g_ex = kf_exchange_create_timeout(id.data(), rank, size, device, timeout_ms);
+    }
     if (!g_ex) throw std::runtime_error(std::string("kf_exchange_create: ") + kf_exchange_last_error());
 }
 

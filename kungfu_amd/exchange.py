@@ -61,9 +61,11 @@ class NativeExchange:
             return obj[0]
         return bytes(uid)
 
-    def __init__(self, group=None, algo="auto", device=None, uid=None):
+    def __init__(self, group=None, algo="auto", device=None, uid=None, timeout_s=None):
         """uid: the bytes of shared_id(group), when the caller shared it
-        already (e.g. to create the communicator on another thread)."""
+        already (e.g. to create the communicator on another thread).
+        timeout_s: give up (KungFuAMDError) if not every rank joined the
+        communicator's init in time (kf_exchange_create_timeout)."""
         if algo not in ALGOS:
             raise ValueError("algo must be one of %s" % sorted(ALGOS))
         self.algo = algo
@@ -77,7 +79,8 @@ class NativeExchange:
         if uid is None:
             uid = self.shared_id(group)
         buf = (ctypes.c_char * 128).from_buffer_copy(uid)
-        h = self.lib.kf_exchange_create(buf, self.rank, self.world, self.device.index)
+        ms = -1 if timeout_s is None else max(0, int(timeout_s * 1000))
+        h = self.lib.kf_exchange_create_timeout(buf, self.rank, self.world, self.device.index, ms)
         if not h:
             raise _lib.KungFuAMDError("kf_exchange_create: " +
                                       self.lib.kf_exchange_last_error().decode())

@@ -257,6 +257,39 @@ def _loop_ranks(world, body):
     loop_ranks(world, body)
 
 
+_LONE_RANK = r"""
+import ctypes, os, sys, time
+sys.path.insert(0, %r)
+from kungfu_amd import _lib
+lib = _lib.load()
+uid = (ctypes.c_char * 128)()
+assert lib.kf_exchange_unique_id(uid) == 0
+t0 = time.monotonic()
+h = lib.kf_exchange_create_timeout(uid, 0, 2, 0, 3000)
+dt = time.monotonic() - t0
+print("RESULT", bool(h), round(dt, 2), lib.kf_exchange_last_error().decode(), flush=True)
+os._exit(0)  # the abandoned init is still waiting for rank 1
+"""
+
+
+@pytest.mark.gpu
+def test_create_timeout_when_a_rank_never_joins():
+    """kf_exchange_create_timeout: rank 0 of a world of 2 whose rank 1 never
+    comes gets NULL and KF_ERR_TIMEOUT's message after the deadline instead
+    of blocking in ncclCommInitRank (the torch op's start-up uses it, so a
+    missing rank costs its peers KUNGFU_AMD_INIT_TIMEOUT_S, then every rank
+    takes the torch.distributed path together)."""
+    import subprocess
+    _gpu()
+    r = subprocess.run([sys.executable, "-c", _LONE_RANK % ROOT], capture_output=True,
+                       text=True, timeout=90)
+    line = [l for l in r.stdout.splitlines() if l.startswith("RESULT")]
+    assert line, r.stdout + r.stderr[-2000:]
+    _, ok, dt, msg = line[0].split(" ", 3)
+    assert ok == "False" and 2.5 <= float(dt) <= 30, line
+    assert "not every rank joined" in msg, msg
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("world,groups", [(2, 1), (4, 1), (4, 2), (3, 1)])
 def test_rs_avg_folds_the_division_into_the_collective(world, groups):
