@@ -59,10 +59,16 @@ func ExchangeUniqueID() ([ExchangeIDBytes]byte, error) {
 
 // NewExchange: the communicator of `size` ranks on HIP device `device`.
 func NewExchange(id [ExchangeIDBytes]byte, rank, size, device int) (*Exchange, error) {
+	return NewExchangeTimeout(id, rank, size, device, -1)
+}
+
+// NewExchangeTimeout: NewExchange that gives up after timeoutMs (< 0: no
+// limit) if not every rank joined the communicator's init.
+func NewExchangeTimeout(id [ExchangeIDBytes]byte, rank, size, device, timeoutMs int) (*Exchange, error) {
 	p := C.malloc(C.size_t(ExchangeIDBytes))
 	defer C.free(p)
 	copy(unsafe.Slice((*byte)(p), ExchangeIDBytes), id[:])
-	h := C.kf_exchange_create(p, C.int(rank), C.int(size), C.int(device))
+	h := C.kf_exchange_create_timeout(p, C.int(rank), C.int(size), C.int(device), C.int(timeoutMs))
 	if h == nil {
 		return nil, errors.New("kf_exchange_create: " + C.GoString(C.kf_exchange_last_error()))
 	}
