@@ -32,6 +32,7 @@
 #include <string>
 #include <vector>
 
+#include "kf_stream.hpp"
 #include "kungfu_amd.h"
 
 namespace
@@ -248,7 +249,10 @@ kf_ingest_t *kf_ingest_create(size_t slot_bytes, int nslots)
     g->done.assign(nslots, nullptr);
     g->armed.assign(nslots, false);
     for (int i = 0; i < nslots; ++i) {
-        if (hipHostMalloc(&g->host[i], slot_bytes, hipHostMallocDefault) != hipSuccess ||
+        // a streamed receive's kernel reads the slot behind a system acquire
+        // fence (kf_stream.hip): no fine-grained memory needed here
+        if (hipHostMalloc(&g->host[i], slot_bytes, hipHostMallocDefault) !=
+                hipSuccess ||
             hipHostGetDevicePointer(&g->hmap[i], g->host[i], 0) != hipSuccess ||
             hipEventCreateWithFlags(&g->done[i], hipEventDisableTiming) != hipSuccess) {
             t_ingest_error = "kf_ingest_create: HIP allocation failed";
@@ -458,3 +462,77 @@ int kf_ingest_sync(kf_ingest_t *g)
 const char *kf_ingest_last_error(void) { return t_ingest_error.c_str(); }
 
 }  // extern "C"
+
+namespace
+{
+// the body of the message whose header was just read, into the landing slot,
+// publishing every read as it lands; on a failure the waiting kernel is told
+int read_published(int fd, char *host, uint32_t len, kf_stream::Ctl *ctl)
+{
+    unsigned char a[4];
+    int rc = read_full(fd, a, 4);
+    if (rc == KF_OK && get_u32(a) != len) rc = proto_fail("unexpected message length");
+    uint32_t got = 0;
+    while (rc == KF_OK && got < len) {
+        ssize_t r = ::read(fd, host + got, len - got);
+        if (r < 0 && errno == EINTR) continue;
+        if (r < 0) {
+            rc = io_fail("read");
+        } else if (r == 0) {
+            rc = proto_fail("unexpected end of stream");
+        } else {
+            got += static_cast<uint32_t>(r);
+            kf_stream::publish(ctl, got);
+        }
+    }
+    if (rc != KF_OK) kf_stream::abort_wait(ctl);
+    return rc;
+}
+
+// the slot's kernel is queued first (it waits in the GPU), then the body is
+// read; the slot is free again once that kernel has run
+template <typename Launch>
+int streamed(kf_ingest_t *g, int fd, uint32_t len, void *stream, kf_stream::Ctl *ctl,
+             uint32_t piece, Launch launch)
+{
+    if (len > g->slot_bytes) return proto_fail("chunk larger than ingest slot");
+    int slot;
+    int rc = g->take(&slot);
+    if (rc != KF_OK) return rc;
+    kf_stream::reset(ctl, piece);
+    rc = launch(g->hmap[slot]);
+    if (rc != KF_OK) {
+        t_ingest_error = "streamed receive: kernel launch failed";
+        return rc;
+    }
+    ING_HIP(hipEventRecord(g->done[slot], static_cast<hipStream_t>(stream)));
+    {
+        std::lock_guard<std::mutex> lock(g->mu);
+        g->armed[slot] = true;
+    }
+    return read_published(fd, static_cast<char *>(g->host[slot]), len, ctl);
+}
+}  // namespace
+
+int kf_ingest_recv_onto_streamed(kf_ingest_t *g, int fd, uint32_t len, void *dev_acc,
+                                 const void *dev_own, KungFu_Datatype dt, void *stream,
+                                 uint32_t piece, kf_stream::Ctl *ctl, kf_stream::Ctl *ctl_dev,
+                                 int deadline_ms, bool mark)
+{
+    if (!g || !dev_acc || !ctl || !ctl_dev) return KF_ERR_ARG;
+    return streamed(g, fd, len, stream, ctl, piece, [&](void *landing) {
+        return kf_stream::launch_fold(dt, dev_own ? dev_own : dev_acc, landing, dev_acc, len,
+                                      piece, ctl_dev, deadline_ms, mark, stream);
+    });
+}
+
+int kf_ingest_recv_into_streamed(kf_ingest_t *g, int fd, uint32_t len, void *dev_dst,
+                                 void *stream, uint32_t piece, kf_stream::Ctl *ctl,
+                                 kf_stream::Ctl *ctl_dev, int deadline_ms)
+{
+    if (!g || (!dev_dst && len > 0) || !ctl || !ctl_dev) return KF_ERR_ARG;
+    return streamed(g, fd, len, stream, ctl, piece, [&](void *landing) {
+        return kf_stream::launch_copy_in(landing, dev_dst, len, piece, ctl_dev, deadline_ms,
+                                         stream);
+    });
+}

@@ -65,6 +65,7 @@
 #include <unordered_set>
 #include <vector>
 
+#include "kf_stream.hpp"
 #include "kungfu_amd.h"
 
 namespace
@@ -429,6 +430,7 @@ struct SendItem {  // one chunk to every fd in `fds` (the node's successors)
     // so the sender writes each piece once it is final
     std::vector<hipEvent_t> pieces;
     int staged_pieces = 0;    // device items: the D2H went out in this many pieces
+    kf_stream::Ctl *sctl = nullptr;  // streamed: the kernel marks the pieces here
 };
 
 // KUNGFU_AMD_SESSION_TRACE=<path>: every step of every chunk, timestamped,
@@ -464,6 +466,7 @@ struct LeasePool {
     std::vector<Lease> idle;
     size_t lent = 0, idle_bytes = 0;
     size_t cap  = 0;
+    bool coherent = false;  // host pools: fine-grained (a kernel waits on it live)
 };
 
 // Host mode: one received chunk body to fold into RecvBuf on a worker thread
@@ -492,6 +495,7 @@ struct SessChunk {
     std::vector<int> waiting;  // reduce predecessors not yet heard from
     hipEvent_t mirror_ev;      // device mode: the last fold went to the mirror (its end)
     std::vector<hipEvent_t> piece_ev;  // ... and each of its pieces' ends (streamed send)
+    bool streamed = false;             // the mirror fold marks its pieces in the op's ctl
     std::deque<FoldJob *> folds;  // host mode: received, not yet folded (front: running)
 };
 
@@ -522,6 +526,7 @@ struct SessOp {
     std::vector<SessChunk> chunks;
     size_t remaining = 0;
     Lease stage, mir;
+    Lease ctl;  // streamed chunks: two kf_stream::Ctl per chunk (reduce, bcast)
     size_t sends = 0;  // its chunks queued for the sender, not yet written (kf_session::mu)
     size_t folds = 0;  // host mode: its fold jobs not yet retired by the poll thread
     int rc       = KF_OK;
@@ -558,6 +563,19 @@ struct kf_session {
     // at 256 KiB, 1.01 at 128, 0.69 at 512, 0.66 whole), so it
     // is for links slow enough to hide a launch per piece (TCP between hosts)
     uint32_t piece = 0;
+    // streamed chunks (KUNGFU_AMD_STREAM; kf_stream.hpp): one kernel per
+    // chunk, launched before the body arrives, folds or copies it as it lands
+    // and marks pieces of stream_piece bytes done for the sender. A mask of
+    // the stages streamed ("out": a leaf's copy out of HBM before its send,
+    // "fold": the completing fold, into the mirror and sent piece by piece,
+    // "in": a bcast copy in; "1" all three)
+    enum { kStreamOut = 1, kStreamFold = 2, kStreamIn = 4 };
+    int stream_mode        = 0;
+    uint32_t stream_piece  = 64u << 10;
+    int stream_deadline_ms = 30000;
+    LeasePool ctl_pool;
+    std::vector<kf_stream::Ctl *> tx_ctl, tx_ctl_dev;  // per tx slot (copy-out)
+    std::vector<void *> tx_dev;                         // tx slots as the GPU sees them
     std::vector<hipEvent_t> tx_piece_ev;  // [slot][piece]: that piece's D2H landed
     size_t max_pieces = 0;
     hipStream_t tx_stream  = nullptr;  // sender's D2H stream
@@ -723,6 +741,8 @@ struct kf_session {
         if (mir_stream) (void)hipStreamDestroy(mir_stream);
         for (auto &l : stage_pool.idle) (void)hipFree(l.p);
         for (auto &l : mirror_pool.idle) (void)hipHostFree(l.p);
+        for (auto &l : ctl_pool.idle) (void)hipHostFree(l.p);
+        if (!tx_ctl.empty()) (void)hipHostFree(tx_ctl[0]);
         if (barrier_dev) (void)hipFree(barrier_dev);
         if (wake_fd >= 0) ::close(wake_fd);
     }
@@ -793,7 +813,12 @@ struct kf_session {
         bool ok = it.ready && it.bytes <= kChunk + 4096 &&
                   hipStreamWaitEvent(tx_stream, it.ready, 0) == hipSuccess;
         const size_t np = piece ? (it.bytes + piece - 1) / piece : 0;
-        if (ok && np >= 2 && np <= max_pieces) {  // piece by piece, an event each
+        if (ok && (stream_mode & kStreamOut) && it.bytes > 0) {  // one kernel, pieces marked as they land
+            kf_stream::reset(tx_ctl[slot], stream_piece);
+            ok = kf_stream::launch_copy_out(it.ptr, tx_dev[slot], static_cast<uint32_t>(it.bytes),
+                                            stream_piece, tx_ctl_dev[slot], tx_stream) == KF_OK;
+            it.sctl = tx_ctl[slot];
+        } else if (ok && np >= 2 && np <= max_pieces) {  // piece by piece, an event each
             for (size_t k = 0; k < np && ok; ++k) {
                 const size_t off = k * piece, pl = std::min<size_t>(piece, it.bytes - off);
                 ok = hipMemcpyAsync(static_cast<char *>(tx[slot]) + off, it.ptr + off, pl,
@@ -848,8 +873,63 @@ struct kf_session {
         return KF_OK;
     }
 
+    // One message per successor, its body written in runs of pieces as the
+    // kernel marks them final in `c` (the first successor waits for them).
+    int send_streamed(const SendItem &it, const char *data, const kf_stream::Ctl *c,
+                      std::string *err)
+    {
+        const uint32_t len = static_cast<uint32_t>(it.bytes);
+        const uint32_t np  = (len + stream_piece - 1) / stream_piece;
+        uint32_t landed    = 0;  // pieces known final
+        for (int fd : it.fds) {
+            if (write_msg_header(fd, it.name, it.flags, len) != KF_OK) {
+                *err = t_sess_error;
+                return KF_ERR_IO;
+            }
+            for (uint32_t k = 0; k < np;) {
+                if (k >= landed) {
+                    const int w = kf_stream::wait_piece(c, k, len, stream_deadline_ms);
+                    if (w != KF_OK) {
+                        *err = w == KF_ERR_TIMEOUT ? "a streamed chunk's piece did not become final"
+                                                   : "a streamed chunk's kernel gave up waiting";
+                        return w;
+                    }
+                    landed = k + kf_stream::ready_run(c, k, len);
+                }
+                const size_t b = static_cast<size_t>(k) * stream_piece;
+                const size_t e = std::min<size_t>(static_cast<size_t>(landed) * stream_piece, len);
+                if (write_bytes(fd, data + b, e - b) != KF_OK) {
+                    *err = t_sess_error;
+                    return KF_ERR_IO;
+                }
+                k = landed;
+            }
+        }
+        return KF_OK;
+    }
+
     int send_staged(SendItem &it, size_t slot, std::string *err)
     {
+        if (it.sctl && it.slot_ok) {  // streamed: the mirror fold's or the copy-out's pieces
+            tr(TR_TX_READY, it.chunk, static_cast<int>(it.flags), 1);
+            const char *data = it.host ? it.ptr : static_cast<const char *>(tx[slot]);
+            const int rc     = send_streamed(it, data, it.sctl, err);
+            if (!it.host && rc == KF_OK && hipEventSynchronize(tx_done[slot]) != hipSuccess) {
+                *err = "D2H of an outgoing chunk failed";
+                return KF_ERR_HIP;
+            }
+            if (it.host) {
+                const bool synced = hipEventSynchronize(it.ready) == hipSuccess;
+                std::lock_guard<std::mutex> l(ev_mu);
+                ev_pool.push_back(it.ready);
+                it.ready = nullptr;
+                if (rc == KF_OK && !synced) {
+                    *err = "the fold of an outgoing chunk failed";
+                    return KF_ERR_HIP;
+                }
+            }
+            return rc;
+        }
         if (it.host && !it.pieces.empty()) {  // the fold writes the mirror piece by piece
             int rc = KF_ERR_HIP;
             if (it.slot_ok) {
@@ -1192,6 +1272,12 @@ struct kf_session {
     void start_fold(SessOp &o, size_t i);
     void retire_folds();
     bool take(LeasePool &pool, size_t need, bool host, Lease *out);
+    // chunk i's control block, `which` 0 = its reduce-phase fold, 1 = its bcast
+    kf_stream::Ctl *ctl_at(SessOp &o, size_t i, int which, bool dev = false)
+    {
+        char *base = dev ? o.ctl.dev : o.ctl.p;
+        return reinterpret_cast<kf_stream::Ctl *>(base) + 2 * i + which;
+    }
     void give(LeasePool &pool, Lease &l);
 };
 
@@ -1229,7 +1315,9 @@ bool kf_session::take(LeasePool &pool, size_t need, bool host, Lease *out)
     Lease l;
     if (host) {
         void *dv = nullptr;
-        if (hipHostMalloc(reinterpret_cast<void **>(&l.p), need, hipHostMallocDefault) != hipSuccess) {
+        const unsigned fl = pool.coherent ? hipHostMallocMapped | hipHostMallocCoherent
+                                          : hipHostMallocDefault;
+        if (hipHostMalloc(reinterpret_cast<void **>(&l.p), need, fl) != hipSuccess) {
             return false;
         }
         if (hipHostGetDevicePointer(&dv, l.p, 0) != hipSuccess) {
@@ -1319,6 +1407,10 @@ int kf_session::plan(SessOp &o)
         // reference does (recvOnto per predecessor), same bits
         for (auto &c : o.chunks) c.batched = false;
     }
+    if (device_mode && (stream_mode & (kStreamFold | kStreamIn)) &&
+        !take(ctl_pool, 2 * o.chunks.size() * sizeof(kf_stream::Ctl), true, &o.ctl)) {
+        o.ctl = Lease{};  // this call moves whole chunks
+    }
     // the fold that completes a chunk goes to the page-locked mirror when the
     // chunk then leaves this node (reduce successors, or bcast successors of a
     // node that receives no bcast itself)
@@ -1365,6 +1457,7 @@ void kf_session::send_chunk(SessOp &o, size_t i, std::vector<int> fds, uint32_t 
         it.chunk    = static_cast<int>(i);
         it.pieces   = std::move(c.piece_ev);
         c.piece_ev.clear();
+        if (c.streamed) it.sctl = ctl_at(o, i, 0);
         c.mirror_ev = nullptr;
         enqueue(std::move(it));
         return;
@@ -1452,12 +1545,18 @@ int kf_session::handle(SessOp &o, size_t i, uint32_t flags, int peer, int fd, co
     const uint32_t len = static_cast<uint32_t>(clen(o, i));
     void *stream       = o.stream;
     int r              = KF_OK;
-    const bool pieces = device_mode && !mem && piece && len > piece;
+    const bool pieces   = device_mode && !mem && piece && len > piece;
+    const bool streamed = device_mode && !mem && o.ctl.p && len > 0;
     if (flags & KF_RCH_WAIT_RECV_BUF) {  // bcast: recvInto RecvBuf
         if (device_mode) {
-            r = mem      ? kf_ingest_copy_host(ingest, mem, len, dst, stream)
-                : pieces ? kf_ingest_recv_into_pieces(ingest, fd, len, dst, stream, piece)
-                         : kf_ingest_recv_into(ingest, fd, len, dst, stream);
+            r = mem ? kf_ingest_copy_host(ingest, mem, len, dst, stream)
+                : streamed && (stream_mode & kStreamIn)
+                    ? kf_ingest_recv_into_streamed(ingest, fd, len, dst, stream,
+                                                          stream_piece, ctl_at(o, i, 1),
+                                                          ctl_at(o, i, 1, true),
+                                                          stream_deadline_ms)
+                : pieces   ? kf_ingest_recv_into_pieces(ingest, fd, len, dst, stream, piece)
+                           : kf_ingest_recv_into(ingest, fd, len, dst, stream);
         } else if (mem) {
             std::memcpy(dst, mem, len);
         } else {
@@ -1502,7 +1601,16 @@ int kf_session::handle(SessOp &o, size_t i, uint32_t flags, int peer, int fd, co
         // the completing fold of a chunk that leaves this node goes to the mirror
         const bool to_mirror = o.use_mirror && c.pending_reduce == 1 && sends_onward(o, i, rank);
         char *out            = to_mirror ? const_cast<char *>(cptr(o, o.mir.dev, i)) : dst;
-        if (pieces) {
+        // streamed: only the fold that completes the chunk (one per chunk per
+        // call, so its control block is never reset under a running kernel)
+        if (streamed && (stream_mode & kStreamFold) && c.pending_reduce == 1 &&
+            kf_stream::supported(o.dt, o.op)) {
+            r = kf_ingest_recv_onto_streamed(ingest, fd, len, out, own, o.dt, stream, stream_piece,
+                                             ctl_at(o, i, 0), ctl_at(o, i, 0, true),
+                                             stream_deadline_ms, to_mirror);
+            if (r != KF_OK) return fail(r, kf_ingest_last_error());
+            c.streamed = to_mirror;
+        } else if (pieces) {
             // the completing fold into the mirror marks each piece, so the
             // sender can write it while the next pieces are read and folded
             std::vector<hipEvent_t> pev;
@@ -1663,6 +1771,7 @@ int kf_session::complete(SessOp &o)
     }
     give(stage_pool, o.stage);
     give(mirror_pool, o.mir);
+    give(ctl_pool, o.ctl);
     if (rc != KF_OK && o.err.empty()) o.err = t_sess_error;
     o.rc = rc;
     return rc;
@@ -2034,13 +2143,35 @@ kf_session_t *create_session(int rank, std::vector<PeerAddr> peers, const char *
         if (const char *e = std::getenv("KUNGFU_AMD_PIECE_KB")) {
             s->piece = static_cast<uint32_t>(std::max(0, std::atoi(e))) << 10;
         }
+        if (const char *e = std::getenv("KUNGFU_AMD_STREAM")) {  // "1": every stage, or a list
+            const std::string v = e;
+            s->stream_mode      = v == "1" ? 7 : 0;
+            if (v.find("out") != std::string::npos) s->stream_mode |= kf_session::kStreamOut;
+            if (v.find("fold") != std::string::npos) s->stream_mode |= kf_session::kStreamFold;
+            if (v.find("in") != std::string::npos) s->stream_mode |= kf_session::kStreamIn;
+        }
+        if (const char *e = std::getenv("KUNGFU_AMD_STREAM_PIECE_KB")) {
+            const uint32_t kb = static_cast<uint32_t>(std::max(4, std::atoi(e)));
+            s->stream_piece   = (kb << 10) & ~(kf_stream::kBlockBytes - 1);
+        }
+        if (const char *e = std::getenv("KUNGFU_AMD_STREAM_TIMEOUT_MS")) {
+            s->stream_deadline_ms = std::max(1, std::atoi(e));
+        }
+        s->ctl_pool.cap       = size_t(64) << 20;
+        s->ctl_pool.coherent  = true;
+
         s->piece &= ~0xFFFu;  // whole 4 KiB: every dtype's elements, aligned pieces
         bool tx_ok = true;
         for (int i = 0; i < nslot && tx_ok; ++i) {
             void *p      = nullptr;
             hipEvent_t e = nullptr;
             tx_ok = hipHostMalloc(&p, kChunk + 4096, hipHostMallocDefault) == hipSuccess;
-            if (tx_ok) s->tx.push_back(p);
+            void *dv = nullptr;
+            tx_ok    = tx_ok && hipHostGetDevicePointer(&dv, p, 0) == hipSuccess;
+            if (tx_ok) {
+                s->tx.push_back(p);
+                s->tx_dev.push_back(dv);
+            }
             tx_ok = tx_ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
             if (tx_ok) s->tx_done.push_back(e);
         }
@@ -2051,6 +2182,16 @@ kf_session_t *create_session(int rank, std::vector<PeerAddr> peers, const char *
         if ((!ms || std::atoi(ms) != 0) &&
             hipStreamCreateWithFlags(&s->mir_stream, hipStreamNonBlocking) != hipSuccess) {
             s->mir_stream = nullptr;  // the copies stay on the caller's stream
+        }
+        if ((s->stream_mode & kf_session::kStreamOut) && tx_ok) {  // a control block per tx slot
+            void *cp = nullptr, *cd = nullptr;
+            tx_ok = hipHostMalloc(&cp, s->tx.size() * sizeof(kf_stream::Ctl),
+                                  hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess &&
+                    hipHostGetDevicePointer(&cd, cp, 0) == hipSuccess;
+            for (size_t k = 0; tx_ok && k < s->tx.size(); ++k) {
+                s->tx_ctl.push_back(static_cast<kf_stream::Ctl *>(cp) + k);
+                s->tx_ctl_dev.push_back(static_cast<kf_stream::Ctl *>(cd) + k);
+            }
         }
         if (s->piece) {
             s->max_pieces = (kChunk + 4096 + s->piece - 1) / s->piece;

@@ -219,6 +219,28 @@ def test_session_device_pieces(strategy, size, piece_kb):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("piece_kb,kind,batch_fold", [("64", "rand", "1"), ("4", "rand", "0"),
+                                                      ("300", "iota", "1"), ("1024", "rand", "0")])
+@pytest.mark.parametrize("strategy,size", [("STAR", 2), ("RING", 3), ("BINARY_TREE", 4),
+                                           ("CLIQUE", 3), ("STAR", 4)])
+def test_session_device_streamed(strategy, size, piece_kb, kind, batch_fold):
+    """KUNGFU_AMD_STREAM=1: one kernel per received chunk, launched before
+    its body arrives, folds (the completing 2-input fold) or copies (bcast)
+    each 4 KiB as the socket delivers it, and marks pieces of
+    KUNGFU_AMD_STREAM_PIECE_KB done in page-locked memory; the sender writes
+    each piece of a folded chunk (and of a leaf's copy out of HBM, also one
+    kernel) as soon as all its 4 KiB blocks are flagged. 4 KiB pieces are
+    single blocks; 300 KiB leaves ragged pieces. Same schedule, same bits as
+    the whole-chunk path."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    run(size, "device", kind, (5 << 20) // 4 + 17, strategy=strategy,
+        env={"KUNGFU_AMD_STREAM": "1", "KUNGFU_AMD_STREAM_PIECE_KB": piece_kb,
+             "KUNGFU_AMD_BATCH_FOLD": batch_fold, "KUNGFU_AMD_STREAM_TIMEOUT_MS": "20000"})
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("strategy", ["STAR", "BINARY_TREE", "CLIQUE"])
 def test_session_device_lease_caps(strategy):
     """HBM staging and page-locked mirrors come from

@@ -10,6 +10,7 @@
 #   bash tools/gpu_r04.sh <tag> c1ab      # C1 session settings, interleaved A/B
 #   bash tools/gpu_r04.sh <tag> session   # the session / hierarchical / C-host GPU tests
 #   bash tools/gpu_r04.sh <tag> prof      # rocprofv3 stats + PMC traffic of the C2 kernel
+#   bash tools/gpu_r04.sh <tag> stream    # streamed-chunk session tests + C1 A/B against whole chunks
 set -u
 TAG=${1:?tag}
 shift
@@ -78,6 +79,13 @@ or hier_all_reduce or fake_agent or rehearsal or branch_single_rank"
     step c1ab 900 python tools/c1_ab.py device device:KUNGFU_AMD_PIECE_KB=512 \
         device:KUNGFU_AMD_TX_AHEAD=4 device:KUNGFU_AMD_MIRROR_SIDE=0 \
         device:KUNGFU_AMD_ROOT_MIRROR=0 cpu cpu_dev --repeats 5 --out "$OUT/c1_ab.json" || exit $? ;;
+  stream)
+    step stream_tests 600 $PYT tests/test_session.py -k "streamed"
+    fatal $?
+    step c1ab_stream 900 python tools/c1_ab.py device device:KUNGFU_AMD_STREAM=1 \
+        device:KUNGFU_AMD_STREAM=out device:KUNGFU_AMD_STREAM=fold device:KUNGFU_AMD_STREAM=in \
+        device:KUNGFU_AMD_STREAM=out+fold cpu --repeats 5 \
+        --out "$OUT/c1_ab_stream.json" || exit $? ;;
   c1trace)
     step c1trace 600 python tools/c1_trace.py --modes device,cpu --steps 60 \
         --out "$OUT/c1_trace.json" || exit $? ;;

@@ -22,7 +22,7 @@ build)
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O1 -g -std=c++17 -fPIC -shared -ffp-contract=off \
         -fvisibility=hidden -Xarch_host -fsanitize=$SAN -Wl,-soname,libkungfu_amd.so \
         -I"$ROOT/include" -o "$D/libkungfu_amd.so" \
-        $SRC/kf_capi.hip $SRC/kf_ingest.hip $SRC/kf_session.hip $SRC/kf_p2p.hip $SRC/kf_exchange.hip -ldl
+        $SRC/kf_capi.hip $SRC/kf_ingest.hip $SRC/kf_session.hip $SRC/kf_p2p.hip $SRC/kf_exchange.hip $SRC/kf_stream.hip -ldl
     CXX="/opt/rocm/lib/llvm/bin/clang++ -std=c++17 -O1 -g -fsanitize=$SAN -D__HIP_PLATFORM_AMD__"
     $CXX -fPIC -shared $INC -o "$D/libkf_testing.so" "$ROOT/tests/c/kf_testing.cpp" \
         -L"$D" -lkungfu_amd -Wl,-rpath,'$ORIGIN' $HIPL -ldl -lpthread

@@ -11,7 +11,7 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 W=${TMPDIR:-/tmp}/kf_sanitize
 mkdir -p "$W"
 SRC="$ROOT/kungfu_amd/csrc"
-SRCS="$SRC/kf_capi.hip $SRC/kf_ingest.hip $SRC/kf_session.hip $SRC/kf_p2p.hip $SRC/kf_exchange.hip"
+SRCS="$SRC/kf_capi.hip $SRC/kf_ingest.hip $SRC/kf_session.hip $SRC/kf_p2p.hip $SRC/kf_exchange.hip $SRC/kf_stream.hip"
 CLANG=/opt/rocm/lib/llvm/bin/clang++
 for san in thread address; do
     D="$W/$san"
