@@ -102,6 +102,17 @@ __global__ void __launch_bounds__(kLanes) in_k(const char *host, uint4 *dst, con
     if (ok) dst[i] = v;
 }
 
+// the session root's whole-chunk fold: out(host) = own(HBM) + landing(host),
+// 1 MiB fp32, grid-stride over 16-B vectors with `blocks` blocks
+__global__ void __launch_bounds__(kLanes) fold_grid_k(const float4 *own, const float4 *landing,
+                                                       float4 *out, unsigned nvec)
+{
+    for (unsigned i = blockIdx.x * kLanes + threadIdx.x; i < nvec; i += gridDim.x * kLanes) {
+        const float4 a = own[i], b = landing[i];
+        out[i]         = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+    }
+}
+
 template <typename F>
 float timed(hipStream_t s, F f)
 {
@@ -188,6 +199,16 @@ int main()
         }
         put(m.name, "memcpy_d2h_one_wall_us", float(tot / 15));
         CK(hipEventDestroy(e));
+    }
+    for (unsigned blocks : {32u, 64u, 128u, 256u, 512u}) {  // grid of the root's fold
+        char name[64];
+        std::snprintf(name, sizeof(name), "fold_host_in_out_%u_blocks_us", blocks);
+        auto *land = reinterpret_cast<const float4 *>(mems[2].d);
+        auto *outh = reinterpret_cast<float4 *>(mems[1].d);
+        put("default", name, timed(s, [&] {
+                fold_grid_k<<<blocks, kLanes, 0, s>>>(reinterpret_cast<const float4 *>(dev), land, outh,
+                                                      kLen / 16);
+            }));
     }
     {  // the CPU's side: memcpy of 1 MiB into and out of each kind (what read()/write() do)
         static char buf[kLen];
