@@ -6,7 +6,9 @@ library is missing, or the process has no GPU, the product path raises.
 """
 import atexit
 import ctypes
+import importlib.util
 import os
+import sys
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libkungfu_amd.so")
@@ -122,6 +124,23 @@ class KungFuAMDError(RuntimeError):
     pass
 
 
+def _preload_hip_runtime():
+    """One HIP runtime per process: torch ships its own libamdhip64 (SONAME
+    libamdhip64.so.7, like /opt/rocm's), which its libraries find by RPATH.
+    Loading torch's file first makes the library's libamdhip64.so.7 resolve
+    to it, and a later `import torch` finds it already mapped — without the
+    2 s of importing torch in processes that never touch a tensor (host-mode
+    peers). Without torch, /opt/rocm's runtime is used."""
+    if "torch" in sys.modules:
+        return
+    spec = importlib.util.find_spec("torch")
+    for d in (spec.submodule_search_locations or []) if spec else []:
+        path = os.path.join(d, "lib", "libamdhip64.so")
+        if os.path.exists(path):
+            ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+            return
+
+
 def load():
     """Load (once) and return the ctypes handle of libkungfu_amd.so."""
     global _lib
@@ -131,12 +150,7 @@ def load():
         raise KungFuAMDError(
             "libkungfu_amd.so not built (%s); run __graft_entry__.build() or "
             "make -C kungfu_amd/csrc" % LIB_PATH)
-    # torch (if present) must bring its HIP runtime first so both resolve the
-    # same libamdhip64.so.7 (same SONAME, one runtime per process).
-    try:
-        import torch  # noqa: F401
-    except ImportError:
-        pass
+    _preload_hip_runtime()
     lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
     c_void_p, c_size_t, c_int = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
     lib.std_transform_2.argtypes = [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int]

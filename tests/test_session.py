@@ -11,7 +11,7 @@ import traceback
 
 import numpy as np
 import pytest
-import torch.multiprocessing as mp
+import multiprocessing as mp
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
@@ -60,12 +60,10 @@ def _body(rank, size, sock_dir, mode, kind, n, errq, strategy=None, env=None):
             s.all_reduce(z, z, "inplace")
             got_inplace = z
         s.close()
-        if strategy is not None:
-            check_strategy(size, kind, n, strategy, "NegotiatedGrad_0/AllReduce", got)
-            check_strategy(size, kind, n, strategy, "inplace", got_inplace)
-        else:
-            check(rank, size, kind, n, got)
-            check(rank, size, kind, n, got_inplace)
+        # the parent checks every rank's results once (the expected chunks are
+        # the same for every rank: one computation instead of one per rank)
+        np.save(os.path.join(sock_dir, "got%d.npy" % rank), got)
+        np.save(os.path.join(sock_dir, "inplace%d.npy" % rank), got_inplace)
     except Exception:
         errq.put("rank %d: %s" % (rank, traceback.format_exc()))
 
@@ -123,11 +121,23 @@ def run(size, mode, kind, n, strategy=None, env=None):
             p.start()
         for p in ps:
             p.join(timeout=300)
-    errs = []
-    while not errq.empty():
-        errs.append(errq.get())
-    assert not errs, "\n".join(errs)
-    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+        errs = []
+        while not errq.empty():
+            errs.append(errq.get())
+        assert not errs, "\n".join(errs)
+        assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+        gots = [(np.load(os.path.join(d, "got%d.npy" % r)),
+                 np.load(os.path.join(d, "inplace%d.npy" % r))) for r in range(size)]
+    # every rank ends with the same bucket (the bcast of each chunk's root)
+    for r in range(1, size):
+        assert np.array_equal(gots[r][0], gots[0][0]), ("rank differs", r)
+        assert np.array_equal(gots[r][1], gots[0][1]), ("rank differs (in place)", r)
+    if strategy is not None:
+        check_strategy(size, kind, n, strategy, "NegotiatedGrad_0/AllReduce", gots[0][0])
+        check_strategy(size, kind, n, strategy, "inplace", gots[0][1])
+    else:
+        check(0, size, kind, n, gots[0][0])
+        check(0, size, kind, n, gots[0][1])
 
 
 @pytest.mark.parametrize("size,kind,n", [(2, "iota", 8), (3, "iota", 12),

@@ -14,7 +14,7 @@ import traceback
 
 import numpy as np
 import pytest
-import torch.multiprocessing as mp
+import multiprocessing as mp
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
