@@ -251,6 +251,19 @@ def test_session_device_streamed(strategy, size, piece_kb, kind, batch_fold):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("stages", ["out", "fold", "in", "out+in"])
+def test_session_device_streamed_stages(stages):
+    """KUNGFU_AMD_STREAM names the stages streamed; each alone (and the two
+    that touch only one side of a hop) beside the whole-chunk others gives
+    the same bits, at np = 3 under BINARY_TREE (inner fold, leaf copies)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    run(3, "device", "rand", (5 << 20) // 4 + 17, strategy="BINARY_TREE",
+        env={"KUNGFU_AMD_STREAM": stages, "KUNGFU_AMD_BATCH_FOLD": "0"})
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("strategy", ["STAR", "BINARY_TREE", "CLIQUE"])
 def test_session_device_lease_caps(strategy):
     """HBM staging and page-locked mirrors come from
