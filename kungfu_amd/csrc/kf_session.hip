@@ -567,8 +567,8 @@ struct kf_session {
     // chunk, launched before the body arrives, folds or copies it as it lands
     // and marks pieces of stream_piece bytes done for the sender. A mask of
     // the stages streamed ("out": a leaf's copy out of HBM before its send,
-    // "fold": the completing fold, into the mirror and sent piece by piece,
-    // "in": a bcast copy in; "1" all three)
+    // "fold": the completing fold, into the mirror and sent piece by piece —
+    // the default; "in": a bcast copy in; "1" all three, "0" none)
     enum { kStreamOut = 1, kStreamFold = 2, kStreamIn = 4 };
     int stream_mode        = 0;
     uint32_t stream_piece  = 64u << 10;
@@ -895,6 +895,7 @@ struct kf_session {
                         return w;
                     }
                     landed = k + kf_stream::ready_run(c, k, len);
+                    if (landed == np) tr(TR_FOLD_END, it.chunk, 0, 1);  // every piece final
                 }
                 const size_t b = static_cast<size_t>(k) * stream_piece;
                 const size_t e = std::min<size_t>(static_cast<size_t>(landed) * stream_piece, len);
@@ -2143,7 +2144,8 @@ kf_session_t *create_session(int rank, std::vector<PeerAddr> peers, const char *
         if (const char *e = std::getenv("KUNGFU_AMD_PIECE_KB")) {
             s->piece = static_cast<uint32_t>(std::max(0, std::atoi(e))) << 10;
         }
-        if (const char *e = std::getenv("KUNGFU_AMD_STREAM")) {  // "1": every stage, or a list
+        s->stream_mode = kf_session::kStreamFold;  // the measured-best default
+        if (const char *e = std::getenv("KUNGFU_AMD_STREAM")) {  // "0", "1" (all), or a list
             const std::string v = e;
             s->stream_mode      = v == "1" ? 7 : 0;
             if (v.find("out") != std::string::npos) s->stream_mode |= kf_session::kStreamOut;

@@ -30,6 +30,10 @@
 #include "kf_reduce_kernels.hpp"
 #include "kf_stream.hpp"
 
+#ifndef KF_STREAM_HOST_STORE_AUX
+#define KF_STREAM_HOST_STORE_AUX 16  // sc1: written through the L2
+#endif
+
 namespace kf_stream
 {
 namespace
@@ -89,8 +93,8 @@ __device__ int wait_seen(Ctl *c, const unsigned long long *seen, uint32_t epoch,
     }
 }
 
-// block 0 watches (returns false); a data block waits for its bytes, then
-// every lane may read them (the barrier, one system acquire fence per block)
+// block 0 watches (returns false); a data block waits for its bytes (its
+// first lane polls, the block meets at a barrier)
 __device__ __forceinline__ bool block_wait(Ctl *c, uint32_t len, uint32_t need,
                                            unsigned long long *seen, uint32_t epoch,
                                            unsigned long long limit, bool *ok)
@@ -102,23 +106,69 @@ __device__ __forceinline__ bool block_wait(Ctl *c, uint32_t len, uint32_t need,
     __shared__ int got;
     if (threadIdx.x == 0) got = wait_seen(c, seen, epoch, need, limit + limit / 8);
     __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     *ok = got != 0;
     return true;
 }
 
-// this block's stores have reached host memory: flag it for the sender
+// Page-locked bytes move with an explicit cache policy instead of fences:
+// the landing slot is read system-coherent (sc0 sc1: from memory, past every
+// GPU cache, so no acquire fence per block), and a page-locked output is
+// written through (kHostStore) so that once the block's stores have drained
+// (vmcnt(0)) they are in host memory and one flag store publishes them — no
+// L2 writeback per block. Per-block system fences cost a write-back and an
+// invalidate of the whole XCD L2 each: 257 of them per chunk held every
+// chunk's last piece 65-240 us past its last byte in C1.
+using v4u = __attribute__((ext_vector_type(4))) unsigned;
+constexpr int kHostLoad  = 17;  // sc0 sc1
+constexpr int kHostStore = KF_STREAM_HOST_STORE_AUX;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *base, uint32_t bytes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, bytes, 0x00020000);
+}
+
+// 16 bytes (n of them at the end) of page-locked memory at base + off
+__device__ __forceinline__ void load16_host(__amdgpu_buffer_rsrc_t r, const char *base, uint32_t off,
+                                            uint32_t n, unsigned char *buf)
+{
+    if (n == 16 && ((reinterpret_cast<uintptr_t>(base) + off) & 15) == 0) {
+        const v4u v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kHostLoad);
+        std::memcpy(buf, &v, 16);
+    } else {
+        for (uint32_t i = 0; i < n; ++i) buf[i] = __builtin_amdgcn_raw_buffer_load_b8(r, off + i, 0, kHostLoad);
+    }
+}
+
+__device__ __forceinline__ void store16_host(__amdgpu_buffer_rsrc_t r, const char *base, uint32_t off,
+                                             uint32_t n, const unsigned char *buf)
+{
+    const uintptr_t a = reinterpret_cast<uintptr_t>(base) + off;
+    if (n == 16 && (a & 15) == 0) {
+        v4u v;
+        std::memcpy(&v, buf, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kHostStore);
+    } else if (n % 4 == 0 && (a & 3) == 0) {
+        for (uint32_t i = 0; i < n; i += 4) {
+            uint32_t w;
+            std::memcpy(&w, buf + i, 4);
+            __builtin_amdgcn_raw_buffer_store_b32(w, r, off + i, 0, kHostStore);
+        }
+    } else {
+        for (uint32_t i = 0; i < n; ++i) __builtin_amdgcn_raw_buffer_store_b8(buf[i], r, off + i, 0, kHostStore);
+    }
+}
+
+// this block's written-through stores have drained: flag it for the sender
 __device__ __forceinline__ void block_done(Ctl *c, uint32_t b)
 {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-        __threadfence_system();
         __hip_atomic_store(&c->done[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
-// 16 bytes of a lane from `src + off` (any alignment)
+// 16 bytes of a lane from `src + off` in HBM (any alignment)
 __device__ __forceinline__ void load16(const char *src, uint32_t n, unsigned char *buf)
 {
     if (n == 16 && (reinterpret_cast<uintptr_t>(src) & 15) == 0) {
@@ -141,7 +191,8 @@ __device__ __forceinline__ void store16(char *dst, uint32_t n, const unsigned ch
     }
 }
 
-// out = own + landed body, element by element, as each 4 KiB lands
+// out = own + landed body, element by element, as each 4 KiB lands; `mark`:
+// out is page-locked (written through, flagged), otherwise HBM
 template <typename T>
 __global__ void __launch_bounds__(kLanes)
     fold_kernel(const typename kf::Elt<T>::S *own, const char *landing,
@@ -158,19 +209,26 @@ __global__ void __launch_bounds__(kLanes)
     if (ok && off < end) {
         const uint32_t nb = min(16u, end - off);
         alignas(16) unsigned char buf[16];
-        load16(landing + off, nb, buf);
-        S peer[16 / sizeof(S)];
+        load16_host(rsrc(landing, len), landing, off, nb, buf);
+        S peer[16 / sizeof(S)], res[16 / sizeof(S)];
         std::memcpy(peer, buf, sizeof(peer));
         const size_t e0 = off / sizeof(S);
         for (uint32_t j = 0; j < nb / sizeof(S); ++j) {
-            out[e0 + j] = kf::finish<T, kf::OP_SUM>(
+            res[j] = kf::finish<T, kf::OP_SUM>(
                 kf::Elt<T>::template combine<kf::OP_SUM>(kf::Elt<T>::load(own[e0 + j]), peer[j]));
+        }
+        std::memcpy(buf, res, sizeof(res));
+        char *o = reinterpret_cast<char *>(out);
+        if (mark) {
+            store16_host(rsrc(o, len), o, off, nb, buf);
+        } else {
+            store16(o + off, nb, buf);
         }
     }
     if (mark) block_done(c, b);
 }
 
-// dst = landed body, as each 4 KiB lands
+// dst (HBM) = landed body, as each 4 KiB lands
 __global__ void __launch_bounds__(kLanes)
     copy_in_kernel(const char *landing, char *dst, uint32_t len, Ctl *c, unsigned long long *seen,
                    uint32_t epoch, unsigned long long limit)
@@ -184,12 +242,12 @@ __global__ void __launch_bounds__(kLanes)
     if (ok && off < end) {
         const uint32_t nb = min(16u, end - off);
         alignas(16) unsigned char buf[16];
-        load16(landing + off, nb, buf);
+        load16_host(rsrc(landing, len), landing, off, nb, buf);
         store16(dst + off, nb, buf);
     }
 }
 
-// host = src (HBM), each piece marked as its blocks finish
+// host (page-locked, written through) = src (HBM), each block flagged
 __global__ void __launch_bounds__(kLanes)
     copy_out_kernel(const char *src, char *host, uint32_t len, Ctl *c)
 {
@@ -199,7 +257,7 @@ __global__ void __launch_bounds__(kLanes)
         const uint32_t nb = min(16u, end - off);
         alignas(16) unsigned char buf[16];
         load16(src + off, nb, buf);
-        store16(host + off, nb, buf);
+        store16_host(rsrc(host, len), host, off, nb, buf);
     }
     block_done(c, blockIdx.x);
 }

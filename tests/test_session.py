@@ -251,11 +251,12 @@ def test_session_device_streamed(strategy, size, piece_kb, kind, batch_fold):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("stages", ["out", "fold", "in", "out+in"])
+@pytest.mark.parametrize("stages", ["0", "out", "fold", "in", "out+in"])
 def test_session_device_streamed_stages(stages):
-    """KUNGFU_AMD_STREAM names the stages streamed; each alone (and the two
-    that touch only one side of a hop) beside the whole-chunk others gives
-    the same bits, at np = 3 under BINARY_TREE (inner fold, leaf copies)."""
+    """KUNGFU_AMD_STREAM names the stages streamed (default "fold"); each
+    alone (and the two that touch only one side of a hop) beside the
+    whole-chunk others gives the same bits, at np = 3 under BINARY_TREE
+    (inner fold, leaf copies); "0" moves every chunk whole."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")

@@ -113,6 +113,31 @@ __global__ void __launch_bounds__(kLanes) fold_grid_k(const float4 *own, const f
     }
 }
 
+// 16-B buffer stores / loads with a cache policy (aux: 1 sc0, 16 sc1, 17 sc0 sc1)
+template <int AUX>
+__global__ void __launch_bounds__(kLanes) out_buf_k(const uint4 *src, char *host, unsigned *flags)
+{
+    const unsigned i = blockIdx.x * (kBlock / 16) + threadIdx.x;
+    const uint4 v    = src[i];
+    __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(host, 0, kLen, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const __attribute__((ext_vector_type(4))) unsigned *>(&v),
+                                           r, i * 16, 0, AUX);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(flags + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+template <int AUX>
+__global__ void __launch_bounds__(kLanes) in_buf_k(const char *host, uint4 *dst)
+{
+    const unsigned i = blockIdx.x * (kBlock / 16) + threadIdx.x;
+    __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(host), 0, kLen, 0x00020000);
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, i * 16, 0, AUX);
+    dst[i]       = make_uint4(v[0], v[1], v[2], v[3]);
+}
+
 template <typename F>
 float timed(hipStream_t s, F f)
 {
@@ -177,6 +202,11 @@ int main()
         put(m.name, "out_sys8_relaxed_add_us", timed(s, [&] { out_k<2, 1><<<g, b, 0, s>>>(src, h, done); }));
         put(m.name, "out_flag_sysfence_us", timed(s, [&] { out_flag_k<0><<<g, b, 0, s>>>(src, h, done); }));
         put(m.name, "out_flag_waitcnt_us", timed(s, [&] { out_flag_k<1><<<g, b, 0, s>>>(src, h, done); }));
+        put(m.name, "out_buf_sc0_flag_us", timed(s, [&] { out_buf_k<1><<<g, b, 0, s>>>(src, h, done); }));
+        put(m.name, "out_buf_sc1_flag_us", timed(s, [&] { out_buf_k<16><<<g, b, 0, s>>>(src, h, done); }));
+        put(m.name, "out_buf_sc0sc1_flag_us", timed(s, [&] { out_buf_k<17><<<g, b, 0, s>>>(src, h, done); }));
+        put(m.name, "in_buf_plain_us", timed(s, [&] { in_buf_k<0><<<g, b, 0, s>>>(h, dst); }));
+        put(m.name, "in_buf_sc0sc1_us", timed(s, [&] { in_buf_k<17><<<g, b, 0, s>>>(h, dst); }));
         put(m.name, "in_plain_noacq_us", timed(s, [&] { in_k<0, 0><<<g, b, 0, s>>>(h, dst, flag); }));
         put(m.name, "in_plain_one_acq_us", timed(s, [&] { in_k<1, 0><<<g, b, 0, s>>>(h, dst, flag); }));
         put(m.name, "in_plain_acq_poll_us", timed(s, [&] { in_k<2, 0><<<g, b, 0, s>>>(h, dst, flag); }));
