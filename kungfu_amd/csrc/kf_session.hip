@@ -568,8 +568,11 @@ struct kf_session {
     // and marks pieces of stream_piece bytes done for the sender. A mask of
     // the stages streamed ("out": a leaf's copy out of HBM before its send,
     // "fold": the completing fold, into the mirror and sent piece by piece —
-    // the default; "in": a bcast copy in; "1" all three, "0" none)
-    enum { kStreamOut = 1, kStreamFold = 2, kStreamIn = 4 };
+    // the default; "in": a bcast copy in; "1" all three, "0" none; and two
+    // that stream only where a stage is on the critical path: "last", the
+    // copy in of a call's last chunk, and "idle", the copy out of a chunk the
+    // sender will write at once, nothing staged ahead of it)
+    enum { kStreamOut = 1, kStreamFold = 2, kStreamIn = 4, kStreamInLast = 8, kStreamOutIdle = 16 };
     int stream_mode        = 0;
     uint32_t stream_piece  = 64u << 10;
     int stream_deadline_ms = 30000;
@@ -768,7 +771,7 @@ struct kf_session {
                     queue.pop_front();
                     l.unlock();
                     const size_t slot = (first_slot + staged.size()) % nslot;
-                    q.slot_ok = send_rc == KF_OK && stage_d2h(q, slot);
+                    q.slot_ok = send_rc == KF_OK && stage_d2h(q, slot, staged.empty());
                     tr(TR_TX_STAGED, q.chunk, static_cast<int>(q.flags), 1);
                     staged.push_back(std::move(q));
                     l.lock();
@@ -807,13 +810,14 @@ struct kf_session {
 
     // Queue the D2H of a device chunk into tx slot `slot` behind the event that
     // marks the chunk final on the caller's stream; tx_done[slot] marks it landed.
-    bool stage_d2h(SendItem &it, size_t slot)
+    bool stage_d2h(SendItem &it, size_t slot, bool idle)
     {
         if (it.host) return it.ready != nullptr;  // synced at send time
         bool ok = it.ready && it.bytes <= kChunk + 4096 &&
                   hipStreamWaitEvent(tx_stream, it.ready, 0) == hipSuccess;
         const size_t np = piece ? (it.bytes + piece - 1) / piece : 0;
-        if (ok && (stream_mode & kStreamOut) && it.bytes > 0) {  // one kernel, pieces marked as they land
+        const bool stream_out = (stream_mode & kStreamOut) || ((stream_mode & kStreamOutIdle) && idle);
+        if (ok && stream_out && it.bytes > 0) {  // one kernel, pieces marked as they land
             kf_stream::reset(tx_ctl[slot], stream_piece);
             ok = kf_stream::launch_copy_out(it.ptr, tx_dev[slot], static_cast<uint32_t>(it.bytes),
                                             stream_piece, tx_ctl_dev[slot], tx_stream) == KF_OK;
@@ -1408,7 +1412,7 @@ int kf_session::plan(SessOp &o)
         // reference does (recvOnto per predecessor), same bits
         for (auto &c : o.chunks) c.batched = false;
     }
-    if (device_mode && (stream_mode & (kStreamFold | kStreamIn)) &&
+    if (device_mode && (stream_mode & (kStreamFold | kStreamIn | kStreamInLast)) &&
         !take(ctl_pool, 2 * o.chunks.size() * sizeof(kf_stream::Ctl), true, &o.ctl)) {
         o.ctl = Lease{};  // this call moves whole chunks
     }
@@ -1551,7 +1555,8 @@ int kf_session::handle(SessOp &o, size_t i, uint32_t flags, int peer, int fd, co
     if (flags & KF_RCH_WAIT_RECV_BUF) {  // bcast: recvInto RecvBuf
         if (device_mode) {
             r = mem ? kf_ingest_copy_host(ingest, mem, len, dst, stream)
-                : streamed && (stream_mode & kStreamIn)
+                : streamed && ((stream_mode & kStreamIn) ||
+                               ((stream_mode & kStreamInLast) && o.remaining == 1))
                     ? kf_ingest_recv_into_streamed(ingest, fd, len, dst, stream,
                                                           stream_piece, ctl_at(o, i, 1),
                                                           ctl_at(o, i, 1, true),
@@ -2151,6 +2156,8 @@ kf_session_t *create_session(int rank, std::vector<PeerAddr> peers, const char *
             if (v.find("out") != std::string::npos) s->stream_mode |= kf_session::kStreamOut;
             if (v.find("fold") != std::string::npos) s->stream_mode |= kf_session::kStreamFold;
             if (v.find("in") != std::string::npos) s->stream_mode |= kf_session::kStreamIn;
+            if (v.find("last") != std::string::npos) s->stream_mode |= kf_session::kStreamInLast;
+            if (v.find("idle") != std::string::npos) s->stream_mode |= kf_session::kStreamOutIdle;
         }
         if (const char *e = std::getenv("KUNGFU_AMD_STREAM_PIECE_KB")) {
             const uint32_t kb = static_cast<uint32_t>(std::max(4, std::atoi(e)));
@@ -2185,7 +2192,8 @@ kf_session_t *create_session(int rank, std::vector<PeerAddr> peers, const char *
             hipStreamCreateWithFlags(&s->mir_stream, hipStreamNonBlocking) != hipSuccess) {
             s->mir_stream = nullptr;  // the copies stay on the caller's stream
         }
-        if ((s->stream_mode & kf_session::kStreamOut) && tx_ok) {  // a control block per tx slot
+        if ((s->stream_mode & (kf_session::kStreamOut | kf_session::kStreamOutIdle)) && tx_ok) {
+            // a control block per tx slot
             void *cp = nullptr, *cd = nullptr;
             tx_ok = hipHostMalloc(&cp, s->tx.size() * sizeof(kf_stream::Ctl),
                                   hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess &&

@@ -251,7 +251,7 @@ def test_session_device_streamed(strategy, size, piece_kb, kind, batch_fold):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("stages", ["0", "out", "fold", "in", "out+in"])
+@pytest.mark.parametrize("stages", ["0", "out", "fold", "in", "out+in", "fold+last+idle"])
 def test_session_device_streamed_stages(stages):
     """KUNGFU_AMD_STREAM names the stages streamed (default "fold"); each
     alone (and the two that touch only one side of a hop) beside the

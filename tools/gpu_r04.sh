@@ -88,7 +88,8 @@ or hier_all_reduce or fake_agent or rehearsal or branch_single_rank"
         --out "$OUT/c1_ab_stream.json" || exit $? ;;
   c1ab_fold)
     step c1ab_fold 900 python tools/c1_ab.py device device:KUNGFU_AMD_STREAM=0 \
-        device:KUNGFU_AMD_STREAM=fold+out device:KUNGFU_AMD_STREAM=1 cpu --repeats 5 \
+        device:KUNGFU_AMD_STREAM=fold+last device:KUNGFU_AMD_STREAM=fold+idle \
+        device:KUNGFU_AMD_STREAM=fold+last+idle cpu --repeats 5 \
         --out "$OUT/c1_ab_fold.json" || exit $? ;;
   c1trace)
     step c1trace 600 python tools/c1_trace.py --modes device,cpu --steps 60 \
