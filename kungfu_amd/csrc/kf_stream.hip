@@ -7,18 +7,18 @@
 // between polls, a system acquire fence whenever the count moves, then the
 // count is re-published in HBM (an agent-scope release store of epoch:bytes
 // into a device word). The data blocks poll that device word (agent-scope
-// loads, served by the L2s: no PCIe reads), each then takes one system
-// acquire fence and folds (SUM, the dtype's own arithmetic:
-// kf_reduce_kernels.hpp Elt<T>) or copies its bytes. With every block polling
-// the host word instead, 257 pollers per chunk slowed the host thread that
-// reads the socket (C1 streamed: 2.1 ms against 0.7 whole-chunk). A deadline
-// (wall clock) and the host's abort word end every wait. A block whose output
-// is page-locked memory a sender reads (`mark`) drains its stores (every
-// wave's vmcnt(0), the barrier), its first lane releases them (one system
-// fence per block, not per wave) and stores the block's done flag: one word
-// per block, no atomics on host memory (kf_stream.hpp has the prices). The
-// host sender spins on those flags and writes every piece once all its
-// blocks are flagged. Bits: element-wise, so those of one whole-chunk launch.
+// loads, served by the L2s: no PCIe reads) and then fold (SUM, the dtype's
+// own arithmetic: kf_reduce_kernels.hpp Elt<T>) or copy their bytes, reading
+// the landing slot system-coherent (sc0 sc1 buffer loads: from memory, past
+// every GPU cache) and writing a page-locked output through the L2 (sc1), so
+// no block takes an L2-wide fence. A block whose output a sender reads
+// (`mark`) drains its stores (every wave's vmcnt(0), the barrier) and its
+// first lane stores the block's done flag: one word per block, no atomics on
+// host memory. The host sender spins on those flags and writes every piece
+// once all its blocks are flagged. A deadline (wall clock) and the host's
+// abort word end every wait. kf_stream.hpp and DESIGN.md §4 have the
+// measurements behind each of these choices. Bits: element-wise, so those of
+// one whole-chunk launch.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>

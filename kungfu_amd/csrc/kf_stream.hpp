@@ -18,12 +18,16 @@
 // kernel.
 //
 // What the GPU pays for it (tools/explore/stream_probe.hip, 1 MiB, 256
-// blocks, on the box): plain 16-B stores to page-locked memory 20 us; the
-// same with one system-scope atomic add per block onto a per-piece counter
-// 254 us (atomics to host memory serialise) — hence one flag word per block
-// behind a system release fence: 36 us. Reads: plain 28 us, one acquire
-// fence per block 59 us, an acquire load per poll an invalidate per poll —
-// so the wait polls with relaxed system-scope loads and fences once.
+// blocks, on the box): plain 16-B stores to page-locked memory 20 us; with
+// one system-scope atomic add per block onto a per-piece counter 254 us
+// (atomics to host memory serialise); one flag word per block behind a
+// system release fence 36 us; written-through (sc1) stores drained before
+// the flag 21.6 us — the shipped form. Reads: plain 24-29 us, one acquire
+// fence per block 54-61 us, system-coherent (sc0 sc1) loads 26.5 us — the
+// shipped form. In a running session the per-block fences also serialise on
+// each XCD's L2 (a write-back and an invalidate of the whole L2 each, 257
+// per chunk): the last piece came 65-240 us after the last byte with them,
+// 4-5 us without.
 #pragma once
 #include <stddef.h>
 #include <stdint.h>
