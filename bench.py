@@ -590,8 +590,8 @@ def c1_child(args):
     # sum_r (r+1) * (i mod 1024) / 1024: every partial sum is exact in fp32
     want = (npeers * (npeers + 1) // 2 * (np.arange(C1_ELEMS) % 1024) / 1024).astype(np.float32)
     if args.c1_mode.startswith("device"):
-        if args.c1_mode == "device_chain":  # the reference's 2-input recvOnto chain
-            os.environ["KUNGFU_AMD_BATCH_FOLD"] = "0"
+        if args.c1_mode == "device_batched":  # A/B: the k-input fold at the root
+            os.environ["KUNGFU_AMD_BATCH_FOLD"] = "1"
         if args.c1_mode == "device_nomirror":  # A/B: the root's result via D2H again
             os.environ["KUNGFU_AMD_ROOT_MIRROR"] = "0"
         dev = torch.device("cuda", 0)
@@ -679,11 +679,25 @@ def gpu_local_cpus(index=0):
     return sorted(cpus) or None
 
 
+# C1's peers are np processes sharing ONE GPU. Each HIP process maps its
+# streams onto up to GPU_MAX_HW_QUEUES hardware queues (4 by default); past
+# what the GPU schedules at once the queues are time-sliced and every hop
+# waits for its process's turn (np = 8: 12.4 ms per all-reduce at 4 queues
+# per peer, 3.3 ms at 2; np = 4: 1.60 -> 1.39 ms; np = 2: 0.65 -> 0.61 ms;
+# profiles/r04/c1_ab_np{2,4,8}_hwq_r04z.json). Two per peer (KUNGFU_AMD_C1_HW_QUEUES
+# overrides it: the box itself exports GPU_MAX_HW_QUEUES=4, HIP's default, so
+# an inherited value says nothing). The same applies to any deployment that
+# puts several peers on one GPU.
+C1_HW_QUEUES = "2"
+
+
 def c1_run(npeers, modes, steps, warmup, timeout=600, cpus=None):
     """Launch the np peers per mode (subprocesses, one unix socket each);
     {mode: rank 0's record}."""
     import subprocess
     import tempfile
+    env = dict(os.environ)
+    env["GPU_MAX_HW_QUEUES"] = os.environ.get("KUNGFU_AMD_C1_HW_QUEUES", C1_HW_QUEUES)
     res = {}
     for mode in modes:
         with tempfile.TemporaryDirectory() as d:
@@ -693,7 +707,7 @@ def c1_run(npeers, modes, steps, warmup, timeout=600, cpus=None):
             if cpus:
                 cmd += ["--c1-cpus", ",".join(map(str, cpus))]
             procs = [subprocess.Popen(cmd + ["--c1-rank", str(r)], stdout=subprocess.PIPE,
-                                      text=True, cwd=ROOT) for r in range(npeers)]
+                                      text=True, cwd=ROOT, env=env) for r in range(npeers)]
             try:
                 outs = [p.communicate(timeout=timeout)[0] for p in procs]
             except subprocess.TimeoutExpired:
@@ -743,14 +757,15 @@ def c1_summary(steps=100, warmup=10, repeats=5):
            "modes": "device: bucket in HBM, HIP fold; cpu: bucket in host memory, the "
                     "reference's CPU fold; cpu_dev: bucket in HBM reduced the reference's "
                     "way for GPU tensors (D2H, the cpu all-reduce, H2D)",
-           "cpus": ("the GPU's NUMA node: %d CPUs" % len(cpus)) if cpus else "not pinned"}
+           "cpus": ("the GPU's NUMA node: %d CPUs" % len(cpus)) if cpus else "not pinned",
+           "hw_queues_per_peer": os.environ.get("KUNGFU_AMD_C1_HW_QUEUES", C1_HW_QUEUES)}
     out.update(res)
     out["correct"] = all(r.get("correct") is True for r in res.values())
     return out
 
 
 def c1_parent(args):
-    modes = ("device", "device_chain", "dropin", "cpu", "cpu_dev") if args.c1_np > 2 else \
+    modes = ("device", "device_batched", "dropin", "cpu", "cpu_dev") if args.c1_np > 2 else \
         ("device", "device_nomirror", "dropin", "cpu", "cpu_dev")
     if args.c1_modes:
         modes = tuple(args.c1_modes.split(","))

@@ -254,7 +254,7 @@ kf_ingest_t *kf_ingest_create(size_t slot_bytes, int nslots)
         if (hipHostMalloc(&g->host[i], slot_bytes, hipHostMallocDefault) !=
                 hipSuccess ||
             hipHostGetDevicePointer(&g->hmap[i], g->host[i], 0) != hipSuccess ||
-            hipEventCreateWithFlags(&g->done[i], hipEventDisableTiming) != hipSuccess) {
+            hipEventCreateWithFlags(&g->done[i], kf_sync::event_flags()) != hipSuccess) {
             t_ingest_error = "kf_ingest_create: HIP allocation failed";
             delete g;
             return nullptr;
@@ -401,7 +401,10 @@ int kf_ingest_send_from_device(kf_ingest_t *g, int fd, const char *name,
     if (rc != KF_OK) return rc;
     hipStream_t s = static_cast<hipStream_t>(stream);
     ING_HIP(hipMemcpyAsync(g->host[slot], dev_src, bytes, hipMemcpyDeviceToHost, s));
-    ING_HIP(hipStreamSynchronize(s));
+    if (kf_sync::stream_sync(s) != KF_OK) {
+        t_ingest_error = "stream sync";
+        return KF_ERR_HIP;
+    }
     return kf_rch_send(fd, name, flags, g->host[slot], static_cast<uint32_t>(bytes));
 }
 

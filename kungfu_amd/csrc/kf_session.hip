@@ -597,7 +597,13 @@ struct kf_session {
     std::deque<FoldJob *> fq, fdone;
     bool fstop = false;
     std::vector<std::vector<char> *> fbodies;  // free chunk bodies (poll thread)
-    int batch_fold = 1;         // device mode: k-input fold at multi-predecessor nodes
+    // device mode: a multi-predecessor node stages its arrivals in HBM and
+    // folds them in one k-input launch (1), or folds each as it lands, the
+    // reference's 2-input recvOnto chain (0, the default since round 4: with
+    // the completing fold streamed the chain wins at every np measured —
+    // C1 np = 3 / 4 / 8: 1.05 / 1.33 / 3.07 ms against 1.29 / 1.44 / 3.28;
+    // DESIGN.md §4)
+    int batch_fold = 0;
     // per collective in flight, lent from these pools (device mode):
     //  * HBM staging for the k-input fold: [predecessor arrival][bucket bytes];
     //  * a page-locked mirror of the bucket. A node that sends its finished
@@ -1014,7 +1020,7 @@ struct kf_session {
                 ev_pool.pop_back();
             }
         }
-        if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+        if (!e && hipEventCreateWithFlags(&e, kf_sync::event_flags()) != hipSuccess) return nullptr;
         if (hipEventRecord(e, static_cast<hipStream_t>(stream)) != hipSuccess) {
             (void)hipEventDestroy(e);
             return nullptr;
@@ -1035,7 +1041,7 @@ struct kf_session {
         }
         while (out->size() < n) {
             hipEvent_t e = nullptr;
-            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+            if (hipEventCreateWithFlags(&e, kf_sync::event_flags()) != hipSuccess) {
                 give_events(*out);
                 return false;
             }
@@ -1759,10 +1765,10 @@ int kf_session::complete(SessOp &o)
     if (!o.trivial && device_mode) {
         const int irc = kf_ingest_sync(ingest);
         if (irc != KF_OK && rc == KF_OK) rc = fail(irc, kf_ingest_last_error());
-        if (hipStreamSynchronize(static_cast<hipStream_t>(o.stream)) != hipSuccess && rc == KF_OK) {
+        if (kf_sync::stream_sync(o.stream) != KF_OK && rc == KF_OK) {
             rc = fail(KF_ERR_HIP, "stream sync");
         }
-        if (o.mir_side && hipStreamSynchronize(mir_stream) != hipSuccess && rc == KF_OK) {
+        if (o.mir_side && kf_sync::stream_sync(mir_stream) != KF_OK && rc == KF_OK) {
             rc = fail(KF_ERR_HIP, "mirror stream sync");
         }
     }
@@ -2181,7 +2187,7 @@ kf_session_t *create_session(int rank, std::vector<PeerAddr> peers, const char *
                 s->tx.push_back(p);
                 s->tx_dev.push_back(dv);
             }
-            tx_ok = tx_ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+            tx_ok = tx_ok && hipEventCreateWithFlags(&e, kf_sync::event_flags()) == hipSuccess;
             if (tx_ok) s->tx_done.push_back(e);
         }
         if (hipStreamCreateWithFlags(&s->tx_stream, hipStreamNonBlocking) != hipSuccess) {
@@ -2207,7 +2213,7 @@ kf_session_t *create_session(int rank, std::vector<PeerAddr> peers, const char *
             s->max_pieces = (kChunk + 4096 + s->piece - 1) / s->piece;
             for (size_t k = 0; k < s->tx.size() * s->max_pieces && tx_ok; ++k) {
                 hipEvent_t e = nullptr;
-                tx_ok = hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+                tx_ok = hipEventCreateWithFlags(&e, kf_sync::event_flags()) == hipSuccess;
                 if (tx_ok) s->tx_piece_ev.push_back(e);
             }
         }

@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <immintrin.h>
 
@@ -426,3 +427,34 @@ uint32_t ready_run(const Ctl *c, uint32_t k, uint32_t len)
     return j - k;
 }
 }  // namespace kf_stream
+
+namespace kf_sync
+{
+namespace
+{
+bool blocking()
+{
+    static const bool b = [] {
+        const char *e = std::getenv("KUNGFU_AMD_BLOCKING_SYNC");
+        return e && std::atoi(e) != 0;
+    }();
+    return b;
+}
+}  // namespace
+
+unsigned event_flags()
+{
+    return hipEventDisableTiming | (blocking() ? hipEventBlockingSync : 0u);
+}
+
+int stream_sync(void *stream)
+{
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (!blocking()) return hipStreamSynchronize(s) == hipSuccess ? KF_OK : KF_ERR_HIP;
+    hipEvent_t e = nullptr;  // a blocking event behind the stream's work: the thread sleeps
+    const bool ok = hipEventCreateWithFlags(&e, event_flags()) == hipSuccess &&
+                    hipEventRecord(e, s) == hipSuccess && hipEventSynchronize(e) == hipSuccess;
+    if (e) (void)hipEventDestroy(e);
+    return ok ? KF_OK : KF_ERR_HIP;
+}
+}  // namespace kf_sync

@@ -76,6 +76,18 @@ int wait_piece(const Ctl *c, uint32_t k, uint32_t len, int timeout_ms);
 uint32_t ready_run(const Ctl *c, uint32_t k, uint32_t len);
 }  // namespace kf_stream
 
+// How the library's host threads wait for the GPU. HIP's default event wait
+// spins a core; with many peer processes on one host (C1 at np = 8: 8
+// processes, 2-3 waiting threads each, on a 16-CPU quota) spinning waits
+// burn the quota. KUNGFU_AMD_BLOCKING_SYNC=1 makes every event the library
+// creates a blocking-sync event (the thread sleeps until the GPU signals)
+// and every stream wait an event wait.
+namespace kf_sync
+{
+unsigned event_flags();          // for hipEventCreateWithFlags
+int stream_sync(void *stream);   // KF_OK or KF_ERR_HIP
+}  // namespace kf_sync
+
 // kf_ingest.hip: the streamed receives (body read into the next landing slot
 // while the kernel launched before it folds / copies each landed block)
 int kf_ingest_recv_onto_streamed(kf_ingest_t *g, int fd, uint32_t len, void *dev_acc,

@@ -275,7 +275,8 @@ def test_session_device_lease_caps(strategy):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     run(4, "device", "rand", (5 << 20) // 4 + 17, strategy=strategy,
-        env={"KUNGFU_AMD_STAGE_CAP_MB": "1", "KUNGFU_AMD_MIRROR_CAP_MB": "1"})
+        env={"KUNGFU_AMD_STAGE_CAP_MB": "1", "KUNGFU_AMD_MIRROR_CAP_MB": "1",
+             "KUNGFU_AMD_BATCH_FOLD": "1"})
 
 
 @pytest.mark.gpu
@@ -286,7 +287,8 @@ def test_session_async_any_order_device_capped():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     _run_any_order(3, "device", None, env={"KUNGFU_AMD_STAGE_CAP_MB": "12",
-                                           "KUNGFU_AMD_MIRROR_CAP_MB": "6"})
+                                           "KUNGFU_AMD_MIRROR_CAP_MB": "6",
+                                           "KUNGFU_AMD_BATCH_FOLD": "1"})
 
 
 @pytest.mark.gpu
@@ -295,7 +297,7 @@ def test_session_device_batched_iota():
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    run(4, "device", "iota", (3 << 20) // 4 + 5)
+    run(4, "device", "iota", (3 << 20) // 4 + 5, env={"KUNGFU_AMD_BATCH_FOLD": "1"})
 
 
 def _repeat_body(rank, size, sock_dir, strategy, steps, errq):
