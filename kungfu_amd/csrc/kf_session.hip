@@ -2227,7 +2227,10 @@ kf_session_t *create_session(int rank, std::vector<PeerAddr> peers, const char *
         delete s;
         return nullptr;
     }
-    s->sender = std::thread([s] { s->sender_loop(); });
+    s->sender = std::thread([s] {
+        if (s->device_mode) (void)hipSetDevice(s->device);  // its copy-out kernels
+        s->sender_loop();
+    });
     return s;
 }
 }  // namespace

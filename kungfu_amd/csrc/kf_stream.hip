@@ -286,14 +286,26 @@ struct Seen {
     uint32_t epoch;
 };
 
+// g_seen has one instance per device: its address on the current one
+unsigned long long *seen_base()
+{
+    constexpr int kMaxDevices = 64;
+    static std::atomic<unsigned long long *> base[kMaxDevices] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return nullptr;
+    unsigned long long *b = base[dev].load(std::memory_order_acquire);
+    if (!b) {
+        void *p = nullptr;
+        if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_seen)) != hipSuccess) return nullptr;
+        b = static_cast<unsigned long long *>(p);
+        base[dev].store(b, std::memory_order_release);
+    }
+    return b;
+}
+
 Seen next_seen()
 {
-    static unsigned long long *base = [] {
-        void *p = nullptr;
-        return hipGetSymbolAddress(&p, HIP_SYMBOL(g_seen)) == hipSuccess
-                   ? static_cast<unsigned long long *>(p)
-                   : nullptr;
-    }();
+    unsigned long long *base   = seen_base();
     const unsigned long long n = g_launches.fetch_add(1, std::memory_order_relaxed);
     // a word is reused kSeen launches later; the epoch tells its owners apart
     return Seen{base ? base + n % kSeen : nullptr, static_cast<uint32_t>(n + 1)};
