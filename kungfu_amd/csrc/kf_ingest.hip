@@ -304,7 +304,14 @@ int kf_ingest_recv_into(kf_ingest_t *g, int fd, uint32_t len, void *dev_dst,
     rc = kf_rch_recv_body(fd, g->host[slot], len);
     if (rc != KF_OK || len == 0) return rc;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    ING_HIP(hipMemcpyAsync(dev_dst, g->host[slot], len, hipMemcpyHostToDevice, s));
+    if (kf_stream::copy_kernels()) {
+        if (kf_stream::launch_copy(dev_dst, g->hmap[slot], len, s) != KF_OK) {
+            t_ingest_error = "copy kernel launch";
+            return KF_ERR_HIP;
+        }
+    } else {
+        ING_HIP(hipMemcpyAsync(dev_dst, g->host[slot], len, hipMemcpyHostToDevice, s));
+    }
     ING_HIP(hipEventRecord(g->done[slot], s));
     {
         std::lock_guard<std::mutex> lock(g->mu);
@@ -440,7 +447,14 @@ int kf_ingest_copy_host(kf_ingest_t *g, const void *host, uint32_t len, void *de
     if (rc != KF_OK || len == 0) return rc;
     std::memcpy(g->host[slot], host, len);
     hipStream_t s = static_cast<hipStream_t>(stream);
-    ING_HIP(hipMemcpyAsync(dev_dst, g->host[slot], len, hipMemcpyHostToDevice, s));
+    if (kf_stream::copy_kernels()) {
+        if (kf_stream::launch_copy(dev_dst, g->hmap[slot], len, s) != KF_OK) {
+            t_ingest_error = "copy kernel launch";
+            return KF_ERR_HIP;
+        }
+    } else {
+        ING_HIP(hipMemcpyAsync(dev_dst, g->host[slot], len, hipMemcpyHostToDevice, s));
+    }
     ING_HIP(hipEventRecord(g->done[slot], s));
     {
         std::lock_guard<std::mutex> lock(g->mu);

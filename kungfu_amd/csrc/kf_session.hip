@@ -836,6 +836,8 @@ struct kf_session {
                      hipEventRecord(tx_piece_ev[slot * max_pieces + k], tx_stream) == hipSuccess;
             }
             it.staged_pieces = static_cast<int>(np);
+        } else if (kf_stream::copy_kernels()) {
+            ok = ok && kf_stream::launch_copy(tx_dev[slot], it.ptr, it.bytes, tx_stream) == KF_OK;
         } else {
             ok = ok &&
                  hipMemcpyAsync(tx[slot], it.ptr, it.bytes, hipMemcpyDeviceToHost, tx_stream) ==
@@ -1492,9 +1494,14 @@ int kf_session::mirror_done(SessOp &o, size_t i, char *dst)
     if (!c.mirror_ev) return fail(KF_ERR_HIP, "mirror event");
     const bool side = mir_stream && c.st->bcast.prev[rank].empty();
     hipStream_t hs  = side ? mir_stream : static_cast<hipStream_t>(o.stream);
-    if ((side && hipStreamWaitEvent(mir_stream, c.mirror_ev, 0) != hipSuccess) ||
-        hipMemcpyAsync(dst, cptr(o, o.mir.p, i), clen(o, i), hipMemcpyHostToDevice, hs) !=
-            hipSuccess) {
+    const bool waited = !side || hipStreamWaitEvent(mir_stream, c.mirror_ev, 0) == hipSuccess;
+    const bool copied =
+        waited &&
+        (kf_stream::copy_kernels()
+             ? kf_stream::launch_copy(dst, cptr(o, o.mir.dev, i), clen(o, i), hs) == KF_OK
+             : hipMemcpyAsync(dst, cptr(o, o.mir.p, i), clen(o, i), hipMemcpyHostToDevice, hs) ==
+                   hipSuccess);
+    if (!copied) {
         return fail(KF_ERR_HIP, "mirror copy to HBM");
     }
     if (side) o.mir_side = true;

@@ -263,6 +263,19 @@ __global__ void __launch_bounds__(kLanes)
     block_done(c, blockIdx.x);
 }
 
+// dst = src, 16 B per lane, one 4 KiB block per block of the grid
+__global__ void __launch_bounds__(kLanes) copy_kernel(char *dst, const char *src, size_t len)
+{
+    const size_t start = static_cast<size_t>(blockIdx.x) * kBlockBytes;
+    const size_t off   = start + threadIdx.x * 16;
+    if (off < len) {
+        const uint32_t nb = static_cast<uint32_t>(min(static_cast<size_t>(16), len - off));
+        alignas(16) unsigned char buf[16];
+        load16(src + off, nb, buf);
+        store16(dst + off, nb, buf);
+    }
+}
+
 unsigned long long ticks(int ms)
 {
     static const int khz = [] {
@@ -398,6 +411,25 @@ int launch_copy_out(const void *src, void *host_dev, uint32_t len, uint32_t piec
     if (!fits(len, piece)) return KF_ERR_ARG;
     copy_out_kernel<<<blocks(len), kLanes, 0, static_cast<hipStream_t>(stream)>>>(
         static_cast<const char *>(src), static_cast<char *>(host_dev), len, c_dev);
+    return hipGetLastError() == hipSuccess ? KF_OK : KF_ERR_HIP;
+}
+
+bool copy_kernels()
+{
+    static const bool on = [] {
+        const char *e = std::getenv("KUNGFU_AMD_COPY_KERNEL");
+        return e && std::atoi(e) != 0;
+    }();
+    return on;
+}
+
+int launch_copy(void *dst, const void *src, size_t len, void *stream)
+{
+    if (len == 0) return KF_OK;
+    const size_t nblk = (len + kBlockBytes - 1) / kBlockBytes;
+    if (nblk > 0x7fffffffu) return KF_ERR_ARG;
+    copy_kernel<<<static_cast<unsigned>(nblk), kLanes, 0, static_cast<hipStream_t>(stream)>>>(
+        static_cast<char *>(dst), static_cast<const char *>(src), len);
     return hipGetLastError() == hipSuccess ? KF_OK : KF_ERR_HIP;
 }
 

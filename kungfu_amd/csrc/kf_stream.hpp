@@ -69,6 +69,14 @@ int launch_copy_in(const void *landing_dev, void *dst, uint32_t len, uint32_t pi
 int launch_copy_out(const void *src, void *host_dev, uint32_t len, uint32_t piece, Ctl *c_dev,
                     void *stream);
 
+// A chunk's copy between HBM and page-locked memory (either way; device
+// addresses) by a kernel instead of hipMemcpyAsync: on some boxes the DMA
+// engines take 150 us for 1 MiB where a kernel takes 20-27 us
+// (profiles/r04/stream_probe*_r04s3.json). Used where copy_kernels() says so
+// (KUNGFU_AMD_COPY_KERNEL=1).
+bool copy_kernels();
+int launch_copy(void *dst, const void *src, size_t len, void *stream);
+
 // Host side of the sender, for a chunk of len bytes: wait until piece k is
 // final (KF_OK), the device gave up (KF_ERR_HIP) or timeout_ms passed
 // (KF_ERR_TIMEOUT); how many pieces from k on are final already.

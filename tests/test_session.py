@@ -265,6 +265,21 @@ def test_session_device_streamed_stages(stages):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("strategy,size,stages", [("STAR", 2, "fold"), ("BINARY_TREE", 4, "0"),
+                                                  ("CLIQUE", 3, "fold"), ("RING", 3, "1")])
+def test_session_device_copy_kernels(strategy, size, stages):
+    """KUNGFU_AMD_COPY_KERNEL=1: a chunk's copies between HBM and page-locked
+    memory (the D2H into a send slot, the H2D out of a landing slot, the
+    mirror's copy to HBM) run as kernels instead of DMA copies; same bits,
+    with and without the streamed stages (a ragged last chunk included)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    run(size, "device", "rand", (5 << 20) // 4 + 17, strategy=strategy,
+        env={"KUNGFU_AMD_COPY_KERNEL": "1", "KUNGFU_AMD_STREAM": stages})
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("strategy", ["STAR", "BINARY_TREE", "CLIQUE"])
 def test_session_device_lease_caps(strategy):
     """HBM staging and page-locked mirrors come from
