@@ -984,6 +984,8 @@ def main():
         }
         if phase_us is not None:
             out["collective"]["phase_us"] = phase_us
+        out["collective"].update(_rccl_report(_NATIVE.get("ex") if fallback is None else None,
+                                              world, fallback))
         if trial is not None:
             out["collective"]["schedule_trial_ms"] = {
                 k: None if v is None else round(v * 1e3, 4) for k, v in trial.items()}
@@ -1445,6 +1447,30 @@ def _primary_exchange(args, rank, world, dev):
         ex.close()
     return Exchange(), how_torch, box.get("err", "not ready within %.0f s or failed on "
                                                  "another rank" % args.native_timeout)
+
+
+def _rccl_report(native, world, fallback):
+    """What RCCL itself says about the primary exchange, for the N > 1 line:
+    the communicator's rank count (ncclCommCount), RCCL's version
+    (ncclGetVersion) and which exchange ran. A communicator whose count is
+    not N means the ranks did not form one N-rank RCCL world (each may be
+    timing a one-rank communicator), so the line would measure nothing of
+    xGMI: that ends the run loudly instead of printing a number."""
+    if native is None:
+        return {"exchange_kind": "torch.distributed", "rccl_world": None, "rccl_version": None,
+                "why_not_native": fallback}
+    count, ver = native.transport_info()
+    if count == -1:  # a host-provided transport (tests' rccl1): RCCL not asked
+        return {"exchange_kind": "native C-ABI (kf_exchange), host transport",
+                "rccl_world": None, "rccl_version": None}
+    if count != world:
+        raise SystemExit("bench.py: the native exchange's RCCL communicator holds %d ranks, not "
+                         "WORLD_SIZE %d: no N-rank collective would be timed" % (count, world))
+    vs = None
+    if ver:  # NCCL_VERSION_CODE: major * 10000 + minor * 100 + patch
+        vs = "%d.%d.%d" % (ver // 10000, ver // 100 % 100, ver % 100)
+    return {"exchange_kind": "native C-ABI (kf_exchange)", "rccl_world": count,
+            "rccl_version": vs, "rccl_version_code": ver}
 
 
 def _exchange(kind):

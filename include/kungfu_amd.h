@@ -565,6 +565,14 @@ int kf_exchange_wait_all(kf_exchange_t *ex, int32_t *order);
  * (ncclCommGetAsyncError). */
 int kf_exchange_check(kf_exchange_t *ex);
 int kf_exchange_info(kf_exchange_t *ex, int *rank, int *world, int *device);
+/* What the transport itself reports, for the bench line and logs: the RCCL
+ * communicator's rank count (ncclCommCount) and RCCL's version
+ * (ncclGetVersion, e.g. 22703). -1 / 0 for a host's own transport
+ * (kf_exchange_create_transport) or a librccl without the symbol. A count
+ * other than the exchange's world means the ranks did not form one
+ * communicator. (The reference's nccl path asks neither,
+ * srcs/cpp/src/nccl/gpu_collective.cpp:151-165; diagnostic only.) */
+int kf_exchange_transport_info(kf_exchange_t *ex, int *comm_count, int *rccl_version);
 void kf_exchange_destroy(kf_exchange_t *ex);
 const char *kf_exchange_last_error(void);
 

@@ -88,6 +88,7 @@ EXPORTED = (
     "kf_exchange_wait_all",
     "kf_exchange_check",
     "kf_exchange_info",
+    "kf_exchange_transport_info",
     "kf_exchange_destroy",
     "kf_exchange_last_error",
     "kf_exchange_all_reduce_named",
@@ -327,6 +328,8 @@ def load():
     lib.kf_exchange_phase_times.restype = c_int
     lib.kf_exchange_info.argtypes = [c_void_p, P(c_int), P(c_int), P(c_int)]
     lib.kf_exchange_info.restype = c_int
+    lib.kf_exchange_transport_info.argtypes = [c_void_p, P(c_int), P(c_int)]
+    lib.kf_exchange_transport_info.restype = c_int
     lib.kf_exchange_destroy.argtypes = [c_void_p]
     lib.kf_exchange_destroy.restype = None
     lib.kf_exchange_last_error.argtypes = []

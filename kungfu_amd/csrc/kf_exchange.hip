@@ -102,6 +102,9 @@ struct Rccl {
     decltype(&::ncclGroupStart) GroupStart               = nullptr;
     decltype(&::ncclGroupEnd) GroupEnd                   = nullptr;
     decltype(&::ncclGetErrorString) GetErrorString       = nullptr;
+    // optional (reporting only): kf_exchange_transport_info
+    decltype(&::ncclCommCount) CommCount                 = nullptr;
+    decltype(&::ncclGetVersion) GetVersion               = nullptr;
 };
 
 const Rccl &rccl()
@@ -134,6 +137,8 @@ const Rccl &rccl()
         KF_LOAD(GroupEnd, ncclGroupEnd)
         KF_LOAD(GetErrorString, ncclGetErrorString)
 #undef KF_LOAD
+        x.CommCount  = reinterpret_cast<decltype(x.CommCount)>(dlsym(h, "ncclCommCount"));
+        x.GetVersion = reinterpret_cast<decltype(x.GetVersion)>(dlsym(h, "ncclGetVersion"));
         x.ok = true;
         return x;
     }();
@@ -1802,6 +1807,29 @@ int kf_exchange_info(kf_exchange_t *ex, int *rank, int *world, int *device)
     if (rank) *rank = ex->rank;
     if (world) *world = ex->world;
     if (device) *device = ex->device;
+    return KF_OK;
+}
+
+int kf_exchange_transport_info(kf_exchange_t *ex, int *comm_count, int *rccl_version)
+{
+    if (!ex) return KF_ERR_ARG;
+    if (comm_count) *comm_count = -1;
+    if (rccl_version) *rccl_version = 0;
+    if (!ex->builtin) return KF_OK;  // a host's own transport: nothing to ask RCCL
+    const Rccl &r = rccl();
+    if (!r.ok) return fail(KF_ERR_RCCL, r.why);
+    if (comm_count && r.CommCount) {
+        int n = -1;
+        const ncclResult_t e = r.CommCount(static_cast<ncclComm_t>(ex->comm), &n);
+        if (e != ncclSuccess) return nccl_fail(e, "ncclCommCount");
+        *comm_count = n;
+    }
+    if (rccl_version && r.GetVersion) {
+        int v = 0;
+        const ncclResult_t e = r.GetVersion(&v);
+        if (e != ncclSuccess) return nccl_fail(e, "ncclGetVersion");
+        *rccl_version = v;
+    }
     return KF_OK;
 }
 

@@ -80,10 +80,22 @@ int read_full(int fd, void *buf, size_t n)
     return KF_OK;
 }
 
+// writev without SIGPIPE: a peer that died must fail the write (EPIPE), not
+// kill this process (a C or Go host does not ignore SIGPIPE as Python does)
+inline ssize_t writev_nosig(int fd, struct iovec *iov, int cnt)
+{
+    struct msghdr m {};
+    m.msg_iov    = iov;
+    m.msg_iovlen = static_cast<size_t>(cnt);
+    const ssize_t w = ::sendmsg(fd, &m, MSG_NOSIGNAL);
+    if (w < 0 && errno == ENOTSOCK) return ::writev(fd, iov, cnt);
+    return w;
+}
+
 int write_full(int fd, struct iovec *iov, int cnt)
 {
     while (cnt > 0) {
-        ssize_t w = ::writev(fd, iov, cnt);
+        ssize_t w = writev_nosig(fd, iov, cnt);
         if (w < 0) {
             if (errno == EINTR) continue;
             return io_fail("writev");
@@ -534,22 +546,23 @@ int streamed(kf_ingest_t *g, int fd, uint32_t len, void *stream, kf_stream::Ctl 
 int kf_ingest_recv_onto_streamed(kf_ingest_t *g, int fd, uint32_t len, void *dev_acc,
                                  const void *dev_own, KungFu_Datatype dt, void *stream,
                                  uint32_t piece, kf_stream::Ctl *ctl, kf_stream::Ctl *ctl_dev,
-                                 int deadline_ms, bool mark)
+                                 kf_stream::Board *board, int deadline_ms, bool mark)
 {
-    if (!g || !dev_acc || !ctl || !ctl_dev) return KF_ERR_ARG;
+    if (!g || !dev_acc || !ctl || !ctl_dev || !board) return KF_ERR_ARG;
     return streamed(g, fd, len, stream, ctl, piece, [&](void *landing) {
         return kf_stream::launch_fold(dt, dev_own ? dev_own : dev_acc, landing, dev_acc, len,
-                                      piece, ctl_dev, deadline_ms, mark, stream);
+                                      piece, ctl_dev, board, deadline_ms, mark, stream);
     });
 }
 
 int kf_ingest_recv_into_streamed(kf_ingest_t *g, int fd, uint32_t len, void *dev_dst,
                                  void *stream, uint32_t piece, kf_stream::Ctl *ctl,
-                                 kf_stream::Ctl *ctl_dev, int deadline_ms)
+                                 kf_stream::Ctl *ctl_dev, kf_stream::Board *board,
+                                 int deadline_ms)
 {
-    if (!g || (!dev_dst && len > 0) || !ctl || !ctl_dev) return KF_ERR_ARG;
+    if (!g || (!dev_dst && len > 0) || !ctl || !ctl_dev || !board) return KF_ERR_ARG;
     return streamed(g, fd, len, stream, ctl, piece, [&](void *landing) {
-        return kf_stream::launch_copy_in(landing, dev_dst, len, piece, ctl_dev, deadline_ms,
+        return kf_stream::launch_copy_in(landing, dev_dst, len, piece, ctl_dev, board, deadline_ms,
                                          stream);
     });
 }

@@ -354,17 +354,30 @@ int read_exact(int fd, void *buf, size_t n)
     while (n > 0) {
         ssize_t r = ::read(fd, p, n);
         if (r < 0 && errno == EINTR) continue;
-        if (r <= 0) return fail(KF_ERR_IO, "read: unexpected end of stream");
+        if (r < 0) return fail(KF_ERR_IO, std::string("read: ") + strerror(errno));
+        if (r == 0) return fail(KF_ERR_IO, "read: unexpected end of stream");
         p += r;
         n -= static_cast<size_t>(r);
     }
     return KF_OK;
 }
 
+// writev without SIGPIPE: a peer that died must fail the write (EPIPE), not
+// kill this process (a C or Go host does not ignore SIGPIPE as Python does)
+inline ssize_t writev_nosig(int fd, struct iovec *iov, int cnt)
+{
+    struct msghdr m {};
+    m.msg_iov    = iov;
+    m.msg_iovlen = static_cast<size_t>(cnt);
+    const ssize_t w = ::sendmsg(fd, &m, MSG_NOSIGNAL);
+    if (w < 0 && errno == ENOTSOCK) return ::writev(fd, iov, cnt);
+    return w;
+}
+
 int write_all(int fd, struct iovec *iov, int cnt)
 {
     while (cnt > 0) {
-        ssize_t w = ::writev(fd, iov, cnt);
+        ssize_t w = writev_nosig(fd, iov, cnt);
         if (w < 0) {
             if (errno == EINTR) continue;
             return fail(KF_ERR_IO, std::string("writev: ") + strerror(errno));
@@ -411,6 +424,29 @@ int write_bytes(int fd, const char *p, size_t n)
 }
 
 struct SessOp;
+
+// KUNGFU_AMD_TEST_LAUNCH_RACE=1 (a regression test's hook, off otherwise):
+// the sender's first copy-out launch and the poll thread's first streamed
+// launch wait here for each other (5 s at most), so both threads launch
+// kf_stream kernels of a fresh session at the same moment: the r04 abort
+// (profiles/r05/failures.md) came from exactly that overlap.
+struct LaunchRace {
+    bool on = false;
+    std::mutex m;
+    std::condition_variable cv;
+    int arrived    = 0;
+    bool used[2]   = {false, false};
+    void meet(int who)
+    {
+        if (!on) return;
+        std::unique_lock<std::mutex> l(m);
+        if (used[who]) return;
+        used[who] = true;
+        ++arrived;
+        cv.notify_all();
+        cv.wait_for(l, std::chrono::seconds(5), [&] { return arrived >= 2; });
+    }
+};
 
 struct SendItem {  // one chunk to every fd in `fds` (the node's successors)
     std::vector<int> fds;
@@ -496,6 +532,8 @@ struct SessChunk {
     hipEvent_t mirror_ev;      // device mode: the last fold went to the mirror (its end)
     std::vector<hipEvent_t> piece_ev;  // ... and each of its pieces' ends (streamed send)
     bool streamed = false;             // the mirror fold marks its pieces in the op's ctl
+    uint8_t sctl_used = 0;  // streamed kernels that ran on its ctl: 1 its reduce fold
+                            // (ctl 0), 2 its bcast copy in (ctl 1); complete() checks err
     std::deque<FoldJob *> folds;  // host mode: received, not yet folded (front: running)
 };
 
@@ -531,6 +569,9 @@ struct SessOp {
     size_t folds = 0;  // host mode: its fold jobs not yet retired by the poll thread
     int rc       = KF_OK;
     std::string err;
+    // KUNGFU_AMD_OP_TIMEOUT_S: the call fails with KF_ERR_TIMEOUT once a
+    // message it waits for has not come by then (0 = no deadline)
+    std::chrono::steady_clock::time_point deadline{};
 };
 
 }  // namespace
@@ -615,6 +656,15 @@ struct kf_session {
     LeasePool stage_pool, mirror_pool;
     bool mirror        = true;
     int device         = 0;        // device mode: the GPU the session was created on
+    kf_stream::Board *board = nullptr;  // device mode: the streamed kernels' device words
+    LaunchRace race;                    // KUNGFU_AMD_TEST_LAUNCH_RACE
+    // KUNGFU_AMD_OP_TIMEOUT_S (0: none): bounds each call's wait for its
+    // messages (the poll) and every socket read and write (SO_RCVTIMEO /
+    // SO_SNDTIMEO), so a peer that stalls fails the call instead of hanging it
+    int op_timeout_ms = 0;
+    // peers whose connection to us reached EOF (the poll loop, under run_mu):
+    // a call that still expects a message from one fails at once
+    std::unordered_set<int> closed;
     char *barrier_dev  = nullptr;  // device mode: the barrier's zeroed u8 workspace
     // KUNGFU_AMD_SESSION_TRACE (see TraceRec)
     std::string trace_path;
@@ -753,6 +803,7 @@ struct kf_session {
         for (auto &l : ctl_pool.idle) (void)hipHostFree(l.p);
         if (!tx_ctl.empty()) (void)hipHostFree(tx_ctl[0]);
         if (barrier_dev) (void)hipFree(barrier_dev);
+        kf_stream::board_destroy(board);  // every kernel on it was synced by complete()
         if (wake_fd >= 0) ::close(wake_fd);
     }
 
@@ -824,6 +875,7 @@ struct kf_session {
         const size_t np = piece ? (it.bytes + piece - 1) / piece : 0;
         const bool stream_out = (stream_mode & kStreamOut) || ((stream_mode & kStreamOutIdle) && idle);
         if (ok && stream_out && it.bytes > 0) {  // one kernel, pieces marked as they land
+            race.meet(0);
             kf_stream::reset(tx_ctl[slot], stream_piece);
             ok = kf_stream::launch_copy_out(it.ptr, tx_dev[slot], static_cast<uint32_t>(it.bytes),
                                             stream_piece, tx_ctl_dev[slot], tx_stream) == KF_OK;
@@ -1566,16 +1618,19 @@ int kf_session::handle(SessOp &o, size_t i, uint32_t flags, int peer, int fd, co
     const bool pieces   = device_mode && !mem && piece && len > piece;
     const bool streamed = device_mode && !mem && o.ctl.p && len > 0;
     if (flags & KF_RCH_WAIT_RECV_BUF) {  // bcast: recvInto RecvBuf
-        if (device_mode) {
-            r = mem ? kf_ingest_copy_host(ingest, mem, len, dst, stream)
-                : streamed && ((stream_mode & kStreamIn) ||
-                               ((stream_mode & kStreamInLast) && o.remaining == 1))
-                    ? kf_ingest_recv_into_streamed(ingest, fd, len, dst, stream,
-                                                          stream_piece, ctl_at(o, i, 1),
-                                                          ctl_at(o, i, 1, true),
-                                                          stream_deadline_ms)
-                : pieces   ? kf_ingest_recv_into_pieces(ingest, fd, len, dst, stream, piece)
-                           : kf_ingest_recv_into(ingest, fd, len, dst, stream);
+        const bool stream_in = streamed && ((stream_mode & kStreamIn) ||
+                                            ((stream_mode & kStreamInLast) && o.remaining == 1));
+        if (device_mode && mem) {
+            r = kf_ingest_copy_host(ingest, mem, len, dst, stream);
+        } else if (device_mode && stream_in) {
+            race.meet(1);
+            c.sctl_used |= 2;
+            r = kf_ingest_recv_into_streamed(ingest, fd, len, dst, stream, stream_piece,
+                                             ctl_at(o, i, 1), ctl_at(o, i, 1, true), board,
+                                             stream_deadline_ms);
+        } else if (device_mode) {
+            r = pieces ? kf_ingest_recv_into_pieces(ingest, fd, len, dst, stream, piece)
+                       : kf_ingest_recv_into(ingest, fd, len, dst, stream);
         } else if (mem) {
             std::memcpy(dst, mem, len);
         } else {
@@ -1624,8 +1679,10 @@ int kf_session::handle(SessOp &o, size_t i, uint32_t flags, int peer, int fd, co
         // call, so its control block is never reset under a running kernel)
         if (streamed && (stream_mode & kStreamFold) && c.pending_reduce == 1 &&
             kf_stream::supported(o.dt, o.op)) {
+            race.meet(1);
+            c.sctl_used |= 1;
             r = kf_ingest_recv_onto_streamed(ingest, fd, len, out, own, o.dt, stream, stream_piece,
-                                             ctl_at(o, i, 0), ctl_at(o, i, 0, true),
+                                             ctl_at(o, i, 0), ctl_at(o, i, 0, true), board,
                                              stream_deadline_ms, to_mirror);
             if (r != KF_OK) return fail(r, kf_ingest_last_error());
             c.streamed = to_mirror;
@@ -1778,6 +1835,20 @@ int kf_session::complete(SessOp &o)
         if (o.mir_side && kf_sync::stream_sync(mir_stream) != KF_OK && rc == KF_OK) {
             rc = fail(KF_ERR_HIP, "mirror stream sync");
         }
+        // a streamed kernel that gave up (its deadline, or the host's abort)
+        // left its chunk without the peer's bytes: the call fails, whatever
+        // the socket reads returned
+        for (size_t i = 0; i < o.chunks.size() && rc == KF_OK && o.ctl.p; ++i) {
+            for (int w = 0; w < 2; ++w) {
+                if ((o.chunks[i].sctl_used & (1 << w)) &&
+                    __atomic_load_n(&ctl_at(o, i, w)->err, __ATOMIC_ACQUIRE) != 0) {
+                    rc = fail(KF_ERR_TIMEOUT, "chunk " + o.chunks[i].name +
+                                                  ": its streamed kernel stopped waiting for the "
+                                                  "body (KUNGFU_AMD_STREAM_TIMEOUT_MS or abort)");
+                    break;
+                }
+            }
+        }
     }
     for (auto &c : o.chunks) {  // a failed collective may leave a mirror event unsent
         std::lock_guard<std::mutex> l(ev_mu);
@@ -1832,9 +1903,46 @@ int kf_session::run(SessOp *one)
             o->remaining = 0;
         }
     };
+    // one call fails alone: its chunks stop being routed (later messages for
+    // them wait in the stash), the others in flight go on
+    auto fail_op = [&](SessOp *o, int rc, const std::string &why) {
+        if (o->rc == KF_OK) {
+            o->rc  = rc;
+            o->err = why;
+        }
+        o->remaining = 0;
+        for (auto &c : o->chunks) {
+            auto f = index.find(c.name);
+            if (f != index.end() && f->second.first == o) index.erase(f);
+        }
+    };
+    // the first chunk of o that still waits for a message from `peer`, or -1
+    auto awaits = [&](const SessOp &o, int peer) -> int {
+        for (size_t i = 0; i < o.chunks.size(); ++i) {
+            const auto &c  = o.chunks[i];
+            const auto &bp = c.st->bcast.prev[rank];
+            if (std::find(c.waiting.begin(), c.waiting.end(), peer) != c.waiting.end() ||
+                (!c.bcast_done && std::find(bp.begin(), bp.end(), peer) != bp.end())) {
+                return static_cast<int>(i);
+            }
+        }
+        return -1;
+    };
+    auto peer_gone = [&](SessOp *o, int peer) {
+        if (o->remaining == 0 || o->rc != KF_OK) return;
+        const int ci = awaits(*o, peer);
+        if (ci < 0) return;
+        fail_op(o, fail(KF_ERR_IO, "peer " + std::to_string(peer) +
+                                       " closed its connection while " + o->chunks[ci].name +
+                                       " still waited for its message"),
+                t_sess_error);
+    };
     auto start = [&](SessOp *o) {
         tr(TR_OP_START, -1, static_cast<int>(o->count), 0);
         t_sess_error.clear();
+        if (op_timeout_ms > 0) {
+            o->deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(op_timeout_ms);
+        }
         o->rc = plan(*o);
         if (o->rc != KF_OK) {
             o->err       = t_sess_error;
@@ -1861,6 +1969,8 @@ int kf_session::run(SessOp *one)
                 return;
             }
         }
+        // a peer that closed before this call started sends it nothing more
+        for (int p : closed) peer_gone(o, p);
     };
     if (one) start(one);
 
@@ -2034,7 +2144,28 @@ int kf_session::run(SessOp *one)
             fail_all(fail(KF_ERR_IO, "every peer connection closed before the all-reduce finished"));
             continue;
         }
-        if (::poll(pfds.data(), pfds.size(), -1) < 0) {
+        // KUNGFU_AMD_OP_TIMEOUT_S: a call past its deadline fails; the poll
+        // sleeps no longer than the nearest one
+        int poll_ms = -1;
+        if (op_timeout_ms > 0) {
+            const auto now = std::chrono::steady_clock::now();
+            bool expired   = false;
+            for (SessOp *o : active) {
+                if (o->remaining == 0) continue;
+                if (o->deadline <= now) {
+                    fail_op(o, fail(KF_ERR_TIMEOUT, o->name + ": no message for " +
+                                                        std::to_string(op_timeout_ms) +
+                                                        " ms (KUNGFU_AMD_OP_TIMEOUT_S)"),
+                            t_sess_error);
+                    expired = true;
+                    continue;
+                }
+                const auto left = std::chrono::duration_cast<std::chrono::milliseconds>(o->deadline - now).count() + 1;
+                if (poll_ms < 0 || left < poll_ms) poll_ms = static_cast<int>(left);
+            }
+            if (expired) continue;
+        }
+        if (::poll(pfds.data(), pfds.size(), poll_ms) < 0) {
             if (errno == EINTR) continue;
             fail_all(fail(KF_ERR_IO, std::string("poll: ") + strerror(errno)));
             continue;
@@ -2052,10 +2183,14 @@ int kf_session::run(SessOp *one)
             }
             char probe;
             if (::recv(fd, &probe, 1, MSG_PEEK | MSG_DONTWAIT) == 0) {
-                // clean EOF at a message boundary: that peer is done with us
-                // (a finished peer closes connections we may not need); stop
-                // polling it
+                // clean EOF at a message boundary: that peer sends us nothing
+                // more. A finished peer closes connections we may not need, so
+                // only the calls still waiting for one of its messages fail
+                // (every one of them, naming the peer; at np >= 3 the other
+                // connections stay open and would keep them waiting)
                 pfds[q].fd = -1;
+                closed.insert(pfd_peer[q]);
+                for (SessOp *o : active) peer_gone(o, pfd_peer[q]);
                 continue;
             }
             rc = kf_rch_recv_header(fd, hname, sizeof(hname), nullptr, &flags);
@@ -2150,8 +2285,22 @@ kf_session_t *create_session(int rank, std::vector<PeerAddr> peers, const char *
         delete s;
         return nullptr;
     }
+    if (const char *e = std::getenv("KUNGFU_AMD_OP_TIMEOUT_S")) {
+        char *end      = nullptr;
+        const long sec = std::strtol(e, &end, 10);
+        if (end == e || *end != '\0' || sec < 0) {
+            t_sess_error = std::string("bad KUNGFU_AMD_OP_TIMEOUT_S ") + e + " (want seconds >= 0)";
+            delete s;
+            return nullptr;
+        }
+        s->op_timeout_ms = static_cast<int>(std::min<long long>(sec, 86400LL * 24) * 1000LL);
+    }
+    if (const char *e = std::getenv("KUNGFU_AMD_TEST_LAUNCH_RACE")) s->race.on = std::atoi(e) != 0;
     if (s->device_mode) {
         (void)hipGetDevice(&s->device);
+        // the streamed kernels' words and code, on this thread, before the
+        // sender / async / fold threads exist (profiles/r05/failures.md)
+        s->board  = kf_stream::board_create();
         s->ingest = kf_ingest_create(kChunk + 4096, 8);
         int nslot = 4;
         if (const char *e = std::getenv("KUNGFU_AMD_TX_SLOTS")) nslot = std::max(1, std::atoi(e));
@@ -2224,8 +2373,9 @@ kf_session_t *create_session(int rank, std::vector<PeerAddr> peers, const char *
                 if (tx_ok) s->tx_piece_ev.push_back(e);
             }
         }
-        if (!s->ingest || !tx_ok || !s->tx_stream) {
-            t_sess_error = "kf_ingest_create failed";
+        if (!s->ingest || !tx_ok || !s->tx_stream || !s->board) {
+            t_sess_error = !s->board ? "streamed kernels' device words (hipMalloc) failed"
+                                     : "kf_ingest_create failed";
             delete s;
             return nullptr;
         }
@@ -2233,6 +2383,13 @@ kf_session_t *create_session(int rank, std::vector<PeerAddr> peers, const char *
     if (s->size > 1 && s->connect_all() != KF_OK) {
         delete s;
         return nullptr;
+    }
+    if (s->op_timeout_ms > 0) {  // a peer that stalls mid-message fails the read / write
+        timeval tv{};
+        tv.tv_sec  = s->op_timeout_ms / 1000;
+        tv.tv_usec = (s->op_timeout_ms % 1000) * 1000;
+        for (auto &kv : s->in_fd) (void)::setsockopt(kv.second, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+        for (auto &kv : s->out_fd) (void)::setsockopt(kv.second, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof(tv));
     }
     s->sender = std::thread([s] {
         if (s->device_mode) (void)hipSetDevice(s->device);  // its copy-out kernels

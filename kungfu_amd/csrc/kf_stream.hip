@@ -10,7 +10,7 @@
 // loads, served by the L2s: no PCIe reads) and then fold (SUM, the dtype's
 // own arithmetic: kf_reduce_kernels.hpp Elt<T>) or copy their bytes, reading
 // the landing slot system-coherent (sc0 sc1 buffer loads: from memory, past
-// every GPU cache) and writing a page-locked output through the L2 (sc1), so
+// every GPU cache) and writing a page-locked output through the L2 (sc0 sc1), so
 // no block takes an L2-wide fence. A block whose output a sender reads
 // (`mark`) drains its stores (every wave's vmcnt(0), the barrier) and its
 // first lane stores the block's done flag: one word per block, no atomics on
@@ -32,7 +32,11 @@
 #include "kf_stream.hpp"
 
 #ifndef KF_STREAM_HOST_STORE_AUX
-#define KF_STREAM_HOST_STORE_AUX 16  // sc1: written through the L2
+// sc0 sc1: system scope, the policy the memory model gives for stores another
+// agent (the host) reads without a release fence. r04 shipped sc1 alone
+// (agent scope), which wrote through on the boxes measured but is not what
+// the model promises; the flag after vmcnt(0) relies on it.
+#define KF_STREAM_HOST_STORE_AUX 17
 #endif
 
 namespace kf_stream
@@ -40,11 +44,8 @@ namespace kf_stream
 namespace
 {
 constexpr int kLanes = 256;
-constexpr uint32_t kSeen = 4096;     // device words for the watchers' counts
+constexpr uint32_t kSeen = 4096;     // device words for the watchers' counts (per board)
 constexpr uint32_t kGaveUp = 1u << 31;  // in a count: the watcher stopped waiting
-
-__device__ unsigned long long g_seen[kSeen];
-std::atomic<unsigned long long> g_launches{0};
 
 __device__ __forceinline__ unsigned long long seen_word(uint32_t epoch, uint32_t v)
 {
@@ -114,7 +115,7 @@ __device__ __forceinline__ bool block_wait(Ctl *c, uint32_t len, uint32_t need,
 // Page-locked bytes move with an explicit cache policy instead of fences:
 // the landing slot is read system-coherent (sc0 sc1: from memory, past every
 // GPU cache, so no acquire fence per block), and a page-locked output is
-// written through (kHostStore) so that once the block's stores have drained
+// written through at system scope (kHostStore) so that once the block's stores have drained
 // (vmcnt(0)) they are in host memory and one flag store publishes them — no
 // L2 writeback per block. Per-block system fences cost a write-back and an
 // invalidate of the whole XCD L2 each: 257 of them per chunk held every
@@ -226,7 +227,7 @@ __global__ void __launch_bounds__(kLanes)
             store16(o + off, nb, buf);
         }
     }
-    if (mark) block_done(c, b);
+    if (mark && ok) block_done(c, b);  // a block that gave up is never final
 }
 
 // dst (HBM) = landed body, as each 4 KiB lands
@@ -298,39 +299,37 @@ struct Seen {
     unsigned long long *word;
     uint32_t epoch;
 };
+}  // namespace
 
-// g_seen has one instance per device: its address on the current one
-unsigned long long *seen_base()
-{
-    constexpr int kMaxDevices = 64;
-    static std::atomic<unsigned long long *> base[kMaxDevices] = {};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return nullptr;
-    unsigned long long *b = base[dev].load(std::memory_order_acquire);
-    if (!b) {
-        void *p = nullptr;
-        if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_seen)) != hipSuccess) return nullptr;
-        b = static_cast<unsigned long long *>(p);
-        base[dev].store(b, std::memory_order_release);
-    }
-    return b;
-}
+// The watchers' words live in HBM the session allocated (hipMalloc) on the
+// thread that created it, before its other threads start: no module-scope
+// __device__ variable, so nothing is resolved lazily under a second thread's
+// launch (r04: a first-use hipGetSymbolAddress of one aborted a rank in the
+// HIP runtime, profiles/r05/failures.md).
+struct Board {
+    unsigned long long *words = nullptr;
+    int device                = 0;
+    std::atomic<unsigned long long> launches{0};
+};
 
-Seen next_seen()
+namespace
 {
-    unsigned long long *base   = seen_base();
-    const unsigned long long n = g_launches.fetch_add(1, std::memory_order_relaxed);
+Seen next_seen(Board *b)
+{
+    if (!b || !b->words) return Seen{nullptr, 0};
+    const unsigned long long n = b->launches.fetch_add(1, std::memory_order_relaxed);
     // a word is reused kSeen launches later; the epoch tells its owners apart
-    return Seen{base ? base + n % kSeen : nullptr, static_cast<uint32_t>(n + 1)};
+    // (epoch 0 is the zeroed word's: never a launch's)
+    return Seen{b->words + n % kSeen, static_cast<uint32_t>(n % 0xffffffffu) + 1};
 }
 
 template <typename T>
 int fold_as(const void *own, const void *landing, void *out, uint32_t len, int mark, Ctl *c,
-            unsigned long long limit, hipStream_t s)
+            Board *board, unsigned long long limit, hipStream_t s)
 {
     using S = typename kf::Elt<T>::S;
     if (len % sizeof(S)) return KF_ERR_ARG;
-    const Seen w = next_seen();
+    const Seen w = next_seen(board);
     if (!w.word) return KF_ERR_HIP;
     fold_kernel<T><<<blocks(len) + 1, kLanes, 0, s>>>(
         static_cast<const S *>(own), static_cast<const char *>(landing), static_cast<S *>(out), len,
@@ -367,7 +366,8 @@ void publish(Ctl *c, uint32_t bytes) { __atomic_store_n(&c->landed, bytes, __ATO
 void abort_wait(Ctl *c) { __atomic_store_n(&c->abort, 1u, __ATOMIC_RELEASE); }
 
 int launch_fold(KungFu_Datatype dt, const void *own, const void *landing_dev, void *out,
-                uint32_t len, uint32_t piece, Ctl *c_dev, int deadline_ms, bool mark, void *stream)
+                uint32_t len, uint32_t piece, Ctl *c_dev, Board *board, int deadline_ms, bool mark,
+                void *stream)
 {
     if (len == 0) return KF_OK;
     if (!fits(len, piece)) return KF_ERR_ARG;
@@ -375,28 +375,28 @@ int launch_fold(KungFu_Datatype dt, const void *own, const void *landing_dev, vo
     hipStream_t s                = static_cast<hipStream_t>(stream);
     const int m                  = mark ? 1 : 0;
     switch (dt) {
-    case KungFu_UINT8: return fold_as<uint8_t>(own, landing_dev, out, len, m, c_dev, lim, s);
-    case KungFu_UINT16: return fold_as<uint16_t>(own, landing_dev, out, len, m, c_dev, lim, s);
-    case KungFu_UINT32: return fold_as<uint32_t>(own, landing_dev, out, len, m, c_dev, lim, s);
-    case KungFu_UINT64: return fold_as<uint64_t>(own, landing_dev, out, len, m, c_dev, lim, s);
-    case KungFu_INT8: return fold_as<int8_t>(own, landing_dev, out, len, m, c_dev, lim, s);
-    case KungFu_INT16: return fold_as<int16_t>(own, landing_dev, out, len, m, c_dev, lim, s);
-    case KungFu_INT32: return fold_as<int32_t>(own, landing_dev, out, len, m, c_dev, lim, s);
-    case KungFu_INT64: return fold_as<int64_t>(own, landing_dev, out, len, m, c_dev, lim, s);
-    case KungFu_FLOAT16: return fold_as<kf::f16_t>(own, landing_dev, out, len, m, c_dev, lim, s);
-    case KungFu_FLOAT: return fold_as<float>(own, landing_dev, out, len, m, c_dev, lim, s);
-    case KungFu_DOUBLE: return fold_as<double>(own, landing_dev, out, len, m, c_dev, lim, s);
-    case KungFu_BFLOAT16: return fold_as<kf::bf16_t>(own, landing_dev, out, len, m, c_dev, lim, s);
+    case KungFu_UINT8: return fold_as<uint8_t>(own, landing_dev, out, len, m, c_dev, board, lim, s);
+    case KungFu_UINT16: return fold_as<uint16_t>(own, landing_dev, out, len, m, c_dev, board, lim, s);
+    case KungFu_UINT32: return fold_as<uint32_t>(own, landing_dev, out, len, m, c_dev, board, lim, s);
+    case KungFu_UINT64: return fold_as<uint64_t>(own, landing_dev, out, len, m, c_dev, board, lim, s);
+    case KungFu_INT8: return fold_as<int8_t>(own, landing_dev, out, len, m, c_dev, board, lim, s);
+    case KungFu_INT16: return fold_as<int16_t>(own, landing_dev, out, len, m, c_dev, board, lim, s);
+    case KungFu_INT32: return fold_as<int32_t>(own, landing_dev, out, len, m, c_dev, board, lim, s);
+    case KungFu_INT64: return fold_as<int64_t>(own, landing_dev, out, len, m, c_dev, board, lim, s);
+    case KungFu_FLOAT16: return fold_as<kf::f16_t>(own, landing_dev, out, len, m, c_dev, board, lim, s);
+    case KungFu_FLOAT: return fold_as<float>(own, landing_dev, out, len, m, c_dev, board, lim, s);
+    case KungFu_DOUBLE: return fold_as<double>(own, landing_dev, out, len, m, c_dev, board, lim, s);
+    case KungFu_BFLOAT16: return fold_as<kf::bf16_t>(own, landing_dev, out, len, m, c_dev, board, lim, s);
     default: return KF_ERR_DTYPE;
     }
 }
 
 int launch_copy_in(const void *landing_dev, void *dst, uint32_t len, uint32_t piece, Ctl *c_dev,
-                   int deadline_ms, void *stream)
+                   Board *board, int deadline_ms, void *stream)
 {
     if (len == 0) return KF_OK;
     if (!fits(len, piece)) return KF_ERR_ARG;
-    const Seen w = next_seen();
+    const Seen w = next_seen(board);
     if (!w.word) return KF_ERR_HIP;
     copy_in_kernel<<<blocks(len) + 1, kLanes, 0, static_cast<hipStream_t>(stream)>>>(
         static_cast<const char *>(landing_dev), static_cast<char *>(dst), len, c_dev, w.word,
@@ -412,6 +412,55 @@ int launch_copy_out(const void *src, void *host_dev, uint32_t len, uint32_t piec
     copy_out_kernel<<<blocks(len), kLanes, 0, static_cast<hipStream_t>(stream)>>>(
         static_cast<const char *>(src), static_cast<char *>(host_dev), len, c_dev);
     return hipGetLastError() == hipSuccess ? KF_OK : KF_ERR_HIP;
+}
+
+namespace
+{
+// Every kernel of this file resolved on the calling thread (its code object
+// loaded for the current device), so the session's threads only launch.
+template <typename T>
+bool warm_fold()
+{
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&fold_kernel<T>)) == hipSuccess;
+}
+}  // namespace
+
+Board *board_create()
+{
+    auto *b = new Board;
+    hipFuncAttributes a;
+    const bool warm =
+        warm_fold<uint8_t>() && warm_fold<uint16_t>() && warm_fold<uint32_t>() &&
+        warm_fold<uint64_t>() && warm_fold<int8_t>() && warm_fold<int16_t>() &&
+        warm_fold<int32_t>() && warm_fold<int64_t>() && warm_fold<kf::f16_t>() &&
+        warm_fold<float>() && warm_fold<double>() && warm_fold<kf::bf16_t>() &&
+        hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&copy_in_kernel)) == hipSuccess &&
+        hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&copy_out_kernel)) == hipSuccess &&
+        hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&copy_kernel)) == hipSuccess;
+    // zeroed on a stream of its own: the null stream (torch's default) may
+    // hold another session's streamed kernel that waits for bytes this
+    // thread has yet to send (sessions created in threads of one process)
+    const size_t bytes = kSeen * sizeof(unsigned long long);
+    hipStream_t st     = nullptr;
+    const bool ok = warm && hipGetDevice(&b->device) == hipSuccess &&
+                    hipMalloc(reinterpret_cast<void **>(&b->words), bytes) == hipSuccess &&
+                    hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess &&
+                    hipMemsetAsync(b->words, 0, bytes, st) == hipSuccess &&
+                    hipStreamSynchronize(st) == hipSuccess;
+    if (st) (void)hipStreamDestroy(st);
+    if (!ok) {
+        board_destroy(b);
+        return nullptr;
+    }
+    return b;
+}
+
+void board_destroy(Board *b)
+{
+    if (!b) return;
+    if (b->words) (void)hipFree(b->words);
+    delete b;
 }
 
 bool copy_kernels()
@@ -452,8 +501,9 @@ int wait_piece(const Ctl *c, uint32_t k, uint32_t len, int timeout_ms)
     const auto t0     = std::chrono::steady_clock::now();
     for (uint32_t spin = 0;; ++spin) {
         if (piece_done(c, k, nb)) return KF_OK;
+        // a block that gave up never flags its piece: the word says so at once
+        if (__atomic_load_n(&c->err, __ATOMIC_ACQUIRE)) return KF_ERR_HIP;
         if ((spin & 1023) == 1023) {
-            if (__atomic_load_n(&c->err, __ATOMIC_RELAXED)) return KF_ERR_HIP;
             if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeout_ms)) {
                 return KF_ERR_TIMEOUT;
             }

@@ -43,10 +43,20 @@ constexpr uint32_t kMaxBlocks  = 272;   // blocks of one chunk (1 MiB + 64 KiB)
 struct Ctl {
     uint32_t landed;  // host: body bytes in the landing buffer (release store)
     uint32_t abort;   // host: the rest of the body will not come
-    uint32_t err;     // device: a block stopped waiting (deadline or abort)
+    uint32_t err;     // device: a block stopped waiting (deadline or abort); the
+                      // host fails the collective on it (kf_session complete())
     uint32_t bpp;     // blocks per piece (the sender's unit)
     uint32_t done[kMaxBlocks];  // device: block b's output is in host memory
 };
+
+// The device words the streamed kernels' watchers publish through (HBM, one
+// board per session). board_create() runs on the thread that creates the
+// session, before its sender / worker threads start: it allocates the words
+// and resolves every kernel of kf_stream.hip for the current device there, so
+// no HIP module state is initialised lazily under a concurrent launch.
+struct Board;
+Board *board_create();  // nullptr on a HIP failure
+void board_destroy(Board *b);
 
 // SUM in any dtype (the S-SGD / SMA sum); other ops take the whole-chunk path
 bool supported(KungFu_Datatype dt, KungFu_Op op);
@@ -62,10 +72,10 @@ void abort_wait(Ctl *c);
 // mark: the fold's output is page-locked memory a sender reads piece by piece
 // (each block flags its 4 KiB done); otherwise it is HBM and nothing is flagged.
 int launch_fold(KungFu_Datatype dt, const void *own, const void *landing_dev, void *out,
-                uint32_t len, uint32_t piece, Ctl *c_dev, int deadline_ms, bool mark,
-                void *stream);
+                uint32_t len, uint32_t piece, Ctl *c_dev, Board *board, int deadline_ms,
+                bool mark, void *stream);
 int launch_copy_in(const void *landing_dev, void *dst, uint32_t len, uint32_t piece, Ctl *c_dev,
-                   int deadline_ms, void *stream);
+                   Board *board, int deadline_ms, void *stream);
 int launch_copy_out(const void *src, void *host_dev, uint32_t len, uint32_t piece, Ctl *c_dev,
                     void *stream);
 
@@ -79,7 +89,8 @@ int launch_copy(void *dst, const void *src, size_t len, void *stream);
 
 // Host side of the sender, for a chunk of len bytes: wait until piece k is
 // final (KF_OK), the device gave up (KF_ERR_HIP) or timeout_ms passed
-// (KF_ERR_TIMEOUT); how many pieces from k on are final already.
+// (KF_ERR_TIMEOUT); how many pieces from k on are final already. A block
+// that gave up (deadline, abort) sets err and never flags itself done.
 int wait_piece(const Ctl *c, uint32_t k, uint32_t len, int timeout_ms);
 uint32_t ready_run(const Ctl *c, uint32_t k, uint32_t len);
 }  // namespace kf_stream
@@ -101,7 +112,8 @@ int stream_sync(void *stream);   // KF_OK or KF_ERR_HIP
 int kf_ingest_recv_onto_streamed(kf_ingest_t *g, int fd, uint32_t len, void *dev_acc,
                                  const void *dev_own, KungFu_Datatype dt, void *stream,
                                  uint32_t piece, kf_stream::Ctl *ctl, kf_stream::Ctl *ctl_dev,
-                                 int deadline_ms, bool mark);
+                                 kf_stream::Board *board, int deadline_ms, bool mark);
 int kf_ingest_recv_into_streamed(kf_ingest_t *g, int fd, uint32_t len, void *dev_dst,
                                  void *stream, uint32_t piece, kf_stream::Ctl *ctl,
-                                 kf_stream::Ctl *ctl_dev, int deadline_ms);
+                                 kf_stream::Ctl *ctl_dev, kf_stream::Board *board,
+                                 int deadline_ms);

@@ -196,11 +196,21 @@ void init_exchange(py::bytes uid, int rank, int size, int device)
         (void)kf_exchange_wait_named(g_ex);
         kf_exchange_destroy(g_ex);
     }
-    // a rank that never joins costs KUNGFU_AMD_INIT_TIMEOUT_S (default 300 s),
-    // then every rank learns it in ops.bring_up's agreement and takes the
-    // torch.distributed path
+    // a rank that never joins costs KUNGFU_AMD_INIT_TIMEOUT_S (default 300 s,
+    // whole seconds in [1, 86400]), then every rank learns it in
+    // ops.bring_up's agreement and takes the torch.distributed path. A timed-out
+    // init leaves its thread blocked in ncclCommInitRank until the process
+    // exits (RCCL has no way to cancel it).
     int timeout_ms = 300 * 1000;
-    if (const char *e = std::getenv("KUNGFU_AMD_INIT_TIMEOUT_S")) timeout_ms = 1000 * std::atoi(e);
+    if (const char *e = std::getenv("KUNGFU_AMD_INIT_TIMEOUT_S")) {
+        char *end      = nullptr;
+        const long sec = std::strtol(e, &end, 10);
+        if (end == e || *end != '\0' || sec <= 0 || sec > 86400) {
+            throw std::runtime_error(std::string("kungfu_amd: KUNGFU_AMD_INIT_TIMEOUT_S must be "
+                                                 "whole seconds in [1, 86400], got '") + e + "'");
+        }
+        timeout_ms = static_cast<int>(static_cast<long long>(sec) * 1000LL);
+    }
     {
         py::gil_scoped_release nogil;
         g_ex = kf_exchange_create_timeout(id.data(), rank, size, device, timeout_ms);

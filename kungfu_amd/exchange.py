@@ -107,6 +107,15 @@ class NativeExchange:
         self._h, self._side, self._sums = h, None, {}
         return self
 
+    def transport_info(self):
+        """(communicator rank count, RCCL version) as the transport reports
+        them (kf_exchange_transport_info: ncclCommCount, ncclGetVersion);
+        (-1, 0) over a host's own transport."""
+        c, v = ctypes.c_int(), ctypes.c_int()
+        _lib.check(self.lib.kf_exchange_transport_info(self._h, ctypes.byref(c), ctypes.byref(v)),
+                   "kf_exchange_transport_info")
+        return c.value, v.value
+
     def split(self, color, key=None):
         """kf_exchange_split (gpu_collective::new_local / new_group,
         gpu_collective.cpp:202-243): the ranks passing the same color form a

@@ -43,3 +43,30 @@ def test_self_launch_starts_n_ranks_and_relays_status():
     assert r.returncode != 0
     assert "the 2 ranks ended with status" in r.stderr, r.stderr[-3000:]
     assert "(local_rank: 0)" in r.stderr and "(local_rank: 1)" in r.stderr, r.stderr[-3000:]
+
+
+class _FakeNative:
+    def __init__(self, count, ver):
+        self.count, self.ver = count, ver
+
+    def transport_info(self):
+        return self.count, self.ver
+
+
+def test_rccl_report_fails_loudly_on_a_short_communicator():
+    """the N > 1 line names the exchange that ran and what
+    RCCL reports (ncclCommCount, ncclGetVersion). A communicator that does not
+    hold N ranks (each rank timing a world of its own) must end the run with
+    an error, never print a number."""
+    import bench
+    with pytest.raises(SystemExit) as e:
+        bench._rccl_report(_FakeNative(1, 22703), 8, None)
+    assert "holds 1 ranks, not WORLD_SIZE 8" in str(e.value)
+    rep = bench._rccl_report(_FakeNative(8, 22703), 8, None)
+    assert rep == {"exchange_kind": "native C-ABI (kf_exchange)", "rccl_world": 8,
+                   "rccl_version": "2.27.3", "rccl_version_code": 22703}
+    # a host-provided transport is not RCCL: nothing to check
+    assert bench._rccl_report(_FakeNative(-1, 0), 2, None)["rccl_world"] is None
+    # the torch.distributed fallback says why
+    rep = bench._rccl_report(None, 2, "not tried: ranks share a GPU (rehearsal)")
+    assert rep["exchange_kind"] == "torch.distributed" and "share a GPU" in rep["why_not_native"]

@@ -62,6 +62,10 @@ def test_bench_gpus2_starts_its_own_ranks():
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and "collective" in d and d["value"] > 0, d
+    # which exchange ran and what RCCL says about it (same-GPU gloo: no RCCL)
+    c = d["collective"]
+    assert c["exchange_kind"] == "torch.distributed" and c["rccl_world"] is None, c
+    assert "share a GPU" in c["why_not_native"], c
     # the per-phase split of the timed step (RS / epilogue / AG)
     ph = d["collective"]["phase_us"]
     total = sum(v for k, v in ph.items() if k in ("reduce_scatter", "epilogue", "all_gather"))
@@ -166,3 +170,38 @@ def test_bench_exchange_branch_single_rank_rccl():
     assert abs(d["value_aggregate"] - d["n_gpus"] * d["value"]) < 1e-2
     for k in extras.split(","):
         assert "error" not in d[k] and d[k]["ms_per_step"] > 0, (k, d[k])
+    # the N > 1 line explains itself: the exchange kind, and the phase split of
+    # C4 and C5 as well as C3's
+    assert d["collective"]["exchange_kind"].startswith("native"), d["collective"]
+    assert "rccl_world" in d["collective"] and "rccl_version" in d["collective"]
+    for k in ("c4", "c5"):
+        ph = d[k]["phase_us"]
+        assert ph and ph["step_us"] > 0 and ph["sum"] > 0, (k, ph)
+
+
+def test_rccl_report_on_real_rccl_world1():
+    """kf_exchange_transport_info on a real one-rank RCCL communicator: the
+    count is 1 and the version decodes (major.minor.patch)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    code = r"""
+import sys
+sys.path[:0] = [%r]
+import torch
+import bench
+from kungfu_amd.exchange import NativeExchange
+ex = NativeExchange(algo="rs", device=torch.device("cuda:0"), uid=NativeExchange.shared_id())
+print("REPORT", bench._rccl_report(ex, 1, None))
+ex.close()
+""" % ROOT
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120,
+                       cwd=ROOT, env=env)
+    line = [l for l in r.stdout.splitlines() if l.startswith("REPORT")]
+    assert r.returncode == 0 and line, r.stdout[-2000:] + r.stderr[-3000:]
+    rep = eval(line[0][len("REPORT "):])
+    assert rep["rccl_world"] == 1 and rep["exchange_kind"].startswith("native"), rep
+    major = int(rep["rccl_version"].split(".")[0])
+    assert major >= 2, rep

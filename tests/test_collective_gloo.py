@@ -13,6 +13,7 @@ import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
+from procs import hung_msg, join_all
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
@@ -52,13 +53,12 @@ def run_world(fn_name, world, use_gpu=False):
              for r in range(world)]
     for p in procs:
         p.start()
-    for p in procs:
-        p.join(timeout=600)
+    hung = join_all(procs, 600)
     errs = []
     while not errq.empty():
         errs.append(errq.get())
     assert not errs, "\n".join(errs)
-    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert not hung and all(p.exitcode == 0 for p in procs), hung_msg(hung, [p.exitcode for p in procs])
 
 
 def _epilogue(use_gpu):

@@ -26,6 +26,7 @@ import numpy as np
 import pytest
 import torch
 import torch.multiprocessing as mp
+from procs import hung_msg, join_all
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
@@ -49,13 +50,12 @@ def _run(target, world, *args):
     ps = [ctx.Process(target=target, args=(r, world, port, errq) + args) for r in range(world)]
     for p in ps:
         p.start()
-    for p in ps:
-        p.join(timeout=600)
+    hung = join_all(ps, 600)
     errs = []
     while not errq.empty():
         errs.append(errq.get())
     assert not errs, "\n".join(errs)
-    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+    assert not hung and all(p.exitcode == 0 for p in ps), hung_msg(hung, [p.exitcode for p in ps])
 
 
 def _init(rank, world, port):

@@ -18,6 +18,7 @@ import traceback
 
 import numpy as np
 import pytest
+from procs import hung_msg, join_all
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
@@ -48,8 +49,7 @@ def test_share_id_over_session(world):
         ps = [ctx.Process(target=_share_body, args=(r, world, d, errq)) for r in range(world)]
         for p in ps:
             p.start()
-        for p in ps:
-            p.join(timeout=120)
+        hung = join_all(ps, 120)
     errs = []
     while not errq.empty():
         errs.append(errq.get())
@@ -336,6 +336,69 @@ def test_rs_avg_folds_the_division_into_the_collective(world, groups):
         assert np.array_equal(_to_np(bi, "i32"), oracle.reduce_k(xi, "i32", "sum"))
 
     _loop_ranks(world, body)
+
+
+def _special_inputs(world, q, seed):
+    """Per-rank fp32 shards whose rank-order sum then /np and whose
+    premultiplied sum (ncclAvg's PreMulSum for floating types) can part: a
+    normal block, pairs near FLT_MAX whose sum overflows, subnormals (x/np
+    loses bits), NaN and +-inf lanes."""
+    rng = np.random.default_rng(seed)
+    big = np.float32(3.0e38)
+    ins = []
+    for r in range(world):
+        x = rng.standard_normal(world * q).astype(np.float32)
+        x[0:64] = big * (1 + np.float32(0.01) * np.float32(r))           # overflow on the sum
+        # subnormals with odd mantissas: x / np is inexact in every one
+        x[64:128] = (rng.integers(0, 1 << 20, 64) * 2 + 1).astype(np.uint32).view(np.float32)
+        x[128:136] = np.float32("nan") if r == world - 1 else np.float32(1.0)
+        x[136:144] = np.float32("inf") if r == 0 else np.float32(-1.0)
+        ins.append(x)
+    return ins
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_rs_avg_special_values_decide_the_default(world):
+    """may KF_ALGO_REDUCE_SCATTER_AVG (the /np inside the
+    reduce-scatter as ncclAvg, which RCCL runs for floats as a premultiply by
+    1/np before the sum) replace the shard /np epilogue at power-of-two
+    worlds? Only if its bits equal sum-then-/np (oracle.reduce_avg,
+    sync_sgd.py:103-104) on every input. On normal values they do (x * 2^-k is
+    exact, every partial sum scales by the same power of two). They do NOT on
+    sums that overflow (inf in the reference, finite premultiplied) nor on
+    subnormals (x / np drops bits before the sum). NaN and inf lanes agree. So
+    the default stays "rs" (sum, then the exact /np epilogue), and rs_avg stays
+    an opt-in whose difference this test pins."""
+    import torch
+    from oracle import oracle
+    dev = _gpu()
+    q = 4096
+    ins = _special_inputs(world, q, 11 + world)
+    want = oracle.reduce_avg(ins, "f32", world)
+    got = {}
+
+    def body(rank, ex):
+        for algo in ("rs", "rs_avg"):
+            ex.algo = algo
+            b = _to_dev(ins[rank], "f32", dev)
+            ex.all_reduce_([b], average=True, coalesce=False)
+            torch.cuda.synchronize()
+            if rank == 0:
+                got[algo] = _to_np(b, "f32")
+
+    _loop_ranks(world, body)
+    same = lambda a, b: (a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))  # noqa: E731
+    # the default: bit-exact everywhere, specials included
+    assert same(got["rs"], want).all()
+    eq = same(got["rs_avg"], want)
+    normal = np.ones(world * q, bool)
+    normal[:144] = False
+    assert eq[normal].all()                      # normal range: identical bits
+    assert eq[128:144].all()                     # NaN / inf lanes agree
+    assert not eq[0:64].any()                    # overflow: reference inf, premultiplied finite
+    assert np.isinf(want[0:64]).all() and np.isfinite(got["rs_avg"][0:64]).all()
+    assert not eq[64:128].all()                  # subnormals: bits dropped by the premultiply
 
 
 @pytest.mark.gpu

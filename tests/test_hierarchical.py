@@ -18,6 +18,7 @@ import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
+from procs import hung_msg, join_all
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
@@ -127,13 +128,12 @@ def _run(hosts_sizes, use_gpu=False, first=None):
               for r in range(sum(hosts_sizes))]
         for p in ps:
             p.start()
-        for p in ps:
-            p.join(timeout=300)
+        hung = join_all(ps, 300)
     errs = []
     while not errq.empty():
         errs.append(errq.get())
     assert not errs, "\n".join(errs)
-    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+    assert not hung and all(p.exitcode == 0 for p in ps), hung_msg(hung, [p.exitcode for p in ps])
 
 
 def test_host_layout_matches_partition_by_host():
