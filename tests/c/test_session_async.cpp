@@ -10,9 +10,15 @@
 // tools/sanitize_session.sh against ThreadSanitizer / AddressSanitizer builds
 // of the same sources (host code only; host mode makes no HIP call).
 //
-//   test_session_async <np> <steps> <sock_dir>
+// "dead" as a fourth argument: the last rank destroys its session once every
+// rank's session is up (its connections close: EOF at every peer) and the
+// others' async all-reduces must FAIL within 30 s, not hang (kf_session.hip's
+// poll loop fails every call still waiting for a message from a closed peer).
+//
+//   test_session_async <np> <steps> <sock_dir> [dead]
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -126,6 +132,48 @@ void rank_main(int rank, int np, int steps, const char *dir)
     }
     kf_session_destroy(s);
 }
+std::atomic<int> g_created{0};
+
+void dead_main(int rank, int np, const char *dir)
+{
+    kf_session_t *s = kf_session_create(rank, np, dir, 0, 0);
+    if (!s) {
+        std::fprintf(stderr, "rank %d: kf_session_create: %s\n", rank, kf_session_last_error());
+        g_failures.fetch_add(1);
+        g_created.fetch_add(1);
+        return;
+    }
+    kf_session_set_host_reduce(s, fold_i32);
+    g_created.fetch_add(1);
+    while (g_created.load() < np) std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    if (rank == np - 1) {  // gone before its first chunk
+        kf_session_destroy(s);
+        return;
+    }
+    std::vector<std::vector<int32_t>> bufs(kNames);
+    Done done;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int j = 0; j < kNames; ++j) {
+        bufs[j].assign(kCounts[j], rank + 1);
+        const std::string name = "d" + std::to_string(j);
+        if (kf_session_all_reduce_async(s, bufs[j].data(), bufs[j].data(), kCounts[j], KungFu_INT32,
+                                        KungFu_SUM, name.c_str(), nullptr, on_done,
+                                        &done) != KF_OK) {
+            g_failures.fetch_add(1);
+        }
+    }
+    const int rc  = kf_session_wait_all(s);
+    const double dt =
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (rc == KF_OK || done.bad.load() == 0) {
+        std::fprintf(stderr, "rank %d: all-reduces succeeded with rank %d gone\n", rank, np - 1);
+        g_failures.fetch_add(1);
+    } else if (dt > 30) {
+        std::fprintf(stderr, "rank %d: the failure took %.1f s\n", rank, dt);
+        g_failures.fetch_add(1);
+    }
+    kf_session_destroy(s);  // a peer still waiting on this one sees it close
+}
 }  // namespace
 
 int main(int argc, char **argv)
@@ -133,8 +181,12 @@ int main(int argc, char **argv)
     const int np    = argc > 1 ? std::atoi(argv[1]) : 3;
     const int steps = argc > 2 ? std::atoi(argv[2]) : 2;
     const char *dir = argc > 3 ? argv[3] : "/tmp";
+    const bool dead = argc > 4 && std::string(argv[4]) == "dead";
     std::vector<std::thread> ts;
-    for (int r = 0; r < np; ++r) ts.emplace_back(rank_main, r, np, steps, dir);
+    for (int r = 0; r < np; ++r) {
+        if (dead) ts.emplace_back(dead_main, r, np, dir);
+        else ts.emplace_back(rank_main, r, np, steps, dir);
+    }
     for (auto &t : ts) t.join();
     if (g_failures.load() != 0) {
         std::printf("FAIL %d\n", g_failures.load());
@@ -144,6 +196,6 @@ int main(int argc, char **argv)
         std::printf("kf_shutdown: %s\n", kf_last_error());
         return 1;
     }
-    std::printf("OK np=%d steps=%d\n", np, steps);
+    std::printf("OK np=%d steps=%d%s\n", np, steps, dead ? " dead" : "");
     return 0;
 }

@@ -187,3 +187,12 @@ def test_c_session_async_any_order(session_async_binary, tmp_path, np_):
     r = subprocess.run([session_async_binary, str(np_), "2", str(tmp_path)],
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "OK" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("np_", [2, 3, 4])
+def test_c_session_dead_peer_fails_calls(session_async_binary, tmp_path, np_):
+    """The last rank destroys its session once every session is up; the
+    others' async all-reduces must fail within 30 s (C++ host, threads)."""
+    r = subprocess.run([session_async_binary, str(np_), "1", str(tmp_path), "dead"],
+                       capture_output=True, text=True, timeout=90)
+    assert r.returncode == 0 and "OK" in r.stdout, r.stdout + r.stderr

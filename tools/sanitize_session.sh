@@ -34,6 +34,16 @@ for san in thread address; do
                 timeout -k 10 300 "$D/test_session_async" $np 2 "$S"
         fi
         rm -rf "$S"
+        S=$(mktemp -d "$W/sock.XXXX")
+        echo "-- $san np=$np, last rank gone"
+        if [ $san = thread ]; then
+            TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1" \
+                timeout -k 10 300 "$D/test_session_async" $np 1 "$S" dead
+        else
+            ASAN_OPTIONS="detect_leaks=1 halt_on_error=1" \
+                timeout -k 10 300 "$D/test_session_async" $np 1 "$S" dead
+        fi
+        rm -rf "$S"
     done
 done
 echo "sanitizers: clean"
