@@ -312,28 +312,61 @@ def exchange_phase2(lib, dev, g, world=8):
     Cache; each checked against the oracle-equivalent torch restatement."""
     from kungfu_amd import _lib
     from kungfu_amd.collective import GradBuckets
-    sp = torch.cuda.current_stream().cuda_stream
+    # every launch below goes to this stream, so it can be captured
+    cap = torch.cuda.Stream(device=dev)
+    sp = cap.cuda_stream
     out = {}
     models = _models()
 
     def timed(launch, nsets):
+        """(GPU us per launch, eager us per launch). The exchange issues
+        these launches from C++ between its collectives, so what they cost is
+        GPU time: 4 * nsets launches are captured into one HIP graph and the
+        graph's replay is timed with events on the capture stream (a graph's
+        kernel boundaries cost what a stream's do, MI355X_MICROARCH.md,
+        launch costs). The eager figure times the same launches called one by
+        one from Python through ctypes: for the short shard /np launches
+        (about 6 us) that loop is host-bound (its ~8 us per call was r04's
+        figure)."""
+        torch.cuda.synchronize()  # inputs were made on the default stream
+        with torch.cuda.stream(cap):
+            for i in range(nsets):
+                _lib.check(launch(i), "launch")
+        torch.cuda.synchronize()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        for i in range(nsets):
-            _lib.check(launch(i), "launch")
-        ts = []
-        for _ in range(5):
-            ev0.record()
+        eager = []
+        with torch.cuda.stream(cap):
+            for _ in range(5):
+                ev0.record(cap)
+                for i in range(4 * nsets):
+                    launch(i % nsets)
+                ev1.record(cap)
+                torch.cuda.synchronize()
+                eager.append(ev0.elapsed_time(ev1) * 1e3 / (4 * nsets))
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=cap):
             for i in range(4 * nsets):
                 launch(i % nsets)
-            ev1.record()
-            torch.cuda.synchronize()
-            ts.append(ev0.elapsed_time(ev1) * 1e3 / (4 * nsets))
+        torch.cuda.synchronize()
+        ts = []
+        with torch.cuda.stream(cap):
+            for _ in range(5):
+                ev0.record(cap)
+                graph.replay()
+                ev1.record(cap)
+                torch.cuda.synchronize()
+                ts.append(ev0.elapsed_time(ev1) * 1e3 / (4 * nsets))
+        del graph
         ts.sort()
-        return ts[2]
+        eager.sort()
+        return ts[2], eager[2]
 
-    def report(name, algo_bytes, us, ok, what, nb):
+    def report(name, algo_bytes, uss, ok, what, nb):
+        us, eager = uss
         out[name] = {"us": round(us, 2), "algorithmic_bytes": algo_bytes,
                      "frac": round(algo_bytes / us / 1e3 / HBM_PEAK_GBPS, 4),
+                     "eager_python_us": round(eager, 2),
+                     "timing": "HIP graph replay of the launches on one stream",
                      "correct": bool(ok), "buckets": nb, "what": what}
 
     # C5 at N = 8: per bucket, the workspace holds the 8 received shards back to
@@ -378,8 +411,10 @@ def exchange_phase2(lib, dev, g, world=8):
             ptrs = _lib.ptr_array([s.data_ptr() for s in shard])
             sets.append((ptrs, (ctypes.c_size_t * len(qs))(*qs), bs, shard))
         ref = [s.clone() for s in sets[0][3]]
+        torch.cuda.synchronize()
         _lib.check(lib.kf_bucket_reduce_batch(sets[0][0], 1, sets[0][0], sets[0][1], len(qs),
                                               KF_FLOAT, KF_SUM, world, sp), name)
+        torch.cuda.synchronize()
         ok = all(torch.equal(s, r / torch.full_like(r, float(world)))
                  for s, r in zip(sets[0][3], ref))
         us = timed(lambda i: lib.kf_bucket_reduce_batch(sets[i][0], 1, sets[i][0], sets[i][1],
