@@ -137,12 +137,15 @@ struct kf_ingest {
     std::vector<void *> host;   // page-locked slots
     std::vector<void *> hmap;   // the same slots as the GPU addresses them
     std::vector<hipEvent_t> done;
+    std::vector<hipEvent_t> pre;  // streamed receives: the caller stream's work before the kernel
     std::vector<bool> armed;
     std::mutex mu;  // slot bookkeeping; callers may share one ingest object
 
     ~kf_ingest()
     {
         for (auto e : done)
+            if (e) (void)hipEventDestroy(e);
+        for (auto e : pre)
             if (e) (void)hipEventDestroy(e);
         for (auto p : host)
             if (p) (void)hipHostFree(p);
@@ -259,6 +262,7 @@ kf_ingest_t *kf_ingest_create(size_t slot_bytes, int nslots)
     g->host.assign(nslots, nullptr);
     g->hmap.assign(nslots, nullptr);
     g->done.assign(nslots, nullptr);
+    g->pre.assign(nslots, nullptr);
     g->armed.assign(nslots, false);
     for (int i = 0; i < nslots; ++i) {
         // a streamed receive's kernel reads the slot behind a system acquire
@@ -266,7 +270,8 @@ kf_ingest_t *kf_ingest_create(size_t slot_bytes, int nslots)
         if (hipHostMalloc(&g->host[i], slot_bytes, hipHostMallocDefault) !=
                 hipSuccess ||
             hipHostGetDevicePointer(&g->hmap[i], g->host[i], 0) != hipSuccess ||
-            hipEventCreateWithFlags(&g->done[i], kf_sync::event_flags()) != hipSuccess) {
+            hipEventCreateWithFlags(&g->done[i], kf_sync::event_flags()) != hipSuccess ||
+            hipEventCreateWithFlags(&g->pre[i], hipEventDisableTiming) != hipSuccess) {
             t_ingest_error = "kf_ingest_create: HIP allocation failed";
             delete g;
             return nullptr;
@@ -518,51 +523,87 @@ int read_published(int fd, char *host, uint32_t len, kf_stream::Ctl *ctl)
     return rc;
 }
 
-// the slot's kernel is queued first (it waits in the GPU), then the body is
-// read; the slot is free again once that kernel has run
+// Does other work wait behind this stream's kernels? The legacy null stream
+// (torch's default) serialises with every blocking stream of the device, in
+// every thread of the process, and a blocking stream with it.
+bool holds_others(hipStream_t s)
+{
+    if (s == nullptr) return true;  // the null stream itself
+    unsigned f = 0;
+    if (hipStreamGetFlags(s, &f) != hipSuccess) {
+        (void)hipGetLastError();  // not left for the launch check that follows
+        return true;
+    }
+    return !(f & hipStreamNonBlocking);
+}
+
+// The slot's kernel is queued first (it waits in the GPU), then the body is
+// read; the slot is free again once that kernel has run. A kernel that waits
+// for bytes from a socket must not sit where unrelated work queues behind it:
+// on a stream that holds others (above) it runs on `wait_stream` (a
+// non-blocking stream of the session) after the caller's earlier work, and
+// the caller's stream takes it back (waits for it) only once the whole body
+// is in, when it finishes at once. Sessions in threads of one process that
+// share the null stream otherwise queued each other's folds behind a kernel
+// waiting for a peer whose own sends were queued there too (r05,
+// profiles/r05/failures.md).
 template <typename Launch>
-int streamed(kf_ingest_t *g, int fd, uint32_t len, void *stream, kf_stream::Ctl *ctl,
-             uint32_t piece, Launch launch)
+int streamed(kf_ingest_t *g, int fd, uint32_t len, void *stream, void *wait_stream,
+             kf_stream::Ctl *ctl, uint32_t piece, Launch launch)
 {
     if (len > g->slot_bytes) return proto_fail("chunk larger than ingest slot");
     int slot;
     int rc = g->take(&slot);
     if (rc != KF_OK) return rc;
     kf_stream::reset(ctl, piece);
-    rc = launch(g->hmap[slot]);
+    hipStream_t cs = static_cast<hipStream_t>(stream), ks = cs;
+    if (wait_stream && holds_others(cs)) {
+        ks = static_cast<hipStream_t>(wait_stream);
+        ING_HIP(hipEventRecord(g->pre[slot], cs));
+        ING_HIP(hipStreamWaitEvent(ks, g->pre[slot], 0));
+    }
+    rc = launch(g->hmap[slot], ks);
     if (rc != KF_OK) {
+        kf_stream::abort_wait(ctl);  // in case a kernel did start: it stops waiting
         t_ingest_error = "streamed receive: kernel launch failed";
         return rc;
     }
-    ING_HIP(hipEventRecord(g->done[slot], static_cast<hipStream_t>(stream)));
+    ING_HIP(hipEventRecord(g->done[slot], ks));
     {
         std::lock_guard<std::mutex> lock(g->mu);
         g->armed[slot] = true;
     }
-    return read_published(fd, static_cast<char *>(g->host[slot]), len, ctl);
+    rc = read_published(fd, static_cast<char *>(g->host[slot]), len, ctl);
+    // the caller's later work (the send of this chunk, the next fold) after
+    // the kernel; on a failed read the kernel has been told to stop
+    if (ks != cs && hipStreamWaitEvent(cs, g->done[slot], 0) != hipSuccess && rc == KF_OK) {
+        rc = hip_fail(hipErrorUnknown, "hipStreamWaitEvent after a streamed receive");
+    }
+    return rc;
 }
 }  // namespace
 
 int kf_ingest_recv_onto_streamed(kf_ingest_t *g, int fd, uint32_t len, void *dev_acc,
                                  const void *dev_own, KungFu_Datatype dt, void *stream,
                                  uint32_t piece, kf_stream::Ctl *ctl, kf_stream::Ctl *ctl_dev,
-                                 kf_stream::Board *board, int deadline_ms, bool mark)
+                                 kf_stream::Board *board, int deadline_ms, bool mark,
+                                 void *wait_stream)
 {
     if (!g || !dev_acc || !ctl || !ctl_dev || !board) return KF_ERR_ARG;
-    return streamed(g, fd, len, stream, ctl, piece, [&](void *landing) {
+    return streamed(g, fd, len, stream, wait_stream, ctl, piece, [&](void *landing, hipStream_t ks) {
         return kf_stream::launch_fold(dt, dev_own ? dev_own : dev_acc, landing, dev_acc, len,
-                                      piece, ctl_dev, board, deadline_ms, mark, stream);
+                                      piece, ctl_dev, board, deadline_ms, mark, ks);
     });
 }
 
 int kf_ingest_recv_into_streamed(kf_ingest_t *g, int fd, uint32_t len, void *dev_dst,
                                  void *stream, uint32_t piece, kf_stream::Ctl *ctl,
                                  kf_stream::Ctl *ctl_dev, kf_stream::Board *board,
-                                 int deadline_ms)
+                                 int deadline_ms, void *wait_stream)
 {
     if (!g || (!dev_dst && len > 0) || !ctl || !ctl_dev || !board) return KF_ERR_ARG;
-    return streamed(g, fd, len, stream, ctl, piece, [&](void *landing) {
+    return streamed(g, fd, len, stream, wait_stream, ctl, piece, [&](void *landing, hipStream_t ks) {
         return kf_stream::launch_copy_in(landing, dev_dst, len, piece, ctl_dev, board, deadline_ms,
-                                         stream);
+                                         ks);
     });
 }

@@ -624,6 +624,8 @@ struct kf_session {
     size_t max_pieces = 0;
     hipStream_t tx_stream  = nullptr;  // sender's D2H stream
     hipStream_t mir_stream = nullptr;  // the bcast root's mirror -> HBM copies
+    hipStream_t wait_stream = nullptr;  // streamed kernels while they wait for a body
+                                        // (when the caller's stream holds others)
     std::vector<hipEvent_t> ev_pool;  // free "chunk is final" events
     std::mutex ev_mu;
     kf_host_reduce_fn host_fn = nullptr;
@@ -798,6 +800,7 @@ struct kf_session {
         for (auto e : ev_pool) (void)hipEventDestroy(e);
         if (tx_stream) (void)hipStreamDestroy(tx_stream);
         if (mir_stream) (void)hipStreamDestroy(mir_stream);
+        if (wait_stream) (void)hipStreamDestroy(wait_stream);
         for (auto &l : stage_pool.idle) (void)hipFree(l.p);
         for (auto &l : mirror_pool.idle) (void)hipHostFree(l.p);
         for (auto &l : ctl_pool.idle) (void)hipHostFree(l.p);
@@ -1627,7 +1630,7 @@ int kf_session::handle(SessOp &o, size_t i, uint32_t flags, int peer, int fd, co
             c.sctl_used |= 2;
             r = kf_ingest_recv_into_streamed(ingest, fd, len, dst, stream, stream_piece,
                                              ctl_at(o, i, 1), ctl_at(o, i, 1, true), board,
-                                             stream_deadline_ms);
+                                             stream_deadline_ms, wait_stream);
         } else if (device_mode) {
             r = pieces ? kf_ingest_recv_into_pieces(ingest, fd, len, dst, stream, piece)
                        : kf_ingest_recv_into(ingest, fd, len, dst, stream);
@@ -1683,7 +1686,7 @@ int kf_session::handle(SessOp &o, size_t i, uint32_t flags, int peer, int fd, co
             c.sctl_used |= 1;
             r = kf_ingest_recv_onto_streamed(ingest, fd, len, out, own, o.dt, stream, stream_piece,
                                              ctl_at(o, i, 0), ctl_at(o, i, 0, true), board,
-                                             stream_deadline_ms, to_mirror);
+                                             stream_deadline_ms, to_mirror, wait_stream);
             if (r != KF_OK) return fail(r, kf_ingest_last_error());
             c.streamed = to_mirror;
         } else if (pieces) {
@@ -2349,6 +2352,9 @@ kf_session_t *create_session(int rank, std::vector<PeerAddr> peers, const char *
         if (hipStreamCreateWithFlags(&s->tx_stream, hipStreamNonBlocking) != hipSuccess) {
             s->tx_stream = nullptr;
         }
+        if (hipStreamCreateWithFlags(&s->wait_stream, hipStreamNonBlocking) != hipSuccess) {
+            s->wait_stream = nullptr;
+        }
         const char *ms = std::getenv("KUNGFU_AMD_MIRROR_SIDE");  // 0: A/B, caller's stream
         if ((!ms || std::atoi(ms) != 0) &&
             hipStreamCreateWithFlags(&s->mir_stream, hipStreamNonBlocking) != hipSuccess) {
@@ -2373,7 +2379,7 @@ kf_session_t *create_session(int rank, std::vector<PeerAddr> peers, const char *
                 if (tx_ok) s->tx_piece_ev.push_back(e);
             }
         }
-        if (!s->ingest || !tx_ok || !s->tx_stream || !s->board) {
+        if (!s->ingest || !tx_ok || !s->tx_stream || !s->board || !s->wait_stream) {
             t_sess_error = !s->board ? "streamed kernels' device words (hipMalloc) failed"
                                      : "kf_ingest_create failed";
             delete s;

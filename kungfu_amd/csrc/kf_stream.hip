@@ -331,6 +331,7 @@ int fold_as(const void *own, const void *landing, void *out, uint32_t len, int m
     if (len % sizeof(S)) return KF_ERR_ARG;
     const Seen w = next_seen(board);
     if (!w.word) return KF_ERR_HIP;
+    (void)hipGetLastError();  // the check below is about this launch only
     fold_kernel<T><<<blocks(len) + 1, kLanes, 0, s>>>(
         static_cast<const S *>(own), static_cast<const char *>(landing), static_cast<S *>(out), len,
         mark, c, w.word, w.epoch, limit);
@@ -398,6 +399,7 @@ int launch_copy_in(const void *landing_dev, void *dst, uint32_t len, uint32_t pi
     if (!fits(len, piece)) return KF_ERR_ARG;
     const Seen w = next_seen(board);
     if (!w.word) return KF_ERR_HIP;
+    (void)hipGetLastError();
     copy_in_kernel<<<blocks(len) + 1, kLanes, 0, static_cast<hipStream_t>(stream)>>>(
         static_cast<const char *>(landing_dev), static_cast<char *>(dst), len, c_dev, w.word,
         w.epoch, ticks(deadline_ms));
@@ -409,6 +411,7 @@ int launch_copy_out(const void *src, void *host_dev, uint32_t len, uint32_t piec
 {
     if (len == 0) return KF_OK;
     if (!fits(len, piece)) return KF_ERR_ARG;
+    (void)hipGetLastError();
     copy_out_kernel<<<blocks(len), kLanes, 0, static_cast<hipStream_t>(stream)>>>(
         static_cast<const char *>(src), static_cast<char *>(host_dev), len, c_dev);
     return hipGetLastError() == hipSuccess ? KF_OK : KF_ERR_HIP;
@@ -477,6 +480,7 @@ int launch_copy(void *dst, const void *src, size_t len, void *stream)
     if (len == 0) return KF_OK;
     const size_t nblk = (len + kBlockBytes - 1) / kBlockBytes;
     if (nblk > 0x7fffffffu) return KF_ERR_ARG;
+    (void)hipGetLastError();
     copy_kernel<<<static_cast<unsigned>(nblk), kLanes, 0, static_cast<hipStream_t>(stream)>>>(
         static_cast<char *>(dst), static_cast<const char *>(src), len);
     return hipGetLastError() == hipSuccess ? KF_OK : KF_ERR_HIP;

@@ -112,8 +112,11 @@ int stream_sync(void *stream);   // KF_OK or KF_ERR_HIP
 int kf_ingest_recv_onto_streamed(kf_ingest_t *g, int fd, uint32_t len, void *dev_acc,
                                  const void *dev_own, KungFu_Datatype dt, void *stream,
                                  uint32_t piece, kf_stream::Ctl *ctl, kf_stream::Ctl *ctl_dev,
-                                 kf_stream::Board *board, int deadline_ms, bool mark);
+                                 kf_stream::Board *board, int deadline_ms, bool mark,
+                                 void *wait_stream);
 int kf_ingest_recv_into_streamed(kf_ingest_t *g, int fd, uint32_t len, void *dev_dst,
                                  void *stream, uint32_t piece, kf_stream::Ctl *ctl,
                                  kf_stream::Ctl *ctl_dev, kf_stream::Board *board,
-                                 int deadline_ms);
+                                 int deadline_ms, void *wait_stream);
+// (wait_stream: a non-blocking stream the kernel runs on while it waits for
+// the body, when `stream` is one other work serialises with; kf_ingest.hip)

@@ -264,12 +264,15 @@ def test_native_hierarchical_threads_two_hosts_two_ranks():
             import traceback
             errs.append("rank %d: %s" % (g, traceback.format_exc()))
 
-    ts = [threading.Thread(target=run, args=(g,)) for g in range(4)]
+    ts = [threading.Thread(target=run, args=(g,), daemon=True) for g in range(4)]
     for t in ts:
         t.start()
+    import time
+    deadline = time.monotonic() + 100  # inside pytest's 120 s, so the errors print
     for t in ts:
-        t.join(timeout=240)
-    assert not any(t.is_alive() for t in ts), "a rank did not finish"
+        t.join(timeout=max(0.0, deadline - time.monotonic()))
+    alive = [g for g, t in enumerate(ts) if t.is_alive()]
+    assert not alive, "ranks %s did not finish; the others reported:\n%s" % (alive, "\n".join(errs))
     for gr in groups:
         gr.close()
     assert not errs, "\n".join(errs)

@@ -110,6 +110,25 @@ __global__ void __launch_bounds__(B) tile_kernel_padded(SegsPadded pa)
         if (v0 + u * B < nv) stp<POL>(p + v0 + u * B, v[u] * 0.125f);
 }
 
+// the tile kernel with the shard found by one division (every shard has the
+// same block count) instead of a binary search over the kernarg table
+template <int B, int U, int POL>
+__global__ void __launch_bounds__(B) tile_kernel_uniform(Segs a, unsigned per)
+{
+    const int s       = blockIdx.x / per;
+    const unsigned t  = blockIdx.x - s * per;
+    const size_t v0   = static_cast<size_t>(t) * (B * U) + threadIdx.x;
+    f32x4 *p          = a.p[s];
+    const unsigned nv = a.nvec[s];
+    f32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        if (v0 + u * B < nv) v[u] = ldp<POL>(p + v0 + u * B);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        if (v0 + u * B < nv) stp<POL>(p + v0 + u * B, v[u] * 0.125f);
+}
+
 // the same, block b taking tile (b / nseg) of shard (b % nseg): every shard
 // is swept by every part of the grid at once
 template <int B, int U, int POL>
@@ -239,7 +258,9 @@ void run_variant(const char *cfg, const char *name, int form, const std::vector<
     CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
     const unsigned pgrid = std::min<unsigned>(nblk, static_cast<unsigned>(ncu) * 4);
     auto launch = [&](int i) {
-        if (form == 3) {
+        if (form == 4) {
+            tile_kernel_uniform<B, U, POL><<<nblk, B>>>(segs[i], nblk / segs[i].nseg);
+        } else if (form == 3) {
             SegsPadded pa{};
             pa.a = segs[i];
             tile_kernel_padded<B, U, POL><<<nblk, B>>>(pa);
@@ -317,6 +338,8 @@ void config(const char *cfg, const std::vector<size_t> &counts)
     for (int warm = 0; warm < 2; ++warm) {
         run_variant<256, 2, 3>(cfg, "tile 256x2 nt (product)", 0, sets, nvec, bytes, warm);
         run_variant<256, 2, 3>(cfg, "tile 256x2 nt, 2.8 KB args", 3, sets, nvec, bytes, warm);
+        run_variant<256, 2, 3>(cfg, "tile 256x2 nt, shard by division", 4, sets, nvec, bytes, warm);
+        run_variant<256, 4, 3>(cfg, "tile 256x4 nt, shard by division", 4, sets, nvec, bytes, warm);
         if (warm) continue;
         run_variant<256, 1, 3>(cfg, "tile 256x1 nt", 0, sets, nvec, bytes, false);
         run_variant<256, 4, 3>(cfg, "tile 256x4 nt", 0, sets, nvec, bytes, false);
