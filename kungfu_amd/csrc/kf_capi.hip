@@ -389,14 +389,17 @@ int launch_batch_kc(const void *const *in, int k, void *const *outs, const size_
     BatchArgsT<NSEG, NPTR> a;
     a.nseg          = 0;
     size_t blocks   = 0;
+    size_t per      = 0;  // the launch's common block count per bucket, 0: they differ
     auto flush      = [&]() -> int {
         if (a.nseg == 0) return KF_OK;
         a.blk0[a.nseg] = static_cast<unsigned>(blocks);
         a.serial       = KC == 0 && blocks >= kSerialMinBlocks ? 1 : 0;
+        a.per          = static_cast<unsigned>(per);
         reduce_batch_kernel<T, OP, EPI, KC, B, U, NSEG, NPTR>
             <<<static_cast<unsigned>(blocks), B, 0, s>>>(a, k, np);
         a.nseg = 0;
         blocks = 0;
+        per    = 0;
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return hip_fail(e, "reduce batch kernel launch");
         return KF_OK;
@@ -428,6 +431,7 @@ int launch_batch_kc(const void *const *in, int k, void *const *outs, const size_
         a.head[j] = p.head;
         a.nvec[j] = p.nvec;
         a.blk0[j] = static_cast<unsigned>(blocks);
+        per       = j == 0 ? nblk : (per == nblk ? per : 0);
         blocks += nblk;
         ++a.nseg;
         if (a.nseg == NSEG) {

@@ -156,6 +156,35 @@ def test_batch_kernel_matches_oracle(name, k, avg):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("k,avg", [(1, True), (2, False), (8, True), (3, False)])
+def test_batch_kernel_equal_buckets(k, avg):
+    """Buckets of one size (the exchange's shards of equal buckets) take the
+    launch's common block count: the kernel finds a block's bucket by one
+    division instead of searching the argument table. 70 equal f32 buckets
+    (two launches at k = 1, five at k >= 2) with one misaligned bucket in the
+    middle (a launch of its own), /np and plain, against the oracle."""
+    import torch
+    from kungfu_amd import _lib
+    from oracle import oracle
+    dev = _gpu()
+    lib = _lib.load()
+    nb, n = 70, 49968 * 4 + 3
+    hs = [[_rand("f32", n, 9000 + 10 * b + j) for j in range(k)] for b in range(nb)]
+    ins = [[_to_dev(a, "f32", dev) for a in row] for row in hs]
+    ins[33] = [torch.cat([t[:1], t])[1:] for t in ins[33]]
+    outs = [torch.empty_like(row[0]) for row in ins]
+    rc = lib.kf_bucket_reduce_batch(
+        _lib.ptr_array([t.data_ptr() for row in ins for t in row]), k,
+        _lib.ptr_array([o.data_ptr() for o in outs]), (ctypes.c_size_t * nb)(*[n] * nb), nb,
+        oracle.DT["f32"], 0, 8 if avg else 0, torch.cuda.current_stream().cuda_stream)
+    _lib.check(rc, "kf_bucket_reduce_batch")
+    torch.cuda.synchronize()
+    for b in range(nb):
+        want = oracle.reduce_avg(hs[b], "f32", 8) if avg else oracle.reduce_k(hs[b], "f32", "sum")
+        assert np.array_equal(_to_np(outs[b], "f32"), want), b
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("name", ["f32", "bf16"])
 def test_batch_kernel_k1_past_64_buckets(name):
     """k = 1 (the shard /np) packs up to 64 buckets per launch (kBatchSeg1):
