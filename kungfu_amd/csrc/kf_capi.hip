@@ -394,9 +394,12 @@ int launch_batch_kc(const void *const *in, int k, void *const *outs, const size_
         if (a.nseg == 0) return KF_OK;
         a.blk0[a.nseg] = static_cast<unsigned>(blocks);
         a.serial       = KC == 0 && blocks >= kSerialMinBlocks ? 1 : 0;
-        a.per          = static_cast<unsigned>(per);
-        reduce_batch_kernel<T, OP, EPI, KC, B, U, NSEG, NPTR>
-            <<<static_cast<unsigned>(blocks), B, 0, s>>>(a, k, np);
+        // equal block counts: one grid row per bucket (the kernel reads the
+        // bucket off blockIdx.y instead of searching blk0)
+        const dim3 grid = per && a.nseg > 1
+                              ? dim3(static_cast<unsigned>(per), static_cast<unsigned>(a.nseg))
+                              : dim3(static_cast<unsigned>(blocks));
+        reduce_batch_kernel<T, OP, EPI, KC, B, U, NSEG, NPTR><<<grid, B, 0, s>>>(a, k, np);
         a.nseg = 0;
         blocks = 0;
         per    = 0;

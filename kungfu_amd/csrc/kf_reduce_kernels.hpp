@@ -566,8 +566,7 @@ template <int NSEG, int NPTR> struct BatchArgsT {
     size_t n[NSEG], head[NSEG], nvec[NSEG];
     unsigned blk0[NSEG + 1];
     int nseg;
-    int serial;    // the runtime-k fold's one-in-flight schedule (reduce_body)
-    unsigned per;  // every bucket of the launch has this many blocks (0: they differ)
+    int serial;  // the runtime-k fold's one-in-flight schedule (reduce_body)
 };
 using BatchArgs  = BatchArgsT<kBatchSeg, kMaxInputs>;
 using BatchArgs1 = BatchArgsT<kBatchSeg1, 1>;
@@ -597,14 +596,17 @@ template <typename T, int OP, int EPI, int KC, int BLOCK, int UNROLL, int NSEG, 
 __global__ void __launch_bounds__(BLOCK) reduce_batch_kernel(BatchArgsT<NSEG, NPTR> a, int k,
                                                              Div np)
 {
-    const unsigned b = blockIdx.x;
-    // equal buckets (the exchange's shards of equal buckets): the bucket by one
-    // division, no search through the kernarg table — its dependent scalar
-    // loads cost 0.4-1.5 us of a ~6 us launch (tools/explore/shard_probe.hip,
-    // profiles/r05/shard_probe_r05k.jsonl)
-    const int s       = a.per ? static_cast<int>(b / a.per) : batch_segment(a, b);
-    const unsigned b0 = a.per ? static_cast<unsigned>(s) * a.per : a.blk0[s];
-    const size_t nblk = a.per ? a.per : a.blk0[s + 1] - a.blk0[s];
+    // Buckets with equal block counts (the exchange's shards of equal
+    // buckets) come as a 2-D grid, one row per bucket: the bucket is
+    // blockIdx.y, known before any kernarg load. Otherwise the bucket of block
+    // b is searched in the kernarg table, one dependent scalar load per step,
+    // which cost 0.4-1.5 us of a ~6 us launch (tools/explore/shard_probe.hip,
+    // profiles/r05/shard_probe_r05k.jsonl).
+    const bool rows   = gridDim.y > 1;
+    const unsigned b  = blockIdx.x;
+    const int s       = rows ? static_cast<int>(blockIdx.y) : batch_segment(a, b);
+    const unsigned b0 = rows ? 0u : a.blk0[s];
+    const size_t nblk = rows ? gridDim.x : a.blk0[s + 1] - a.blk0[s];
     InPtrs one;  // NPTR == 1: the bucket's single input (only p[0] is read, KC == 1)
     if constexpr (NPTR == 1) one.p[0] = a.in[s][0];
     const InPtrs &in = [&]() -> const InPtrs & {

@@ -18,9 +18,11 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "kungfu_amd.h"
+#include "../../kungfu_amd/csrc/kf_reduce_kernels.hpp"
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -333,6 +335,52 @@ void config(const char *cfg, const std::vector<size_t> &counts)
             printf("{\"config\": \"%s\", \"variant\": \"library kf_bucket_reduce_batch\", "
                    "\"warm\": %s, \"us\": %.2f, \"frac\": %.4f}\n",
                    cfg, warm ? "true" : "false", us, bytes / us / 1e3 / 8000.0);
+        }
+    }
+    // the product's batch kernel itself, launched here with the arguments the
+    // host builds (so the launch path is the probe's), per = common blocks or 0
+    for (int variant = 0; variant < 3; ++variant) {
+        constexpr int B = 256;
+        const int U = variant == 2 ? 4 : 2;
+        std::vector<kf::BatchArgsT<64, 1>> args(nsets);
+        unsigned nblk_total = 0;
+        for (int i = 0; i < nsets; ++i) {
+            auto &a = args[i];
+            memset(&a, 0, sizeof(a));
+            a.nseg = static_cast<int>(nvec.size());
+            unsigned blk = 0;
+            const unsigned per = (nvec[0] + B * U - 1) / (B * U);
+            for (int j = 0; j < a.nseg; ++j) {
+                a.in[j][0] = sets[i].shards[j];
+                a.out[j]   = sets[i].shards[j];
+                a.n[j]     = counts[j];
+                a.head[j]  = 0;
+                a.nvec[j]  = nvec[j];
+                a.blk0[j]  = blk;
+                blk += per;
+            }
+            a.blk0[a.nseg] = blk;
+            a.serial       = 0;
+            nblk_total     = blk;
+        }
+        kf::Div np{};
+        np.f = 8.0f; np.fi = 0.125f; np.d = 8.0; np.di = 0.125; np.pow2 = 1;
+        for (int warm = 0; warm < 2; ++warm) {
+            const unsigned nseg = static_cast<unsigned>(nvec.size());
+            const dim3 grid = variant == 1 ? dim3(nblk_total) : dim3(nblk_total / nseg, nseg);
+            auto launch = [&](int i) {
+                if (U == 2)
+                    kf::reduce_batch_kernel<float, kf::OP_SUM, kf::EPI_DIV, 1, 256, 2, 64, 1>
+                        <<<grid, 256>>>(args[i], 1, np);
+                else
+                    kf::reduce_batch_kernel<float, kf::OP_SUM, kf::EPI_DIV, 1, 256, 4, 64, 1>
+                        <<<grid, 256>>>(args[i], 1, np);
+            };
+            const double us = time_us(launch, warm ? 1 : nsets);
+            printf("{\"config\": \"%s\", \"variant\": \"product kernel U=%d %s\", "
+                   "\"warm\": %s, \"us\": %.2f, \"frac\": %.4f}\n",
+                   cfg, U, variant == 1 ? "search" : "grid rows", warm ? "true" : "false", us,
+                   bytes / us / 1e3 / 8000.0);
         }
     }
     for (int warm = 0; warm < 2; ++warm) {
