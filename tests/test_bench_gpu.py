@@ -162,7 +162,7 @@ def test_bench_exchange_branch_single_rank_rccl():
     assert d["value"] == d["collective"]["algbw_GiBps_per_gpu"]
     # the primary's schedule trial: every schedule parity-checked and timed
     trial = d["collective"]["schedule_trial_ms"]
-    assert sorted(trial) == ["a2a", "fused", "grouped", "pipelined", "rs_avg"], trial
+    assert sorted(trial) == ["a2a", "fused", "grouped", "pipelined"], trial
     # the per-phase split of the timed step on the native exchange
     ph = d["collective"]["phase_us"]
     assert ph["timed_calls_per_step"] > 0 or ph.get("pipelined_calls_untimed"), ph

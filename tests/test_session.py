@@ -269,6 +269,21 @@ def test_session_device_streamed(strategy, size, piece_kb, kind, batch_fold):
 
 
 @pytest.mark.gpu
+def test_session_device_streamed_stress():
+    """the streamed kernels write page-locked memory the
+    host sender reads after per-block flags. Every byte of a 40-chunk bucket
+    per call, every stage streamed (copy out, fold, copy in), 4 KiB pieces
+    (one block per piece: the most flags), np = 3 under RING, whose result is
+    order-free, so each chunk is checked exactly against the schedule oracle;
+    out of place and in place."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    run(3, "device", "rand", (40 << 20) // 4 + 5, strategy="RING",
+        env={"KUNGFU_AMD_STREAM": "1", "KUNGFU_AMD_STREAM_PIECE_KB": "4"})
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("strategy", ["RING", "BINARY_TREE"])
 def test_session_device_streamed_launch_race(strategy):
     """rank 2 of [RING-3-4-rand-0] aborted in the HIP
