@@ -541,7 +541,8 @@ bool holds_others(hipStream_t s)
 // read; the slot is free again once that kernel has run. A kernel that waits
 // for bytes from a socket must not sit where unrelated work queues behind it:
 // on a stream that holds others (above) it runs on `wait_stream` (a
-// non-blocking stream of the session) after the caller's earlier work, and
+// non-blocking stream of the session, passed when other sessions share the
+// process; kf_session.hip g_device_sessions) after the caller's earlier work, and
 // the caller's stream takes it back (waits for it) only once the whole body
 // is in, when it finishes at once. Sessions in threads of one process that
 // share the null stream otherwise queued each other's folds behind a kernel

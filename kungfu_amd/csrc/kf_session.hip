@@ -50,6 +50,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cerrno>
 #include <chrono>
 #include <condition_variable>
@@ -77,6 +78,16 @@ constexpr int kConnRetry     = 500;              // config.go:15-18
 constexpr int kRetryPeriodUs = 200000;
 
 thread_local std::string t_sess_error;
+
+// device-mode sessions alive in this process. A streamed kernel waiting for a
+// socket body on a stream that holds others (the null stream) is harmless
+// while it is the process's only session: nothing else in the process has to
+// run for that body to come. With several (ranks emulated as threads, the
+// hierarchical path's sessions) another session's sends may queue behind it,
+// so the kernel then waits on the session's own non-blocking stream instead
+// (kf_ingest.hip streamed(); that costs two cross-stream event hops per
+// chunk, C1 np = 2 0.60 -> 0.65 ms, so it is not taken when not needed).
+std::atomic<int> g_device_sessions{0};
 
 int fail(int rc, const std::string &what)
 {
@@ -625,7 +636,13 @@ struct kf_session {
     hipStream_t tx_stream  = nullptr;  // sender's D2H stream
     hipStream_t mir_stream = nullptr;  // the bcast root's mirror -> HBM copies
     hipStream_t wait_stream = nullptr;  // streamed kernels while they wait for a body
-                                        // (when the caller's stream holds others)
+                                        // (when the caller's stream holds others and
+                                        // other sessions live in the process)
+    bool counted = false;               // in g_device_sessions
+    void *waiting_stream() const
+    {
+        return g_device_sessions.load(std::memory_order_relaxed) > 1 ? wait_stream : nullptr;
+    }
     std::vector<hipEvent_t> ev_pool;  // free "chunk is final" events
     std::mutex ev_mu;
     kf_host_reduce_fn host_fn = nullptr;
@@ -801,6 +818,7 @@ struct kf_session {
         if (tx_stream) (void)hipStreamDestroy(tx_stream);
         if (mir_stream) (void)hipStreamDestroy(mir_stream);
         if (wait_stream) (void)hipStreamDestroy(wait_stream);
+        if (counted) g_device_sessions.fetch_sub(1, std::memory_order_relaxed);
         for (auto &l : stage_pool.idle) (void)hipFree(l.p);
         for (auto &l : mirror_pool.idle) (void)hipHostFree(l.p);
         for (auto &l : ctl_pool.idle) (void)hipHostFree(l.p);
@@ -1630,7 +1648,7 @@ int kf_session::handle(SessOp &o, size_t i, uint32_t flags, int peer, int fd, co
             c.sctl_used |= 2;
             r = kf_ingest_recv_into_streamed(ingest, fd, len, dst, stream, stream_piece,
                                              ctl_at(o, i, 1), ctl_at(o, i, 1, true), board,
-                                             stream_deadline_ms, wait_stream);
+                                             stream_deadline_ms, waiting_stream());
         } else if (device_mode) {
             r = pieces ? kf_ingest_recv_into_pieces(ingest, fd, len, dst, stream, piece)
                        : kf_ingest_recv_into(ingest, fd, len, dst, stream);
@@ -1686,7 +1704,7 @@ int kf_session::handle(SessOp &o, size_t i, uint32_t flags, int peer, int fd, co
             c.sctl_used |= 1;
             r = kf_ingest_recv_onto_streamed(ingest, fd, len, out, own, o.dt, stream, stream_piece,
                                              ctl_at(o, i, 0), ctl_at(o, i, 0, true), board,
-                                             stream_deadline_ms, to_mirror, wait_stream);
+                                             stream_deadline_ms, to_mirror, waiting_stream());
             if (r != KF_OK) return fail(r, kf_ingest_last_error());
             c.streamed = to_mirror;
         } else if (pieces) {
@@ -2379,6 +2397,8 @@ kf_session_t *create_session(int rank, std::vector<PeerAddr> peers, const char *
                 if (tx_ok) s->tx_piece_ev.push_back(e);
             }
         }
+        s->counted = true;
+        g_device_sessions.fetch_add(1, std::memory_order_relaxed);
         if (!s->ingest || !tx_ok || !s->tx_stream || !s->board || !s->wait_stream) {
             t_sess_error = !s->board ? "streamed kernels' device words (hipMalloc) failed"
                                      : "kf_ingest_create failed";
