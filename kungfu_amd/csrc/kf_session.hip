@@ -2174,9 +2174,9 @@ int kf_session::run(SessOp *one)
             for (SessOp *o : active) {
                 if (o->remaining == 0) continue;
                 if (o->deadline <= now) {
-                    fail_op(o, fail(KF_ERR_TIMEOUT, o->name + ": no message for " +
+                    fail_op(o, fail(KF_ERR_TIMEOUT, o->name + ": its messages did not all come within " +
                                                         std::to_string(op_timeout_ms) +
-                                                        " ms (KUNGFU_AMD_OP_TIMEOUT_S)"),
+                                                        " ms of its start (KUNGFU_AMD_OP_TIMEOUT_S)"),
                             t_sess_error);
                     expired = true;
                     continue;
