@@ -6,7 +6,10 @@
   from a peer whose connection reached EOF) and the test ends inside 60 s.
   VERDICT r04: at np = 3 the survivors kept their connection to each other
   and waited in poll(-1) for 600 s. The reference has no such detection
-  (rchannel/handler/collective.go:27-30 blocks on a channel).
+  (rchannel/handler/collective.go:27-30 blocks on a channel); its own
+  failure test is a worker that exits with status 1 mid-run
+  (tests/go/cmd/kungfu-bad-worker/kungfu-bad-worker.go:30-38), which leaves
+  ending the job to the runner. Here the library ends the calls itself.
 * device mode, streamed stages: a CPU-side fake peer speaks the
   rchannel wire format, sends a header and part of a body, then closes, or
   stalls past KUNGFU_AMD_STREAM_TIMEOUT_MS and sends the rest, or stalls
