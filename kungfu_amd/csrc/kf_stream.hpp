@@ -22,7 +22,8 @@
 // one system-scope atomic add per block onto a per-piece counter 254 us
 // (atomics to host memory serialise); one flag word per block behind a
 // system release fence 36 us; written-through (sc1) stores drained before
-// the flag 21.6 us — the shipped form. Reads: plain 24-29 us, one acquire
+// the flag 21.6 us — the r04 form; r05 ships the same with system scope
+// (sc0 sc1, kf_stream.hip KF_STREAM_HOST_STORE_AUX). Reads: plain 24-29 us, one acquire
 // fence per block 54-61 us, system-coherent (sc0 sc1) loads 26.5 us — the
 // shipped form. In a running session the per-block fences also serialise on
 // each XCD's L2 (a write-back and an invalidate of the whole L2 each, 257
