@@ -110,6 +110,18 @@ func (e *Exchange) AllReduceBatch(bufs []DevicePtr, counts []int, t DataType, op
 // Check reports an asynchronous RCCL failure.
 func (e *Exchange) Check() error { return exStatus("kf_exchange_check", C.kf_exchange_check(e.h)) }
 
+// TransportInfo is what RCCL itself reports (kf_exchange_transport_info):
+// the communicator's rank count (ncclCommCount) and RCCL's version code
+// (ncclGetVersion); -1 and 0 over a host-provided transport.
+func (e *Exchange) TransportInfo() (commCount int, version int, err error) {
+	var c, v C.int
+	if err := exStatus("kf_exchange_transport_info",
+		C.kf_exchange_transport_info(e.h, &c, &v)); err != nil {
+		return 0, 0, err
+	}
+	return int(c), int(v), nil
+}
+
 // SetPipeline splits every batch call into groups whose HIP work overlaps the
 // next group's RCCL phases (kf_exchange_set_pipeline; 1 = off). Same results.
 func (e *Exchange) SetPipeline(groups int) error {
