@@ -31,7 +31,7 @@ def test_bench_n2_rehearsal_with_p2p_children():
            "--master-addr", "127.0.0.1", "--master-port", str(_port()),
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
            "--device-index", "0", "--steps", "3", "--warmup", "1", "--elems", str(4 << 20),
-           "--extras", "c4_torch,c3_p2p,c5_p2p", "--extras-timeout", "100"]
+           "--extras", "c4_torch,c5_torch,c3_p2p,c5_p2p", "--extras-timeout", "100"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.strip()]
@@ -39,6 +39,13 @@ def test_bench_n2_rehearsal_with_p2p_children():
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["value"] > 0 and d["scaling"] == "weak"
     assert "error" not in d["c4_torch"], d["c4_torch"]
+    # the N > 1 line says which exchange ran and splits C4's and C5's steps
+    # into phases too; same-GPU gloo has no RCCL world
+    c = d["collective"]
+    assert c["exchange_kind"] == "torch.distributed" and c["rccl_world"] is None, c
+    for k in ("c4_torch", "c5_torch"):
+        ph = d[k]["phase_us"]
+        assert ph and ph["step_us"] > 0 and ph["sum"] > 0, (k, ph)
     for k in ("c3_p2p", "c5_p2p"):
         assert "error" not in d[k], d[k]
         assert d[k]["ms_per_step"] > 0
