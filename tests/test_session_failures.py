@@ -266,3 +266,62 @@ def test_streamed_peer_fails_call(role, how, stages, monkeypatch):
     assert dt < 20, (dt, msg)
     if how == "stall_resume":  # the body came in full, late: the kernel had given up
         assert "KF_ERR_TIMEOUT" in msg or "HIP" in msg or "stopped waiting" in msg, msg
+
+
+@pytest.mark.parametrize("how", ["silent", "stall", "close"])
+def test_host_session_bounded_by_op_timeout(how, monkeypatch):
+    """Host mode, CPU only: KUNGFU_AMD_OP_TIMEOUT_S bounds a call whose peer
+    stays connected but never sends ("silent": the poll's deadline), or
+    stops partway through a body ("stall": SO_RCVTIMEO on the read); a peer
+    that closes mid-body fails the call at once ("close"). The real session
+    is the STAR root; the fake leaf speaks the rchannel wire format."""
+    from kungfu_amd import _lib
+    from kungfu_amd.session import Session
+    from test_session import oracle_reduce_fn
+    lib = _lib.load()
+    monkeypatch.setenv("KUNGFU_ALLREDUCE_STRATEGY", "STAR")
+    monkeypatch.setenv("KUNGFU_AMD_OP_TIMEOUT_S", "2")
+    body = np.full(NF, 2.0, np.float32).tobytes()
+    with tempfile.TemporaryDirectory() as d:
+        def script(rx, tx):
+            if how != "silent":
+                _partial_then(tx, 0, body, "close" if how == "close" else "stall", 0)
+            _drain(rx, 6)
+
+        fake = FakePeer(lib, d, 1, script)
+        fake.start()
+        s = Session(0, 2, d, mode="host", host_reduce_fn=oracle_reduce_fn())
+        x = np.ones(NF, np.float32)
+        y = np.zeros_like(x)
+        t0 = time.monotonic()
+        with pytest.raises(RuntimeError) as ei:
+            s.all_reduce(x, y, NAME)
+        dt = time.monotonic() - t0
+        s.close()
+        fake.join(15)
+        fake.close()
+        assert fake.err is None, fake.err
+    msg = str(ei.value)
+    if how == "close":
+        assert dt < 2, (dt, msg)
+        assert "KF_ERR_IO" in msg or "KF_ERR_PROTO" in msg, msg
+    else:
+        assert 1.5 < dt < 8, (dt, msg)
+        assert ("KF_ERR_TIMEOUT" in msg or "KUNGFU_AMD_OP_TIMEOUT_S" in msg
+                or "KF_ERR_IO" in msg), msg
+
+
+def test_op_timeout_rejects_bad_values(monkeypatch):
+    """KUNGFU_AMD_OP_TIMEOUT_S must be whole seconds >= 0 (0: no deadline);
+    anything else fails session creation with a message, never silently."""
+    from kungfu_amd import _lib
+    from kungfu_amd.session import Session
+    for bad in ("-1", "abc", "2.5", ""):
+        monkeypatch.setenv("KUNGFU_AMD_OP_TIMEOUT_S", bad)
+        with tempfile.TemporaryDirectory() as d:
+            with pytest.raises(_lib.KungFuAMDError) as ei:
+                Session(0, 1, d, mode="host")
+            assert "KUNGFU_AMD_OP_TIMEOUT_S" in str(ei.value), (bad, ei.value)
+    monkeypatch.setenv("KUNGFU_AMD_OP_TIMEOUT_S", "0")
+    with tempfile.TemporaryDirectory() as d:
+        Session(0, 1, d, mode="host").close()
