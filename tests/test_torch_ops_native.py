@@ -30,6 +30,20 @@ def test_module_surface_and_uninitialised_errors():
         m.init_exchange(b"short", 0, 1, 0)
 
 
+@pytest.mark.parametrize("bad", ["0", "-5", "abc", "2.5", "99999999"])
+def test_init_timeout_env_is_validated(bad, monkeypatch):
+    """KUNGFU_AMD_INIT_TIMEOUT_S was read with atoi and
+    multiplied in int, so "0" or junk timed every init out at once and huge
+    values overflowed to "wait forever". Now anything but whole seconds in
+    [1, 86400] is refused, with a message, before RCCL is touched."""
+    m = _mod()
+    if m.initialized():
+        pytest.skip("already initialised in this process")
+    monkeypatch.setenv("KUNGFU_AMD_INIT_TIMEOUT_S", bad)
+    with pytest.raises(RuntimeError, match="KUNGFU_AMD_INIT_TIMEOUT_S"):
+        m.init_exchange(b"\0" * 128, 0, 1, 0)
+
+
 @pytest.mark.gpu
 def test_cuda_ops_world1():
     """One rank: the all-reduce is the identity for every op and dtype; the
