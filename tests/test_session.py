@@ -268,6 +268,103 @@ def test_session_device_streamed(strategy, size, piece_kb, kind, batch_fold):
              "KUNGFU_AMD_BATCH_FOLD": batch_fold, "KUNGFU_AMD_STREAM_TIMEOUT_MS": "20000"})
 
 
+_DT_ITEM = {"f16": 2, "bf16": 2, "f64": 8, "i8": 1, "u8": 1, "i16": 2, "u16": 2, "i64": 8,
+            "u32": 4, "u64": 8}
+
+
+def _dt_inputs(rank, dt, n):
+    from oracle import oracle
+    rng = np.random.default_rng(700 + rank)
+    if dt == "bf16":
+        return oracle.f32_to_bf16_bits(rng.standard_normal(n).astype(np.float32))
+    if dt in ("f16", "f64"):
+        return rng.standard_normal(n).astype(oracle.NP[dt])
+    info = np.iinfo(oracle.NP[dt])
+    return rng.integers(info.min, info.max, n, endpoint=True, dtype=oracle.NP[dt])
+
+
+def _dt_to_dev(a, dt):
+    import torch
+    if dt == "bf16":
+        return torch.from_numpy(a.view(np.int16)).view(torch.bfloat16).to("cuda:0")
+    if dt in ("u16", "u32", "u64"):
+        signed = {"u16": np.int16, "u32": np.int32, "u64": np.int64}[dt]
+        tdt = getattr(torch, {"u16": "uint16", "u32": "uint32", "u64": "uint64"}[dt])
+        return torch.from_numpy(a.view(signed)).view(tdt).to("cuda:0")
+    return torch.from_numpy(a).to("cuda:0")
+
+
+def _dt_to_np(t, dt):
+    import torch
+    if dt in ("bf16", "u16"):
+        return t.cpu().view(torch.int16).numpy().view(np.uint16)
+    if dt in ("u32", "u64"):
+        signed = {"u32": torch.int32, "u64": torch.int64}[dt]
+        return t.cpu().view(signed).numpy().view({"u32": np.uint32, "u64": np.uint64}[dt])
+    return t.cpu().numpy()
+
+
+def _dtype_body(rank, size, sock_dir, dt, n, errq, env):
+    sys.path[:0] = [ROOT, HERE]
+    os.environ.update(env)
+    try:
+        from kungfu_amd.session import Session
+        x = _dt_to_dev(_dt_inputs(rank, dt, n), dt)
+        y = x.clone().zero_()
+        s = Session(rank, size, sock_dir, mode="device")
+        s.all_reduce(x, y, "dt/%s" % dt)
+        z = x.clone()
+        s.all_reduce(z, z, "dt/%s/inplace" % dt)
+        s.close()
+        np.save(os.path.join(sock_dir, "got%d.npy" % rank), _dt_to_np(y, dt))
+        np.save(os.path.join(sock_dir, "inplace%d.npy" % rank), _dt_to_np(z, dt))
+    except Exception:
+        errq.put("rank %d: %s" % (rank, traceback.format_exc()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stages", ["fold", pytest.param("1", marks=pytest.mark.gpu_slow)])
+@pytest.mark.parametrize("dt", ["f16", "bf16", "f64", "i8", "u8", "i16", "u16", "i64", "u64"])
+def test_session_device_dtypes(dt, stages):
+    """Every dtype the streamed fold supports (kf_stream.hip fold_kernel<T>,
+    the dtype's own arithmetic: kf_reduce_kernels.hpp Elt<T>) through a
+    device-mode session: np = 3 under RING, whose accumulation order is fixed,
+    2.5 MiB + 3 elements per rank (three chunks, a ragged one), out of place
+    and in place, each chunk equal bit for bit to the schedule oracle
+    (oracle/schedule.py over the oracle's own two-input fold, pinned by the
+    reference's compiled std_transform_2). bf16 has no reference (parity
+    unpinned: the build's fp32-accumulate-then-round per hop)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    if dt in ("u16", "u64") and not hasattr(torch, {"u16": "uint16", "u64": "uint64"}[dt]):
+        pytest.skip("torch has no %s" % dt)
+    from oracle import schedule
+    size = 3
+    n = (5 << 19) // _DT_ITEM[dt] + 3
+    env = {"KUNGFU_ALLREDUCE_STRATEGY": "RING", "KUNGFU_AMD_STREAM": stages}
+    ctx = mp.get_context("spawn")
+    errq = ctx.SimpleQueue()
+    with tempfile.TemporaryDirectory() as d:
+        ps = [ctx.Process(target=_dtype_body, args=(r, size, d, dt, n, errq, env))
+              for r in range(size)]
+        for p in ps:
+            p.start()
+        hung = join_all(ps, 180)
+        errs = []
+        while not errq.empty():
+            errs.append(errq.get())
+        assert not errs, "\n".join(errs)
+        assert not hung and all(p.exitcode == 0 for p in ps), hung_msg(hung, [p.exitcode for p in ps])
+        gots = [(np.load(os.path.join(d, "got%d.npy" % r)),
+                 np.load(os.path.join(d, "inplace%d.npy" % r))) for r in range(size)]
+    xs = [_dt_inputs(r, dt, n) for r in range(size)]
+    for name, which in (("dt/%s" % dt, 0), ("dt/%s/inplace" % dt, 1)):
+        want = schedule.all_reduce(xs, dt, "sum", strategy="RING", name=name)[0]
+        for r in range(size):
+            assert np.array_equal(gots[r][which], want), (dt, name, r)
+
+
 @pytest.mark.gpu
 def test_session_device_streamed_stress():
     """the streamed kernels write page-locked memory the
