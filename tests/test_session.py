@@ -268,8 +268,8 @@ def test_session_device_streamed(strategy, size, piece_kb, kind, batch_fold):
              "KUNGFU_AMD_BATCH_FOLD": batch_fold, "KUNGFU_AMD_STREAM_TIMEOUT_MS": "20000"})
 
 
-_DT_ITEM = {"f16": 2, "bf16": 2, "f64": 8, "i8": 1, "u8": 1, "i16": 2, "u16": 2, "i64": 8,
-            "u32": 4, "u64": 8}
+_DT_ITEM = {"f16": 2, "bf16": 2, "f32": 4, "f64": 8, "i8": 1, "u8": 1, "i16": 2, "u16": 2,
+            "i32": 4, "i64": 8, "u32": 4, "u64": 8}
 
 
 def _dt_inputs(rank, dt, n):
@@ -277,7 +277,7 @@ def _dt_inputs(rank, dt, n):
     rng = np.random.default_rng(700 + rank)
     if dt == "bf16":
         return oracle.f32_to_bf16_bits(rng.standard_normal(n).astype(np.float32))
-    if dt in ("f16", "f64"):
+    if dt in ("f16", "f32", "f64"):
         return rng.standard_normal(n).astype(oracle.NP[dt])
     info = np.iinfo(oracle.NP[dt])
     return rng.integers(info.min, info.max, n, endpoint=True, dtype=oracle.NP[dt])
@@ -304,22 +304,55 @@ def _dt_to_np(t, dt):
     return t.cpu().numpy()
 
 
-def _dtype_body(rank, size, sock_dir, dt, n, errq, env):
+def _dtype_body(rank, size, sock_dir, dt, n, errq, env, op="sum", mode="device"):
     sys.path[:0] = [ROOT, HERE]
     os.environ.update(env)
     try:
         from kungfu_amd.session import Session
-        x = _dt_to_dev(_dt_inputs(rank, dt, n), dt)
-        y = x.clone().zero_()
-        s = Session(rank, size, sock_dir, mode="device")
-        s.all_reduce(x, y, "dt/%s" % dt)
-        z = x.clone()
-        s.all_reduce(z, z, "dt/%s/inplace" % dt)
+        if mode == "device":
+            x = _dt_to_dev(_dt_inputs(rank, dt, n), dt)
+            y = x.clone().zero_()
+            s = Session(rank, size, sock_dir, mode="device")
+        else:
+            x = _dt_inputs(rank, dt, n)
+            y = np.zeros_like(x)
+            s = Session(rank, size, sock_dir, mode="host", host_reduce_fn=oracle_reduce_fn())
+        s.all_reduce(x, y, "dt/%s" % dt, op=op)
+        z = x.clone() if mode == "device" else x.copy()
+        s.all_reduce(z, z, "dt/%s/inplace" % dt, op=op)
         s.close()
-        np.save(os.path.join(sock_dir, "got%d.npy" % rank), _dt_to_np(y, dt))
-        np.save(os.path.join(sock_dir, "inplace%d.npy" % rank), _dt_to_np(z, dt))
+        conv = (lambda t: _dt_to_np(t, dt)) if mode == "device" else (lambda a: a)
+        np.save(os.path.join(sock_dir, "got%d.npy" % rank), conv(y))
+        np.save(os.path.join(sock_dir, "inplace%d.npy" % rank), conv(z))
     except Exception:
         errq.put("rank %d: %s" % (rank, traceback.format_exc()))
+
+
+def _run_dtype(dt, n, env, op="sum", mode="device", size=3):
+    """np = `size` peers under RING (fixed accumulation order); every rank's
+    out-of-place and in-place results against the schedule oracle."""
+    from oracle import schedule
+    ctx = mp.get_context("spawn")
+    errq = ctx.SimpleQueue()
+    env = dict(env, KUNGFU_ALLREDUCE_STRATEGY="RING")
+    with tempfile.TemporaryDirectory() as d:
+        ps = [ctx.Process(target=_dtype_body, args=(r, size, d, dt, n, errq, env, op, mode))
+              for r in range(size)]
+        for p in ps:
+            p.start()
+        hung = join_all(ps, 180)
+        errs = []
+        while not errq.empty():
+            errs.append(errq.get())
+        assert not errs, "\n".join(errs)
+        assert not hung and all(p.exitcode == 0 for p in ps), hung_msg(hung, [p.exitcode for p in ps])
+        gots = [(np.load(os.path.join(d, "got%d.npy" % r)),
+                 np.load(os.path.join(d, "inplace%d.npy" % r))) for r in range(size)]
+    xs = [_dt_inputs(r, dt, n) for r in range(size)]
+    for name, which in (("dt/%s" % dt, 0), ("dt/%s/inplace" % dt, 1)):
+        want = schedule.all_reduce(xs, dt, op, strategy="RING", name=name)[0]
+        for r in range(size):
+            assert np.array_equal(gots[r][which], want), (dt, op, name, r)
 
 
 @pytest.mark.gpu
@@ -339,30 +372,34 @@ def test_session_device_dtypes(dt, stages):
         pytest.skip("no GPU")
     if dt in ("u16", "u64") and not hasattr(torch, {"u16": "uint16", "u64": "uint64"}[dt]):
         pytest.skip("torch has no %s" % dt)
-    from oracle import schedule
-    size = 3
-    n = (5 << 19) // _DT_ITEM[dt] + 3
-    env = {"KUNGFU_ALLREDUCE_STRATEGY": "RING", "KUNGFU_AMD_STREAM": stages}
-    ctx = mp.get_context("spawn")
-    errq = ctx.SimpleQueue()
-    with tempfile.TemporaryDirectory() as d:
-        ps = [ctx.Process(target=_dtype_body, args=(r, size, d, dt, n, errq, env))
-              for r in range(size)]
-        for p in ps:
-            p.start()
-        hung = join_all(ps, 180)
-        errs = []
-        while not errq.empty():
-            errs.append(errq.get())
-        assert not errs, "\n".join(errs)
-        assert not hung and all(p.exitcode == 0 for p in ps), hung_msg(hung, [p.exitcode for p in ps])
-        gots = [(np.load(os.path.join(d, "got%d.npy" % r)),
-                 np.load(os.path.join(d, "inplace%d.npy" % r))) for r in range(size)]
-    xs = [_dt_inputs(r, dt, n) for r in range(size)]
-    for name, which in (("dt/%s" % dt, 0), ("dt/%s/inplace" % dt, 1)):
-        want = schedule.all_reduce(xs, dt, "sum", strategy="RING", name=name)[0]
-        for r in range(size):
-            assert np.array_equal(gots[r][which], want), (dt, name, r)
+    _run_dtype(dt, (5 << 19) // _DT_ITEM[dt] + 3, {"KUNGFU_AMD_STREAM": stages})
+
+
+_OP_CASES = [("f32", "min"), ("f32", "max"), ("f32", "prod"), ("i32", "min"), ("i32", "max"),
+             ("i32", "prod"), ("f64", "max"), ("i8", "prod"), ("u16", "min")]
+
+
+@pytest.mark.parametrize("dt,op", _OP_CASES)
+def test_session_host_ops(dt, op):
+    """MIN / MAX / PROD through the session engine (KungFu_Op reaches every
+    fold; the reference's call_as<T>, op.cpp:22-43, via the oracle's fold as
+    the host callback): np = 3 RING, three chunks, out of place and in place,
+    against the schedule oracle."""
+    _run_dtype(dt, (5 << 19) // _DT_ITEM[dt] + 3, {}, op=op, mode="host")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt,op", _OP_CASES)
+def test_session_device_ops(dt, op):
+    """The same through device-mode sessions: non-SUM ops take the
+    whole-chunk HIP fold (the streamed fold is SUM only), bit-exact vs the
+    schedule oracle (MIN / MAX select an input, so no rounding question)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    if dt == "u16" and not hasattr(torch, "uint16"):
+        pytest.skip("torch has no uint16")
+    _run_dtype(dt, (5 << 19) // _DT_ITEM[dt] + 3, {}, op=op, mode="device")
 
 
 @pytest.mark.gpu
