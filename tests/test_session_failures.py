@@ -325,3 +325,36 @@ def test_op_timeout_rejects_bad_values(monkeypatch):
     monkeypatch.setenv("KUNGFU_AMD_OP_TIMEOUT_S", "0")
     with tempfile.TemporaryDirectory() as d:
         Session(0, 1, d, mode="host").close()
+
+
+def test_host_async_calls_bounded_by_op_timeout(monkeypatch):
+    """The async worker's poll loop (kf_session_all_reduce_async) honours
+    KUNGFU_AMD_OP_TIMEOUT_S per call: three calls in flight at once on a peer
+    that never sends all fail with KF_ERR_TIMEOUT, each done callback runs,
+    and wait_all reports the failure within the deadline."""
+    from kungfu_amd import _lib
+    from kungfu_amd.session import Session
+    from test_session import oracle_reduce_fn
+    lib = _lib.load()
+    monkeypatch.setenv("KUNGFU_ALLREDUCE_STRATEGY", "STAR")
+    monkeypatch.setenv("KUNGFU_AMD_OP_TIMEOUT_S", "2")
+    with tempfile.TemporaryDirectory() as d:
+        fake = FakePeer(lib, d, 1, lambda rx, tx: _drain(rx, 6))
+        fake.start()
+        s = Session(0, 2, d, mode="host", host_reduce_fn=oracle_reduce_fn())
+        xs = [np.ones(n, np.float32) for n in (5, NF, 3 * NF)]
+        got = []
+        t0 = time.monotonic()
+        hs = [s.all_reduce_async(x, np.zeros_like(x), "async/%d" % i,
+                                 callback=lambda st: got.append(st))
+              for i, x in enumerate(xs)]
+        with pytest.raises(RuntimeError) as ei:
+            s.wait_all()
+        dt = time.monotonic() - t0
+        s.close()
+        fake.join(15)
+        fake.close()
+        assert fake.err is None, fake.err
+    assert 1.5 < dt < 8, (dt, str(ei.value))
+    assert len(got) == 3 and all(st == 8 for st in got), got  # KF_ERR_TIMEOUT
+    assert all(h.done() for h in hs)
