@@ -406,7 +406,11 @@ def exchange_phase2(lib, dev, g, world=8):
         nsets = max(2, -(-(768 << 20) // per_set))
         sets = []
         for _ in range(nsets):
-            bs = [torch.randn(c, device=dev, generator=g) for c in counts]
+            # the buckets back to back in ONE flat buffer, as GradBuckets lays
+            # them out for the exchange: one shard every bucket's length
+            flat = torch.randn(sum(counts), device=dev, generator=g)
+            offs = [sum(counts[:i]) for i in range(len(counts))]
+            bs = [flat[o:o + c] for o, c in zip(offs, counts)]
             shard = [b[q * 3:q * 4] for b, q in zip(bs, qs)]  # rank 3's shard
             ptrs = _lib.ptr_array([s.data_ptr() for s in shard])
             sets.append((ptrs, (ctypes.c_size_t * len(qs))(*qs), bs, shard))

@@ -358,15 +358,16 @@ int check_args(const void *const *inputs, int k, const void *out, size_t n)
 // ---------------------------------------------------------------------------
 // tile shape of the batched launch (tools/ab_batch_shape.py builds variants;
 // profiles/r03/ab_batch_shape.jsonl). k = 1 (the shard /np after a
-// reduce-scatter) takes two vectors per lane while the whole grid is resident
-// at once (256-thread blocks, eight per CU): its launches are small and
+// reduce-scatter) takes two vectors per lane: its launches are small and
 // latency-bound, and twice the blocks for the same bytes finish sooner (C4's
-// 16 shards at N = 8: 8.4 -> 7.0 us; C3's 64: 16.2 -> 15.8 us). Past one
-// resident wave of blocks it takes four, so every block starts at once
-// (tools/explore/shard_probe.hip, profiles/r05/shard_probe_r05{g,h}.jsonl:
-// C3's 64 shards 14.5 -> 13.5-13.8 us; C4's 16 stay at two, 6.1 us against
-// 7.1-7.3 at four). k >= 2 keeps four (k = 2 16 x 4 MiB, the k = 8 fold of C5:
-// equal within 1 %, one lane per vector up to 6 % slower).
+// 16 shards at N = 8: 8.4 -> 7.0 us; C3's 64: 16.2 -> 15.8 us). Four per lane
+// once the grid outgrows one resident wave looked better on shards allocated
+// one by one (C3 14.3 -> 13.4 us, shard_probe.hip), but the exchange's shards
+// are slices of ONE flat buffer of buckets, one shard every bucket's length;
+// there four per lane is 30 % slower (C3 15.2 -> 19.8 us,
+// tools/explore/shard_xcd_probe.hip, profiles/r05/shard_xcd_probe_r05ae.jsonl),
+// so k = 1 stays at two. k >= 2 keeps four (k = 2 16 x 4 MiB, the k = 8 fold
+// of C5: equal within 1 %, one lane per vector up to 6 % slower).
 #ifndef KF_BATCH_UNROLL
 #define KF_BATCH_UNROLL 4
 #endif
@@ -445,38 +446,12 @@ int launch_batch_kc(const void *const *in, int k, void *const *outs, const size_
     return flush();
 }
 
-// blocks of 256 threads the device holds at once (eight per CU)
-size_t resident_blocks()
-{
-    static const size_t n = [] {
-        int dev = 0, cus = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            cus <= 0) {
-            cus = 256;  // MI355X
-        }
-        return static_cast<size_t>(cus) * (2048 / KF_BATCH_BLOCK);
-    }();
-    return n;
-}
-
 template <typename T, int OP, int EPI>
 int launch_batch(const void *const *in, int k, void *const *outs, const size_t *counts, int nb,
                  int npi, hipStream_t s)
 {
     const Div np = make_div(npi);
-    if (k == 1) {
-        using S          = typename Elt<T>::S;
-        const size_t per = static_cast<size_t>(KF_BATCH_BLOCK) * KF_BATCH_UNROLL_K1 * 16;
-        size_t blocks    = 0;  // the plan's block count at two vectors per lane
-        for (int b = 0; b < nb; ++b) blocks += (counts[b] * sizeof(S) + per - 1) / per;
-        if (blocks > resident_blocks()) {
-            return launch_batch_kc<T, OP, EPI, 1, 2 * KF_BATCH_UNROLL_K1>(in, k, outs, counts, nb,
-                                                                           np, npi, s);
-        }
-        return launch_batch_kc<T, OP, EPI, 1, KF_BATCH_UNROLL_K1>(in, k, outs, counts, nb, np,
-                                                                  npi, s);
-    }
+    if (k == 1) return launch_batch_kc<T, OP, EPI, 1, KF_BATCH_UNROLL_K1>(in, k, outs, counts, nb, np, npi, s);
     if (k == 2) return launch_batch_kc<T, OP, EPI, 2, KF_BATCH_UNROLL>(in, k, outs, counts, nb, np, npi, s);
     return launch_batch_kc<T, OP, EPI, 0, KF_BATCH_UNROLL>(in, k, outs, counts, nb, np, npi, s);
 }
