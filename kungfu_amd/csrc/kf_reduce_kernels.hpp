@@ -602,9 +602,22 @@ __global__ void __launch_bounds__(BLOCK) reduce_batch_kernel(BatchArgsT<NSEG, NP
     // b is searched in the kernarg table, one dependent scalar load per step,
     // which cost 0.4-1.5 us of a ~6 us launch (tools/explore/shard_probe.hip,
     // profiles/r05/shard_probe_r05k.jsonl).
+    // With a multiple of 8 rows, the blocks are handed out XCD by XCD:
+    // workgroups go to the 8 XCDs round-robin in dispatch order, so linear
+    // block L runs on XCD L % 8, and that XCD's j-th block takes bucket
+    // (L % 8) + 8 * (j / per). Each XCD then sweeps an eighth of the buckets
+    // instead of a slice of every one. It pays with many buckets: C3's 64
+    // shards of a flat bucket buffer at N = 8, 15.3 -> 14.2 us in the probe,
+    // 14.6 -> 13.8 us in bench.py; with C4's 16 it lost 0.1-0.4 us, so it
+    // starts at 32 rows (tools/explore/shard_xcd_probe.hip,
+    // profiles/r05/shard_xcd_probe_r05ah.jsonl, phase2_graph_xcd_r05ai.json).
     const bool rows   = gridDim.y > 1;
-    const unsigned b  = blockIdx.x;
-    const int s       = rows ? static_cast<int>(blockIdx.y) : batch_segment(a, b);
+    const bool by_xcd = rows && gridDim.y >= 32 && (gridDim.y & 7u) == 0;
+    const unsigned L  = blockIdx.y * gridDim.x + blockIdx.x;
+    const unsigned b  = by_xcd ? (L >> 3) % gridDim.x : blockIdx.x;
+    const int s       = by_xcd ? static_cast<int>((L & 7u) + 8u * ((L >> 3) / gridDim.x))
+                        : rows ? static_cast<int>(blockIdx.y)
+                               : batch_segment(a, b);
     const unsigned b0 = rows ? 0u : a.blk0[s];
     const size_t nblk = rows ? gridDim.x : a.blk0[s + 1] - a.blk0[s];
     InPtrs one;  // NPTR == 1: the bucket's single input (only p[0] is read, KC == 1)

@@ -82,6 +82,58 @@ __global__ void __launch_bounds__(B) xcd_kernel(Segs a)
 }
 
 template <typename Launch>
+double time_us(Launch launch, int nsets);
+
+// the same map on the product's 2-D grid (per x nseg): the dispatch order is
+// linear (x fastest), so the linear id picks the XCD
+template <int U>
+__global__ void __launch_bounds__(B) xcd2d_kernel(Segs a)
+{
+    const unsigned L   = blockIdx.y * gridDim.x + blockIdx.x;
+    const unsigned xcd = L & 7;
+    const unsigned j   = L >> 3;
+    const unsigned s   = xcd + 8 * (j / gridDim.x);
+    const unsigned t   = j % gridDim.x;
+    tile<U>(a.p[s], a.nvec, t);
+}
+
+// C4 at N = 8: 16 buckets of 1,598,976 floats back to back in one flat
+// buffer, rank 3's shard of each (199,872 floats)
+void c4_flat()
+{
+    const int nb = 16;
+    const size_t c = 1598976, q = c / 8;
+    const unsigned nvec = static_cast<unsigned>(q / 4);
+    const double bytes  = 2.0 * nb * q * 4;
+    const int nsets = 8;
+    std::vector<Segs> segs(nsets);
+    std::vector<void *> allocs;
+    for (int i = 0; i < nsets; ++i) {
+        char *base = nullptr;
+        CHECK(hipMalloc(&base, nb * c * 4));
+        CHECK(hipMemset(base, 0x3f, nb * c * 4));
+        allocs.push_back(base);
+        segs[i].nseg = nb;
+        segs[i].nvec = nvec;
+        segs[i].per  = (nvec + B * 2 - 1) / (B * 2);
+        for (int s = 0; s < nb; ++s)
+            segs[i].p[s] = reinterpret_cast<f32x4 *>(base + s * c * 4 + 3 * q * 4);
+    }
+    const unsigned per = segs[0].per;
+    for (int map = 0; map < 2; ++map) {
+        auto launch = [&](int i) {
+            if (map == 0) rows_kernel<2><<<dim3(per, nb), B>>>(segs[i]);
+            else xcd2d_kernel<2><<<dim3(per, nb), B>>>(segs[i]);
+        };
+        const double us = time_us(launch, nsets);
+        printf("{\"layout\": \"c4 flat\", \"map\": \"%s\", \"unroll\": 2, \"us\": %.2f, "
+               "\"frac\": %.4f}\n", map ? "xcd 2-D" : "rows", us, bytes / us / 1e3 / 8000.0);
+        fflush(stdout);
+    }
+    for (auto p : allocs) CHECK(hipFree(p));
+}
+
+template <typename Launch>
 double time_us(Launch launch, int nsets)
 {
     hipEvent_t e0, e1;
@@ -135,10 +187,13 @@ int main()
             const int U          = u == 0 ? 2 : 4;
             const unsigned per   = (nvec + B * U - 1) / (B * U);
             for (auto &a : segs) a.per = per;
-            for (int map = 0; map < 4; ++map) {
+            for (int map = 0; map < 5; ++map) {
                 const unsigned step = map == 2 ? 1u : (per / 8 ? per / 8 : 1u) * 3 + 1;
                 auto launch = [&](int i) {
-                    if (map >= 2) {
+                    if (map == 4) {
+                        if (U == 2) xcd2d_kernel<2><<<dim3(per, kSeg), B>>>(segs[i]);
+                        else xcd2d_kernel<4><<<dim3(per, kSeg), B>>>(segs[i]);
+                    } else if (map >= 2) {
                         if (U == 2) rows_rot_kernel<2><<<dim3(per, kSeg), B>>>(segs[i], step);
                         else rows_rot_kernel<4><<<dim3(per, kSeg), B>>>(segs[i], step);
                     } else if (map == 0) {
@@ -153,7 +208,7 @@ int main()
                 printf("{\"layout\": \"%s\", \"map\": \"%s\", \"unroll\": %d, \"us\": %.2f, "
                        "\"frac\": %.4f}\n",
                        layout ? "strided" : "packed",
-                       map == 0 ? "rows" : map == 1 ? "xcd" : map == 2 ? "rows rot 1" : "rows rot 3p/8+1",
+                       map == 0 ? "rows" : map == 1 ? "xcd" : map == 2 ? "rows rot 1" : map == 3 ? "rows rot 3p/8+1" : "xcd 2-D",
                        U, us,
                        bytes / us / 1e3 / 8000.0);
                 fflush(stdout);
@@ -179,5 +234,6 @@ int main()
         }
         for (auto p : allocs) CHECK(hipFree(p));
     }
+    c4_flat();
     return 0;
 }
