@@ -186,6 +186,14 @@ unsigned grid_for(size_t nvec, size_t nedge, int unroll, int cap = 0)
 // wins (64 MiB: 92.2 vs 96.3 us), and from 8192 blocks (128 MiB) the
 // residency cap adds to it (256 MiB: 382 vs 391 us uncapped, 405 batched).
 constexpr unsigned kSerialMinBlocks = 2048;
+// the batched launch's own threshold (tools/ab_batch_shape.py builds variants).
+// At 256, 1024 or 2048 blocks, C5's a2a fold (~1670 blocks) and the
+// 16 x 4 MiB k = 2 batch time within 0.5 % of each other
+// (profiles/r05/ab_batch_serial_r05an.jsonl), so it stays at the fold's 2048
+#ifndef KF_BATCH_SERIAL_MIN_BLOCKS
+#define KF_BATCH_SERIAL_MIN_BLOCKS 2048
+#endif
+constexpr unsigned kBatchSerialMinBlocks = KF_BATCH_SERIAL_MIN_BLOCKS;
 constexpr unsigned kCapMinBlocks    = 8192;
 
 // dynamic LDS of an HBM streaming launch of `blocks` blocks over k inputs
@@ -394,7 +402,7 @@ int launch_batch_kc(const void *const *in, int k, void *const *outs, const size_
     auto flush      = [&]() -> int {
         if (a.nseg == 0) return KF_OK;
         a.blk0[a.nseg] = static_cast<unsigned>(blocks);
-        a.serial       = KC == 0 && blocks >= kSerialMinBlocks ? 1 : 0;
+        a.serial       = KC == 0 && blocks >= kBatchSerialMinBlocks ? 1 : 0;
         // equal block counts: one grid row per bucket (the kernel reads the
         // bucket off blockIdx.y instead of searching blk0)
         const dim3 grid = per && a.nseg > 1

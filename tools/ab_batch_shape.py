@@ -26,6 +26,15 @@ OUT = os.path.join(ROOT, "tools", "ab_lib")
 # variant name -> compile-time flags (kf_capi.hip / kf_reduce_kernels.hpp)
 VARIANTS = {"u%d_b%d" % (u, b): {"KF_BATCH_UNROLL": u, "KF_BATCH_UNROLL_K1": u, "KF_BATCH_BLOCK": b}
             for u, b in [(4, 256), (2, 256), (1, 256), (2, 512), (1, 512), (1, 1024)]}
+# round 5: the k >= 3 batched fold's one-in-flight threshold (blocks per
+# launch, KF_BATCH_SERIAL_MIN_BLOCKS; C5's a2a fold is ~1670 blocks at four
+# vectors per lane, so it runs four-together by default) and two vectors per
+# lane, where the same bytes make ~3340 blocks and the schedule turns on
+#   AB_SET=serial python tools/ab_batch_shape.py build|run
+if os.environ.get("AB_SET") == "serial":
+    VARIANTS = {"u%d_s%d" % (u, t): {"KF_BATCH_UNROLL": u, "KF_BATCH_SERIAL_MIN_BLOCKS": t}
+                for u, t in [(4, 2048), (4, 1024), (4, 256), (2, 2048), (2, 1 << 30), (8, 1 << 30)]}
+CASES = os.environ.get("AB_CASES")  # comma list; all when unset
 # (round 3 also built a KF_FOLD_ALLIN variant of the runtime-k fold here —
 # every input's vectors in flight before the first add on resident grids —
 # equal within noise at every shape, profiles/r03/ab_fold_allin_r03u.jsonl;
@@ -149,6 +158,8 @@ def run():
                                                                      n, F32, SUM, sp),
             (k + 1) * n * 4, lambda i, fs=fs: fs[i][1].clone(), None)
 
+    if CASES:
+        cases = {c: v for c, v in cases.items() if c in CASES.split(",")}
     # bits: every variant equals the shipped library on set 0
     ok = {}
     for name, (ns, launch, _, snap, restore) in cases.items():
