@@ -34,6 +34,10 @@ VARIANTS = {"u%d_b%d" % (u, b): {"KF_BATCH_UNROLL": u, "KF_BATCH_UNROLL_K1": u, 
 if os.environ.get("AB_SET") == "serial":
     VARIANTS = {"u%d_s%d" % (u, t): {"KF_BATCH_UNROLL": u, "KF_BATCH_SERIAL_MIN_BLOCKS": t}
                 for u, t in [(4, 2048), (4, 1024), (4, 256), (2, 2048), (2, 1 << 30), (8, 1 << 30)]}
+# (round 5 also timed 1-D batched launches with the blocks handed out XCD by
+# XCD, each XCD a contiguous eighth, through a temporary KF_BATCH_XCD1D
+# variant: C5's fold 42.04 vs 41.93 us, profiles/r05/ab_batch_xcd1d_r05ao.jsonl;
+# not kept)
 CASES = os.environ.get("AB_CASES")  # comma list; all when unset
 # (round 3 also built a KF_FOLD_ALLIN variant of the runtime-k fold here —
 # every input's vectors in flight before the first add on resident grids —
