@@ -18,7 +18,7 @@ import traceback
 
 import numpy as np
 import pytest
-from procs import hung_msg, join_all
+from procs import join_all
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
