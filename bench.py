@@ -117,6 +117,13 @@ def parse():
     ap.add_argument("--p2p-child", default="", help=argparse.SUPPRESS)
     ap.add_argument("--p2p-out", default="", help=argparse.SUPPRESS)
     ap.add_argument("--p2p-timeout", type=float, default=150.0, help=argparse.SUPPRESS)
+    ap.add_argument("--test-transport", default="none", choices=["none", "ipc"],
+                    help="testing: with --dist-backend gloo and every rank on one GPU, run "
+                         "the native exchange (primary, sub-benchmarks, c4_named) over the "
+                         "TEST-ONLY cross-process IPC transport of tests/c/libkf_testing.so "
+                         "instead of falling back to torch.distributed (RCCL refuses two "
+                         "ranks per GPU); the line says exchange_kind 'native (test "
+                         "transport)' and its rates are not xGMI rates")
     ap.add_argument("--rehearse-exchange", action="store_true",
                     help="testing: run the N > 1 branch (native exchange over RCCL, "
                          "sub-benchmarks, line) with a single rank")
@@ -339,14 +346,16 @@ def exchange_phase2(lib, dev, g, world=8):
             for _ in range(5):
                 ev0.record(cap)
                 for i in range(4 * nsets):
-                    launch(i % nsets)
+                    _lib.check(launch(i % nsets), "launch")
                 ev1.record(cap)
                 torch.cuda.synchronize()
                 eager.append(ev0.elapsed_time(ev1) * 1e3 / (4 * nsets))
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph, stream=cap):
             for i in range(4 * nsets):
-                launch(i % nsets)
+                # a launch refused during capture would leave the graph short
+                # and its replay fast for nothing: fail instead
+                _lib.check(launch(i % nsets), "launch during capture")
         torch.cuda.synchronize()
         ts = []
         with torch.cuda.stream(cap):
@@ -583,6 +592,27 @@ def chunk_latency(lib, x, reps=2000, chunk_bytes=1 << 20):
     ok = bool(torch.equal(zh, xh + yh))
     xa, ya = xh.numpy().copy(), yh.numpy().copy()
     za = np.empty_like(xa)
+    # the same chunk in ordinary (malloc'd) host memory page-locked through
+    # kf_host_register, as a Go host would register its receive pool
+    # (byte_slice_pool.go:28-60): the library finds it in its registry
+    # instead of asking HIP for six pointer attributes per call
+    rx, ry, rz = (np.empty(n + 1024, np.float32) for _ in range(3))
+    off = lambda a: (-a.ctypes.data % 4096) // 4  # noqa: E731  page-aligned views
+    rx, ry, rz = (a[off(a):off(a) + n] for a in (rx, ry, rz))
+    rx[:], ry[:] = xa, ya
+    regd = [a for a in (rx, ry, rz) if lib.kf_host_register(a.ctypes.data, a.nbytes) == 0]
+    reg_us = None
+    if len(regd) == 3:
+        rargs = (rx.ctypes.data, ry.ctypes.data, rz.ctypes.data, n, KF_FLOAT, KF_SUM)
+        for _ in range(5):
+            lib.std_transform_2(*rargs)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            lib.std_transform_2(*rargs)
+        reg_us = (time.perf_counter() - t0) / reps * 1e6
+        ok = ok and bool(np.array_equal(rz, rx + ry))
+    for a in regd:
+        lib.kf_host_unregister(a.ctypes.data)
     ref = oracle.ref_transform2_addr()
     if ref is not None:
         run = lambda r: oracle.bench_ref(ref, xa, ya, za, "f32", "sum", r)  # noqa: E731
@@ -590,7 +620,9 @@ def chunk_latency(lib, x, reps=2000, chunk_bytes=1 << 20):
         run = lambda r: oracle.bench_transform2(xa, ya, za, "f32", "sum", r)  # noqa: E731
     run(5)
     cpu_s = run(reps) / reps
-    return {"gpu_pinned_us": round(gpu_s * 1e6, 2), "cpu_us": round(cpu_s * 1e6, 2),
+    return {"gpu_pinned_us": round(gpu_s * 1e6, 2),
+            "gpu_registered_us": None if reg_us is None else round(reg_us, 2),
+            "cpu_us": round(cpu_s * 1e6, 2),
             "cpu_kind": "reference" if ref is not None else "port",
             "correct": ok, "reps": reps}
 
@@ -604,6 +636,8 @@ def chunk_sweep(lib, x):
         r = chunk_latency(lib, x, reps=reps, chunk_bytes=kib << 10)
         r["chunk_KiB"] = kib
         r["gpu_over_cpu"] = round(r["cpu_us"] / r["gpu_pinned_us"], 3)
+        if r["gpu_registered_us"]:
+            r["gpu_registered_over_cpu"] = round(r["cpu_us"] / r["gpu_registered_us"], 3)
         out.append(r)
     return out
 
@@ -860,6 +894,7 @@ def launch_ranks(args):
 
 def main():
     args = parse()
+    _OPTS["test_transport"] = args.test_transport
     if args.c1_child:
         return c1_child(args)
     if args.config == "c1":
@@ -1024,6 +1059,7 @@ def main():
             "frac_of_xgmi": _xgmi_frac(busbw, world),
             "buckets": args.buckets,
             "exchange": how,
+            "correct": bool(ok),
         }
         if phase_us is not None:
             out["collective"]["phase_us"] = phase_us
@@ -1295,6 +1331,7 @@ def _fill(gb, rank_seed, dev, dtype):
 
 
 _NATIVE = {}  # the primary's NativeExchange, reused by the sub-benchmarks
+_OPTS = {"test_transport": "none"}  # --test-transport, for the helpers below
 
 # The peer-to-peer sub-benchmarks map every peer's buckets and signal words
 # over xGMI (HIP IPC) and spin on device barriers: the one part of the line
@@ -1323,6 +1360,8 @@ def _named_in_child(world, rank, dev, steps):
     name negotiation's first over RCCL (a split-off control communicator and
     a negotiation thread), so it is isolated like the P2P paths — a hang or
     fault there ends the child, not the line."""
+    if "ex" not in _NATIVE and _OPTS.get("test_transport") == "ipc":
+        _NATIVE["ex"] = _ipc_exchange(rank, world, dev, "auto")
     if "ex" not in _NATIVE:
         if dist.get_backend() != "nccl":
             raise RuntimeError("the name-keyed path needs the native exchange (nccl backend)")
@@ -1349,7 +1388,7 @@ def p2p_extras(args, rank, world, local_rank, dev, keys, seconds):
     cmd = [sys.executable, os.path.abspath(__file__), "--p2p-child", ",".join(keys),
            "--p2p-out", path, "--p2p-timeout", str(seconds - 10.0),
            "--elems", str(args.elems), "--steps", str(min(args.steps, 50)),
-           "--dist-backend", args.dist_backend]
+           "--dist-backend", args.dist_backend, "--test-transport", args.test_transport]
     if args.device_index is not None:
         cmd += ["--device-index", str(args.device_index)]
     t0 = time.perf_counter()
@@ -1406,6 +1445,7 @@ def p2p_child(args):
     world = int(os.environ["WORLD_SIZE"])
     rank = int(os.environ["RANK"])
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    _OPTS["test_transport"] = args.test_transport
 
     def give_up():
         print("[bench] p2p child rank %d: not done within %.0f s" % (rank, args.p2p_timeout),
@@ -1462,6 +1502,13 @@ def _primary_exchange(args, rank, world, dev):
     not the whole line. The id is shared on this thread (a torch collective)."""
     from kungfu_amd.collective import Exchange
     how_torch = "torch.distributed RCCL RS -> HIP /np -> AG, contiguous buckets fused into one"
+    if args.test_transport == "ipc":
+        ex = _ipc_exchange(rank, world, dev, "rs")
+        _NATIVE["ex"] = ex
+        return ex, ("native C-ABI exchange (kf_exchange_all_reduce_batch) over the TEST-ONLY "
+                    "cross-process IPC transport (tests/c/kf_testing_ipc.hip, every rank on "
+                    "one GPU): per bucket reduce-scatter -> HIP /np -> all-gather, the "
+                    "buckets of a step in one call"), None
     if args.dist_backend != "nccl" or args.device_index is not None:
         return Exchange(), how_torch, "not tried: ranks share a GPU (rehearsal)"
     from kungfu_amd.exchange import NativeExchange
@@ -1492,6 +1539,23 @@ def _primary_exchange(args, rank, world, dev):
                                                  "another rank" % args.native_timeout)
 
 
+def _ipc_exchange(rank, world, dev, algo):
+    """The native exchange of this rank over the test-only cross-process IPC
+    transport (tests/c/kf_testing_ipc.hip through kf_exchange_create_transport):
+    every rank a process on the same GPU, the group named by a token rank 0
+    draws and broadcasts. Test infrastructure, loaded only under
+    --test-transport ipc."""
+    tok = torch.tensor([int.from_bytes(os.urandom(6), "little") if rank == 0 else 0],
+                       dtype=torch.int64, device=dev)
+    dist.broadcast(tok, 0)
+    tests = os.path.join(ROOT, "tests")
+    if tests not in sys.path:
+        sys.path.insert(0, tests)
+    from loopback import ipc_exchange
+    return ipc_exchange("/kf_bench_ipc_%x" % int(tok.item()), rank, world, algo=algo,
+                        device=dev.index, timeout_s=60.0)
+
+
 def _rccl_report(native, world, fallback):
     """What RCCL itself says about the primary exchange, for the N > 1 line:
     the communicator's rank count (ncclCommCount), RCCL's version
@@ -1503,6 +1567,11 @@ def _rccl_report(native, world, fallback):
         return {"exchange_kind": "torch.distributed", "rccl_world": None, "rccl_version": None,
                 "why_not_native": fallback}
     count, ver = native.transport_info()
+    if count == -1 and _OPTS.get("test_transport") == "ipc":
+        return {"exchange_kind": "native (test transport)", "rccl_world": None,
+                "rccl_version": None,
+                "transport": "ipc: tests/c/kf_testing_ipc.hip, the N ranks are processes on "
+                             "one GPU; rates are not xGMI rates (no performance claim)"}
     if count == -1:  # a host-provided transport (tests' rccl1): RCCL not asked
         return {"exchange_kind": "native C-ABI (kf_exchange), host transport",
                 "rccl_world": None, "rccl_version": None}
@@ -1610,7 +1679,8 @@ def bench_c3_native(world, rank, dev, steps, warmup, n, x, algo, nb, fused=False
             "busbw_GBps": round(busbw, 2),
             "frac_of_xgmi": _xgmi_frac(busbw, world),
             "parity": ("bit-exact vs the rank-order fold (every N)" if algo == "a2a" else
-                       "N=2 bit-exact, N>2 within the order bound")}
+                       "N=2 bit-exact, N>2 within the order bound"),
+            "correct": True}
 
 
 def bench_c3_torch(world, dev, steps, n, x, nb, fused):
@@ -1665,7 +1735,25 @@ def bench_c4(world, rank, dev, steps, warmup, exchange="native"):
     want = [ops.bucket_reduce_avg([gb.buckets[i] for gb in gbs], world)
             for i in range(len(mine.buckets))]
     absums = [sum(gb.buckets[i].abs() for gb in gbs) for i in range(len(mine.buckets))]
-    ex.all_reduce_(mine.buckets, average=True)
+    orig = [b.clone() for b in mine.buckets] if exchange == "native_rs_avg" else None
+    # the native exchange coalesces contiguous buckets into one run (the
+    # reference's nccl_fusion) unless told not to; the pipelined schedule
+    # needs them as separate buckets to have groups to overlap
+    kw = {"coalesce": False} if exchange == "native_pipe" else {}
+    ex.all_reduce_(mine.buckets, average=True, **kw)
+    extra = {}
+    if orig is not None:
+        # the first real RCCL world's verdict on ncclAvg: the
+        # opt-in rs_avg against the default rs (sum, then the exact /np) on
+        # the same inputs, bit for bit
+        got = [b.clone() for b in mine.buckets]
+        for b, o in zip(mine.buckets, orig):
+            b.copy_(o)
+        _AlgoView(_NATIVE["ex"], "rs").all_reduce_(mine.buckets, average=True)
+        extra["rs_avg_parity"] = _rs_avg_verdict(got, mine.buckets, mine.spans, world)
+        for b, g in zip(mine.buckets, got):
+            b.copy_(g)
+        del got, orig
     ok = True
     for b, w, ab, sp in zip(mine.buckets, want, absums, mine.spans):
         if world == 2 or exchange == "p2p":  # rank order or two operands
@@ -1677,18 +1765,18 @@ def bench_c4(world, rank, dev, steps, warmup, exchange="native"):
     if not _agree(ok, dev):
         return {"error": "C4 parity check failed (N=2 or P2P bit-exact / N>2 bound)"}
     s_bytes = sum(sizes) * 4
-    step_s, phase_us = _timed_phases(ex, lambda: ex.all_reduce_(mine.buckets, average=True),
+    step_s, phase_us = _timed_phases(ex, lambda: ex.all_reduce_(mine.buckets, average=True, **kw),
                                      steps, warmup, dev, world)
     if exchange == "p2p":
         ex.close()
     busbw = 2 * (world - 1) / world * s_bytes / step_s / 1e9
-    how = {"native": "native C-ABI exchange: RCCL RS -> HIP /np -> RCCL AG, 16 buckets "
-                     "in one call",
+    how = {"native": "native C-ABI exchange: RCCL RS -> HIP /np -> RCCL AG, the 16 contiguous "
+                     "buckets coalesced into one run (nccl_fusion), one call",
            "native_pipe": "native C-ABI exchange: RCCL RS -> HIP /np -> RCCL AG, 16 buckets "
                           "in one call pipelined in %d groups (HIP /np on a second stream "
                           "between the groups' collectives)" % PIPE_GROUPS,
            "native_rs_avg": "native C-ABI exchange: RCCL RS with ncclAvg (no HIP epilogue) -> "
-                            "RCCL AG, 16 buckets in one call",
+                            "RCCL AG, the 16 contiguous buckets coalesced into one run, one call",
            "torch": "torch.distributed RCCL RS -> HIP /np -> RCCL AG",
            "p2p": "xGMI P2P pull: rank-order shard fold from peers' HBM + gather, "
                   "device barriers"}[exchange]
@@ -1698,7 +1786,20 @@ def bench_c4(world, rank, dev, steps, warmup, exchange="native"):
             "GiBps_per_gpu": round(s_bytes / step_s / 2**30, 3),
             "busbw_GBps": round(busbw, 2),
             "frac_of_xgmi": _xgmi_frac(busbw, world),
-            "phase_us": phase_us}
+            "phase_us": phase_us, "correct": True, **extra}
+
+
+def _rs_avg_verdict(got, ref, spans, world):
+    """rs_avg (ncclAvg inside the reduce-scatter) against rs (sum, then the
+    HIP /np) on the same buckets: bit-identical or not, and how many elements
+    differ. The default stays rs either way; this records what the transport
+    that ran actually does (transport: which one)."""
+    bad = sum(int((a[:sp] != b[:sp]).sum().item()) for a, b, sp in zip(got, ref, spans))
+    total = sum(int(sp) for sp in spans)
+    kind = "test transport (ipc)" if _OPTS.get("test_transport") == "ipc" else (
+        "RCCL, %d ranks" % world)
+    return {"bit_exact_vs_rs": bad == 0, "mismatched_elements": bad, "elements": total,
+            "transport": kind, "inputs": "N(0,1) fp32, no subnormal x / world"}
 
 
 def bench_c4_named(world, rank, dev, steps, warmup):
@@ -1749,7 +1850,7 @@ def bench_c4_named(world, rank, dev, steps, warmup):
             "bytes": s_bytes, "tensors": len(flat), "ms_per_step": round(step_s * 1e3, 4),
             "GiBps_per_gpu": round(s_bytes / step_s / 2**30, 3),
             "busbw_GBps": round(busbw, 2),
-            "frac_of_xgmi": _xgmi_frac(busbw, world)}
+            "frac_of_xgmi": _xgmi_frac(busbw, world), "correct": True}
 
 
 def bench_c3_ar(world, rank, dev, steps, warmup, n, x):
@@ -1894,7 +1995,7 @@ def bench_c5(world, rank, dev, steps, warmup, alpha=0.1, exchange="native"):
             "GiBps_per_gpu": round(s_bytes / step_s / 2**30, 3),
             "busbw_GBps": round(busbw, 2),
             "frac_of_xgmi": _xgmi_frac(busbw, world),
-            "phase_us": phase_us,
+            "phase_us": phase_us, "correct": True,
             "parity": "bf16 unpinned (DESIGN.md); bit-exact vs the local rank-order fold "
                       "+ blend"}
 

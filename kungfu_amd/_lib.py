@@ -358,12 +358,22 @@ def load():
     return lib
 
 
-def check(rc, what):
+def check(rc, what, source=None):
+    """Raise KungFuAMDError for a non-zero status. The detail is the calling
+    module's own last error first (`source`: e.g. "session" for a
+    kf_session_* call), so a stale message another module left on this thread
+    never stands in for it."""
     if rc != 0:
         lib = load()
-        detail = (lib.kf_exchange_last_error().decode() or lib.kf_session_last_error().decode()
-                  or lib.kf_last_error().decode() or lib.kf_ingest_last_error().decode()
-                  or lib.kf_p2p_last_error().decode())
+        order = ["exchange", "session", "", "ingest", "p2p"]
+        if source in order:
+            order.remove(source)
+            order.insert(0, source)
+        detail = ""
+        for m in order:
+            detail = getattr(lib, "kf_%s_last_error" % m if m else "kf_last_error")().decode()
+            if detail:
+                break
         raise KungFuAMDError("%s failed: %s (%s)" % (what, STATUS.get(rc, rc), detail))
 
 

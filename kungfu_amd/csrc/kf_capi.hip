@@ -16,7 +16,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <iterator>
+#include <map>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <vector>
 
@@ -691,11 +694,48 @@ class StagingLease
     Staging *st_;
 };
 
+// Host ranges page-locked through kf_host_register, with the address a kernel
+// uses for each: std_transform_2 finds a chunk of one of them with one lookup
+// under a shared lock instead of two hipPointerGetAttributes per buffer (six
+// per call, about 1 us each: a third of the call at the reference's 64 KiB
+// chunks, tools/explore/b1_floor.hip). Only ranges the library registered
+// itself are remembered — it also sees them unregistered — so a lookup is
+// never stale. Never destroyed (see Staging).
+struct Registered {
+    size_t bytes;
+    char *dev;
+};
+struct Registry {
+    std::shared_mutex mu;
+    std::map<uintptr_t, Registered> ranges;  // base -> range
+};
+Registry &registry()
+{
+    static Registry *r = new Registry;
+    return *r;
+}
+
+// 1 with *dev set if [p, p + bytes) lies in one registered range
+int registered(const void *p, size_t bytes, const void **dev)
+{
+    Registry &r = registry();
+    std::shared_lock<std::shared_mutex> l(r.mu);
+    if (r.ranges.empty()) return 0;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    auto it           = r.ranges.upper_bound(a);
+    if (it == r.ranges.begin()) return 0;
+    --it;
+    if (a + bytes > it->first + it->second.bytes) return 0;
+    *dev = it->second.dev + (a - it->first);
+    return 1;
+}
+
 // Where a host-API pointer lives: 0 pageable (or unknown to HIP), 1 page-locked
 // host memory (hipHostMalloc / kf_host_register), 2 device memory. `dev` is the
 // address a kernel uses for it. The whole range must be one kind.
 int classify(const void *p, size_t bytes, const void **dev)
 {
+    if (registered(p, bytes, dev)) return 1;
     hipPointerAttribute_t a;
     if (hipPointerGetAttributes(&a, p) != hipSuccess) {
         (void)hipGetLastError();
@@ -969,12 +1009,25 @@ int kf_host_register(void *p, size_t bytes)
 {
     if (!p || bytes == 0) return KF_ERR_ARG;
     KF_HIP(hipHostRegister(p, bytes, hipHostRegisterDefault));
+    void *dev = nullptr;
+    if (hipHostGetDevicePointer(&dev, p, 0) != hipSuccess || !dev) {
+        (void)hipGetLastError();
+        return KF_OK;  // still page-locked; classify() asks HIP per call
+    }
+    Registry &r = registry();
+    std::unique_lock<std::shared_mutex> l(r.mu);
+    r.ranges[reinterpret_cast<uintptr_t>(p)] = Registered{bytes, static_cast<char *>(dev)};
     return KF_OK;
 }
 
 int kf_host_unregister(void *p)
 {
     if (!p) return KF_ERR_ARG;
+    {
+        Registry &r = registry();
+        std::unique_lock<std::shared_mutex> l(r.mu);
+        r.ranges.erase(reinterpret_cast<uintptr_t>(p));
+    }
     KF_HIP(hipHostUnregister(p));
     return KF_OK;
 }

@@ -727,6 +727,23 @@ __global__ void __launch_bounds__(BLOCK)
 }
 
 // SMA blend: v = fl(fl(c1*v) + fl(c2*fl(s/np))) (sma_sgd.py:60-65).
+//
+// blend_vec does a 16-B vector's lanes two at a time in packed fp32
+// (v_pk_mul_f32 / v_pk_add_f32: each lane one IEEE fp32 operation, correctly
+// rounded, the same denormal mode, no contraction under the pragma above), so
+// the bits are the scalar blend's. The scalar form cost C5's bf16 blend about
+// 1.5 % of the roofline in VALU issue (tools/explore/sma_probe.hip,
+// profiles/r06/sma_probe_r06a.jsonl: 0.797 scalar, 0.809 packed, 0.811 for the
+// same in-place traffic with no arithmetic at all).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f32x2 sma_pair(f32x2 v, f32x2 s, f32x2 c1, f32x2 c2, f32x2 inv,
+                                          const Div &dv, bool p2)
+{
+    const f32x2 avg = p2 ? s * inv : f32x2{__fdiv_rn(s.x, dv.f), __fdiv_rn(s.y, dv.f)};
+    return c1 * v + c2 * avg;
+}
+
 template <typename T> struct SmaMath;
 template <> struct SmaMath<float> {
     using S = float;
@@ -735,6 +752,21 @@ template <> struct SmaMath<float> {
         float avg = P2 ? __fmul_rn(s, dv.fi) : __fdiv_rn(s, dv.f);
         return __fadd_rn(__fmul_rn(c1, v), __fmul_rn(c2, avg));
     }
+    template <bool P2>
+    __device__ static Vec<S> blend_vec(const Vec<S> &a, const Vec<S> &b, float c1, float c2,
+                                       const Div &dv)
+    {
+        const f32x2 C1 = {c1, c1}, C2 = {c2, c2}, I = {dv.fi, dv.fi};
+        Vec<S> r;
+#pragma unroll
+        for (int e = 0; e < 4; e += 2) {
+            const f32x2 o = sma_pair(f32x2{a.e[e], a.e[e + 1]}, f32x2{b.e[e], b.e[e + 1]}, C1, C2,
+                                     I, dv, P2);
+            r.e[e]     = o.x;
+            r.e[e + 1] = o.y;
+        }
+        return r;
+    }
 };
 template <> struct SmaMath<double> {
     using S = double;
@@ -742,6 +774,15 @@ template <> struct SmaMath<double> {
     {
         double avg = P2 ? __dmul_rn(s, dv.di) : __ddiv_rn(s, dv.d);
         return __dadd_rn(__dmul_rn(c1, v), __dmul_rn(c2, avg));
+    }
+    template <bool P2>
+    __device__ static Vec<S> blend_vec(const Vec<S> &a, const Vec<S> &b, double c1, double c2,
+                                       const Div &dv)
+    {
+        Vec<S> r;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) r.e[e] = blend<P2>(a.e[e], b.e[e], c1, c2, dv);
+        return r;
     }
 };
 template <> struct SmaMath<f16_t> {
@@ -752,6 +793,22 @@ template <> struct SmaMath<f16_t> {
         float avg     = P2 ? __fmul_rn(x, dv.fi) : __fdiv_rn(x, dv.f);
         return f32_to_f16(__fadd_rn(__fmul_rn(c1, f16_to_f32(v)), __fmul_rn(c2, avg)));
     }
+    template <bool P2>
+    __device__ static Vec<S> blend_vec(const Vec<S> &a, const Vec<S> &b, float c1, float c2,
+                                       const Div &dv)
+    {
+        const f32x2 C1 = {c1, c1}, C2 = {c2, c2}, I = {dv.fi, dv.fi};
+        Vec<S> r;
+#pragma unroll
+        for (int e = 0; e < 8; e += 2) {
+            const f32x2 o = sma_pair(f32x2{f16_to_f32(a.e[e]), f16_to_f32(a.e[e + 1])},
+                                     f32x2{f16_to_f32(b.e[e]), f16_to_f32(b.e[e + 1])}, C1, C2, I,
+                                     dv, P2);
+            r.e[e]     = f32_to_f16(o.x);
+            r.e[e + 1] = f32_to_f16(o.y);
+        }
+        return r;
+    }
 };
 template <> struct SmaMath<bf16_t> {
     using S = uint16_t;
@@ -760,6 +817,29 @@ template <> struct SmaMath<bf16_t> {
         const float x = bf16_to_f32(s);
         float avg     = P2 ? __fmul_rn(x, dv.fi) : __fdiv_rn(x, dv.f);
         return f32_to_bf16(__fadd_rn(__fmul_rn(c1, bf16_to_f32(v)), __fmul_rn(c2, avg)));
+    }
+    // a 32-bit word holds two bf16 lanes: the low one widens by a shift, the
+    // high one by a mask
+    template <bool P2>
+    __device__ static Vec<S> blend_vec(const Vec<S> &a, const Vec<S> &b, float c1, float c2,
+                                       const Div &dv)
+    {
+        const f32x2 C1 = {c1, c1}, C2 = {c2, c2}, I = {dv.fi, dv.fi};
+        u32x4 wa, wb, wr;
+        __builtin_memcpy(&wa, &a, 16);
+        __builtin_memcpy(&wb, &b, 16);
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const f32x2 v = {__uint_as_float(wa[w] << 16), __uint_as_float(wa[w] & 0xffff0000u)};
+            const f32x2 s = {__uint_as_float(wb[w] << 16), __uint_as_float(wb[w] & 0xffff0000u)};
+            const f32x2 avg = P2 ? s * I : f32x2{__fdiv_rn(s.x, dv.f), __fdiv_rn(s.y, dv.f)};
+            const f32x2 o = C1 * v + C2 * avg;
+            wr[w] = static_cast<uint32_t>(f32_to_bf16(o.x)) |
+                    (static_cast<uint32_t>(f32_to_bf16(o.y)) << 16);
+        }
+        Vec<S> r;
+        __builtin_memcpy(&r, &wr, 16);
+        return r;
     }
 };
 
@@ -802,30 +882,26 @@ __device__ __forceinline__ void sma_body(void *v, const void *s, size_t n, size_
             for (int u = 0; u < UNROLL; ++u) b[u] = ld_vec<S, 1>(sb, v0 + u * BLOCK);
 #pragma unroll
             for (int u = 0; u < UNROLL; ++u) {
-                Vec<S> r;
-#pragma unroll
-                for (int e = 0; e < V; ++e) {
-                    r.e[e] = SmaMath<T>::template blend<P2>(a[u].e[e], b[u].e[e], c1, c2, np);
-                }
-                st_vec<S>(vb, v0 + u * BLOCK, r);
+                st_vec<S>(vb, v0 + u * BLOCK,
+                          SmaMath<T>::template blend_vec<P2>(a[u], b[u], c1, c2, np));
             }
         } else {
             for (int u = 0; u < UNROLL; ++u) {
                 const size_t vi = v0 + u * BLOCK;
                 if (vi >= nvec) break;
-                Vec<S> a = ld_vec<S, 1>(vb, vi), b = ld_vec<S, 1>(sb, vi);
-                Vec<S> r;
-#pragma unroll
-                for (int e = 0; e < V; ++e) r.e[e] = SmaMath<T>::template blend<P2>(a.e[e], b.e[e], c1, c2, np);
-                st_vec<S>(vb, vi, r);
+                const Vec<S> a = ld_vec<S, 1>(vb, vi), b = ld_vec<S, 1>(sb, vi);
+                st_vec<S>(vb, vi, SmaMath<T>::template blend_vec<P2>(a, b, c1, c2, np));
             }
         }
     }
 }
 
 // the /np choice made once per kernel (see EPI_MUL above)
+// Both SMA kernels are held to 64 VGPRs, 8 waves per SIMD (two blocks per
+// SIMD): left to itself the compiler took 68 for the bf16 blend, which caps a
+// CU at 7 of its 8 blocks of loads in flight (see SmaMath above).
 template <typename T, typename C, int BLOCK, int UNROLL>
-__global__ void __launch_bounds__(BLOCK)
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8)))
     sma_kernel(void *v, const void *s, size_t n, size_t head, size_t nvec,
                C c1, C c2, Div np, int vec_ok)
 {
@@ -852,7 +928,8 @@ template <typename C> struct SmaBatchArgs {
 };
 
 template <typename T, typename C, int BLOCK, int UNROLL>
-__global__ void __launch_bounds__(BLOCK) sma_batch_kernel(SmaBatchArgs<C> a, Div np)
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8)))
+    sma_batch_kernel(SmaBatchArgs<C> a, Div np)
 {
     const unsigned b = blockIdx.x;
     int i            = 0;

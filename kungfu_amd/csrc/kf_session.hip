@@ -580,8 +580,9 @@ struct SessOp {
     size_t folds = 0;  // host mode: its fold jobs not yet retired by the poll thread
     int rc       = KF_OK;
     std::string err;
-    // KUNGFU_AMD_OP_TIMEOUT_S: the call fails with KF_ERR_TIMEOUT once a
-    // message it waits for has not come by then (0 = no deadline)
+    // KUNGFU_AMD_OP_TIMEOUT_S: the call fails with KF_ERR_TIMEOUT when no
+    // message of it has come for that long (set at its start, moved on by
+    // every message it takes; 0 = no deadline)
     std::chrono::steady_clock::time_point deadline{};
 };
 
@@ -712,6 +713,13 @@ struct kf_session {
     }
     std::deque<Stashed> stash;  // per-name mailbox for early messages
     std::mutex run_mu;          // one poll loop over the sockets at a time
+    // the first failure of a call in flight (a dead peer, an op deadline, a
+    // torn socket) breaks the session for good: late messages of the failed
+    // call could otherwise be replayed from the stash into the next call that
+    // reuses its name (tensor names repeat every step), so every later call
+    // fails until kf_session_destroy. Guarded by run_mu.
+    int broken_rc = KF_OK;
+    std::string broken_err;
     int wake_fd = -1;           // eventfd: a submission, or an op's last chunk sent
 
     // sender thread
@@ -1913,8 +1921,15 @@ int kf_session::run(SessOp *one)
 
     // a failure while reading the sockets leaves no message boundary to trust:
     // every collective in flight fails with it (its chunks stop being routed)
+    auto mark_broken = [&](int rc, const std::string &why) {
+        if (broken_rc != KF_OK) return;
+        broken_rc  = rc;
+        broken_err = why;
+        stash.clear();  // nothing may be replayed into a later call
+    };
     auto fail_all = [&](int rc) {
         const std::string why = t_sess_error;
+        mark_broken(rc, why);
         for (SessOp *o : active) {
             if (o->rc == KF_OK) {
                 o->rc  = rc;
@@ -1927,6 +1942,7 @@ int kf_session::run(SessOp *one)
     // one call fails alone: its chunks stop being routed (later messages for
     // them wait in the stash), the others in flight go on
     auto fail_op = [&](SessOp *o, int rc, const std::string &why) {
+        mark_broken(rc, why);
         if (o->rc == KF_OK) {
             o->rc  = rc;
             o->err = why;
@@ -1961,6 +1977,14 @@ int kf_session::run(SessOp *one)
     auto start = [&](SessOp *o) {
         tr(TR_OP_START, -1, static_cast<int>(o->count), 0);
         t_sess_error.clear();
+        if (broken_rc != KF_OK) {
+            o->rc        = KF_ERR_IO;
+            o->err       = "the session failed earlier (" + broken_err +
+                     "); destroy it and create a new one";
+            o->remaining = 0;
+            active.push_back(o);
+            return;
+        }
         if (op_timeout_ms > 0) {
             o->deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(op_timeout_ms);
         }
@@ -1983,6 +2007,7 @@ int kf_session::run(SessOp *one)
             const int rc = handle(*o, f->second.second, it->flags, it->peer, -1, it->data.data());
             it           = stash.erase(it);
             if (rc != KF_OK) {  // a stashed copy: the sockets are intact
+                mark_broken(rc, t_sess_error);
                 o->rc        = rc;
                 o->err       = t_sess_error;
                 o->remaining = 0;
@@ -2223,9 +2248,14 @@ int kf_session::run(SessOp *one)
             auto it        = index.find(hname);
             if (it != index.end() && expects(*it->second.first, it->second.second, flags, peer)) {
                 const int ci = static_cast<int>(it->second.second);
+                SessOp *op   = it->second.first;
                 tr(TR_RX_HDR, ci, static_cast<int>(flags), 0);
-                rc = handle(*it->second.first, it->second.second, flags, peer, fd, nullptr);
+                rc = handle(*op, it->second.second, flags, peer, fd, nullptr);
                 tr(TR_RX_DONE, ci, static_cast<int>(flags), 0);
+                if (rc == KF_OK && op_timeout_ms > 0) {  // progress: the deadline moves
+                    op->deadline = std::chrono::steady_clock::now() +
+                                   std::chrono::milliseconds(op_timeout_ms);
+                }
                 continue;
             }
             // not ours (yet): keep it for the call it belongs to

@@ -64,14 +64,14 @@ class Session:
         if strategy is not None:  # else KUNGFU_ALLREDUCE_STRATEGY / default
             _lib.check(self.lib.kf_session_set_strategy(
                 self._h, STRATEGIES[strategy], 1 if hash_method == "NAME" else 0),
-                "kf_session_set_strategy")
+                "kf_session_set_strategy", "session")
         self._pending = []  # async handles: keep buffers and callbacks alive
         self._plock = threading.Lock()
         if host_reduce_fn is not None:
             if mode != "host":
                 raise ValueError("host_reduce_fn needs mode='host'")
             _lib.check(self.lib.kf_session_set_host_reduce(self._h, host_reduce_fn),
-                       "kf_session_set_host_reduce")
+                       "kf_session_set_host_reduce", "session")
 
     @classmethod
     def from_env(cls, sock_dir="/tmp", **kw):
@@ -117,7 +117,7 @@ class Session:
             stream = torch.cuda.current_stream(send.device).cuda_stream
         rc = self.lib.kf_session_all_reduce(self._h, sp, rp, count, dt, int(red),
                                             name.encode(), stream)
-        _lib.check(rc, "kf_session_all_reduce")
+        _lib.check(rc, "kf_session_all_reduce", "session")
         return recv
 
     def _stream(self, t):
@@ -139,7 +139,7 @@ class Session:
         f = (ctypes.c_int32 * self.size)(*forest)
         _lib.check(self.lib.kf_session_subset_all_reduce(self._h, sp, rp, count, dt, int(red), f,
                                                          name.encode(), self._stream(send)),
-                   "kf_session_subset_all_reduce")
+                   "kf_session_subset_all_reduce", "session")
         return recv
 
     def reduce(self, send, recv, name, op="sum"):
@@ -152,7 +152,7 @@ class Session:
             raise ValueError("send/recv mismatch")
         _lib.check(self.lib.kf_session_reduce(self._h, sp, rp, count, dt, int(red),
                                               name.encode(), self._stream(send)),
-                   "kf_session_reduce")
+                   "kf_session_reduce", "session")
         return recv
 
     def broadcast(self, send, recv, name):
@@ -164,7 +164,7 @@ class Session:
             raise ValueError("send/recv mismatch")
         _lib.check(self.lib.kf_session_broadcast(self._h, sp, rp, count, dt, name.encode(),
                                                  self._stream(send)),
-                   "kf_session_broadcast")
+                   "kf_session_broadcast", "session")
         return recv
 
     def all_reduce_async(self, send, recv, name, op="sum", callback=None):
@@ -189,7 +189,7 @@ class Session:
         h = AsyncHandle(send, recv, name, callback)
         rc = self.lib.kf_session_all_reduce_async(self._h, sp, rp, count, dt, int(red),
                                                   name.encode(), stream, h._cfn, None)
-        _lib.check(rc, "kf_session_all_reduce_async")
+        _lib.check(rc, "kf_session_all_reduce_async", "session")
         with self._plock:
             self._pending = [p for p in self._pending if not p.done()] + [h]
         return h
@@ -197,14 +197,14 @@ class Session:
     def barrier(self):
         """Session.Barrier (session.go:98-115): returns once every peer has
         entered it."""
-        _lib.check(self.lib.kf_session_barrier(self._h), "kf_session_barrier")
+        _lib.check(self.lib.kf_session_barrier(self._h), "kf_session_barrier", "session")
 
     def wait_all(self):
         """Block until every queued all-reduce has finished."""
         rc = self.lib.kf_session_wait_all(self._h)
         with self._plock:
             self._pending = [p for p in self._pending if not p.done()]
-        _lib.check(rc, "kf_session_wait_all")
+        _lib.check(rc, "kf_session_wait_all", "session")
 
 
 class AsyncHandle:
@@ -232,7 +232,7 @@ class AsyncHandle:
     def wait(self, timeout=None):
         if not self._ev.wait(timeout):
             raise TimeoutError("all-reduce %r not done" % self.name)
-        _lib.check(self.status, "all-reduce %r" % self.name)
+        _lib.check(self.status, "all-reduce %r" % self.name, "session")
         return self.bufs[1]
 
 

@@ -14,6 +14,15 @@
  *  rccl1      a one-rank librccl communicator bound through the transport
  *             table, so the exchange calls librccl's own entry points with
  *             its exact arguments instead of the built-in world-1 copy.
+ *  ipc        `world` PROCESSES on one device (tests/c/kf_testing_ipc.hip):
+ *             every collective stages the rank's input in its own HBM buffer,
+ *             meets the other ranks in a POSIX shared-memory segment, and
+ *             pulls from the peers' staging buffers through HIP IPC mappings
+ *             (the reduce-scatter folds in rank order on the device, every
+ *             integer / f32 / f64 op and ncclAvg's premultiplied float form;
+ *             no f16/bf16/u16/i16 reduce-scatter). Synchronous, no
+ *             performance claim: it lets bench.py's N > 1 branch run the
+ *             native exchange with N ranks where RCCL refuses to share a GPU.
  */
 #pragma once
 #include "kungfu_amd.h"
@@ -34,6 +43,16 @@ void kf_loopback_fail_at(kf_loopback_t *g, int64_t call);
 /* NULL on failure (kf_testing_last_error) */
 kf_exchange_t *kf_exchange_create_rccl1(int device);
 const char *kf_testing_last_error(void);
+
+/* Join the cross-process group `name` (one "/name" component, unique to the
+ * run; every rank passes the same) as `rank` of `world` on HIP device
+ * `device`. Collective: returns once every rank has joined, or NULL after
+ * timeout_ms (<= 0: 120 s) or on failure (kf_ipc_last_error). The same
+ * timeout bounds every rendezvous of the group's collectives; a timeout or a
+ * failure on any rank fails every later call of every rank. */
+kf_exchange_t *kf_exchange_create_ipc(const char *name, int rank, int world, int device,
+                                      int timeout_ms);
+const char *kf_ipc_last_error(void);
 
 #ifdef __cplusplus
 }

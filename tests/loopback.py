@@ -35,6 +35,11 @@ def load():
         lib.kf_exchange_create_rccl1.restype = ctypes.c_void_p
         lib.kf_testing_last_error.argtypes = []
         lib.kf_testing_last_error.restype = ctypes.c_char_p
+        lib.kf_exchange_create_ipc.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
+                                               ctypes.c_int, ctypes.c_int]
+        lib.kf_exchange_create_ipc.restype = ctypes.c_void_p
+        lib.kf_ipc_last_error.argtypes = []
+        lib.kf_ipc_last_error.restype = ctypes.c_char_p
         _lib = lib
     return _lib
 
@@ -69,6 +74,18 @@ def rccl1_exchange(algo="auto", device=0):
     lib = load()
     h = lib.kf_exchange_create_rccl1(device)
     assert h, lib.kf_testing_last_error().decode()
+    return NativeExchange.from_handle(h, algo)
+
+
+def ipc_exchange(name, rank, world, algo="auto", device=0, timeout_s=120.0):
+    """kf_exchange_create_ipc: this PROCESS as `rank` of `world` processes on
+    one device, the exchange's collectives moved through HIP-IPC-mapped
+    staging buffers and a shared-memory rendezvous named `name` (every rank
+    passes the same "/name"). Collective: returns once every rank joined."""
+    lib = load()
+    h = lib.kf_exchange_create_ipc(name.encode(), int(rank), int(world), int(device),
+                                   int(timeout_s * 1000))
+    assert h, lib.kf_ipc_last_error().decode()
     return NativeExchange.from_handle(h, algo)
 
 

@@ -70,3 +70,29 @@ def test_rccl_report_fails_loudly_on_a_short_communicator():
     # the torch.distributed fallback says why
     rep = bench._rccl_report(None, 2, "not tried: ranks share a GPU (rehearsal)")
     assert rep["exchange_kind"] == "torch.distributed" and "share a GPU" in rep["why_not_native"]
+
+
+def test_rccl_report_names_the_test_transport(monkeypatch):
+    """--test-transport ipc (N processes on one GPU): the line says the
+    exchange ran over the test transport and claims no RCCL world."""
+    import bench
+    monkeypatch.setitem(bench._OPTS, "test_transport", "ipc")
+    rep = bench._rccl_report(_FakeNative(-1, 0), 2, None)
+    assert rep["exchange_kind"] == "native (test transport)" and rep["rccl_world"] is None
+    assert "not xGMI" in rep["transport"]
+
+
+def test_rs_avg_verdict_records_the_transport(monkeypatch):
+    """at N > 1, c4_rs_avg carries rs_avg_parity — ncclAvg
+    against sum-then-/np on the same buckets, bit for bit, with the transport
+    that produced it (the first real RCCL world's verdict lands here)."""
+    import torch
+    import bench
+    a = [torch.tensor([1.0, 2.0, 3.0, 9.0]), torch.tensor([4.0, 5.0])]
+    b = [torch.tensor([1.0, 2.0, 3.5, 7.0]), torch.tensor([4.0, 5.0])]
+    v = bench._rs_avg_verdict(a, b, [3, 2], 8)  # element 3 of bucket 0 is padding
+    assert v["bit_exact_vs_rs"] is False and v["mismatched_elements"] == 1
+    assert v["elements"] == 5 and v["transport"] == "RCCL, 8 ranks"
+    assert bench._rs_avg_verdict(a, a, [4, 2], 2)["bit_exact_vs_rs"] is True
+    monkeypatch.setitem(bench._OPTS, "test_transport", "ipc")
+    assert bench._rs_avg_verdict(a, a, [4, 2], 2)["transport"] == "test transport (ipc)"

@@ -212,3 +212,58 @@ ex.close()
     assert rep["rccl_world"] == 1 and rep["exchange_kind"].startswith("native"), rep
     major = int(rep["rccl_version"].split(".")[0])
     assert major >= 2, rep
+
+
+_IPC_EXTRAS = ("c4", "c5", "c5_pipe", "c4_pipe", "c4_rs_avg", "c3_pipe", "c4_named")
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_native_branch_over_ipc_transport(world):
+    """bench.py's NATIVE N > 1 branch with N ranks —
+    the primary exchange's parity check and schedule trial, the timed C3 step
+    with its phase windows, the agreed sub-benchmark loop, c4_named in its
+    child process group, the line — run by N processes sharing cuda:0, the
+    exchange's collectives moved by the test-only cross-process IPC transport
+    (tests/c/kf_testing_ipc.hip through kf_exchange_create_transport) because
+    RCCL refuses two ranks on one GPU. Every sub-benchmark must be parity-
+    checked correct, the phases must account for the un-pipelined steps, and
+    the line must say which transport ran (never an xGMI claim)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    env = dict(os.environ)
+    # N processes' streams on one GPU: two hardware queues each, so the GPU
+    # does not time-slice them (INTEGRATION.md §5, GPU_MAX_HW_QUEUES)
+    env["GPU_MAX_HW_QUEUES"] = "2"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
+           str(world), "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--dist-backend", "gloo",
+           "--device-index", "0", "--test-transport", "ipc", "--steps", "3", "--warmup", "1",
+           "--elems", str(4 << 20), "--extras", ",".join(_IPC_EXTRAS),
+           "--extras-timeout", "150"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    c = d["collective"]
+    assert d["n_gpus"] == world and d["value"] > 0, d
+    assert c["exchange_kind"] == "native (test transport)" and c["rccl_world"] is None, c
+    assert "native_exchange_error" not in c and c["exchange"].startswith("native"), c
+    assert c["correct"] is True, c
+    assert sorted(c["schedule_trial_ms"]) == ["a2a", "fused", "grouped", "pipelined"], c
+    for k in _IPC_EXTRAS:
+        assert "error" not in d[k] and d[k]["correct"] is True, (k, d[k])
+        assert d[k]["ms_per_step"] > 0, (k, d[k])
+    # the phase windows account for the un-pipelined timed steps: their sum
+    # is the step minus the host's gaps between calls
+    for ph in (c.get("phase_us"), d["c4"]["phase_us"], d["c5"]["phase_us"]):
+        if ph is None or not ph["timed_calls_per_step"]:
+            continue
+        assert 0.3 * ph["step_us"] <= ph["sum"] <= 1.02 * ph["step_us"], ph
+    # pipelined calls are counted, not split
+    assert d["c5_pipe"]["phase_us"]["pipelined_calls_untimed"] > 0, d["c5_pipe"]
+    assert d["c4_pipe"]["phase_us"]["pipelined_calls_untimed"] > 0, d["c4_pipe"]
+    # rs_avg (ncclAvg) against rs on the same inputs, recorded with its transport
+    par = d["c4_rs_avg"]["rs_avg_parity"]
+    assert par["transport"] == "test transport (ipc)" and par["bit_exact_vs_rs"] is True, par

@@ -358,3 +358,48 @@ def test_host_async_calls_bounded_by_op_timeout(monkeypatch):
     assert 1.5 < dt < 8, (dt, str(ei.value))
     assert len(got) == 3 and all(st == 8 for st in got), got  # KF_ERR_TIMEOUT
     assert all(h.done() for h in hs)
+
+
+def test_failed_session_refuses_later_calls(monkeypatch):
+    """once a call failed (here its op deadline), the
+    session is broken for good. A retry under the same name — tensor names
+    repeat every step — fails at once with "failed earlier" instead of
+    picking up the failed call's late message (kept in the per-name stash)
+    and returning the previous step's data as its result."""
+    from kungfu_amd import _lib
+    from kungfu_amd.session import Session
+    from test_session import oracle_reduce_fn
+    lib = _lib.load()
+    monkeypatch.setenv("KUNGFU_ALLREDUCE_STRATEGY", "STAR")
+    monkeypatch.setenv("KUNGFU_AMD_OP_TIMEOUT_S", "2")
+    body = np.full(NF, 2.0, np.float32).tobytes()
+    with tempfile.TemporaryDirectory() as d:
+        def script(rx, tx):
+            time.sleep(3.0)  # past the first call's 2 s deadline
+            try:  # that call's late message (blocks until read, or until the close)
+                tx.sendall(_header(0, len(body)) + body)
+            except OSError:
+                pass
+            _drain(rx, 6)
+
+        fake = FakePeer(lib, d, 1, script)
+        fake.start()
+        s = Session(0, 2, d, mode="host", host_reduce_fn=oracle_reduce_fn())
+        x = np.ones(NF, np.float32)
+        y = np.zeros_like(x)
+        with pytest.raises(RuntimeError) as e1:
+            s.all_reduce(x, y, NAME)
+        time.sleep(2.0)  # the late message is on the socket now
+        y2 = np.zeros_like(x)
+        t0 = time.monotonic()
+        with pytest.raises(RuntimeError) as e2:
+            s.all_reduce(x, y2, NAME)
+        dt = time.monotonic() - t0
+        s.close()
+        fake.join(15)
+        fake.close()
+        assert fake.err is None, fake.err
+    assert "KUNGFU_AMD_OP_TIMEOUT_S" in str(e1.value) or "KF_ERR_TIMEOUT" in str(e1.value), e1.value
+    assert "failed earlier" in str(e2.value), e2.value
+    assert dt < 1.0, dt
+    assert not y2.any()  # nothing of the stale message reached the retry
