@@ -1832,14 +1832,24 @@ def bench_c4_named(world, rank, dev, steps, warmup):
             ex.all_reduce_named(names[i], flat[i], average=True)
         ex.wait_named()
 
+    inp = [f.clone() for f in flat]
     step()
-    ok = True
-    for v, w, ab in zip(flat, want, absums):
-        ok &= bool(torch.equal(v, w)) if world <= 2 else _within(v, w, ab, world)
-    del want, absums
+    bad = [i for i, (v, w, ab) in enumerate(zip(flat, want, absums))
+           if not (bool(torch.equal(v, w)) if world <= 2 else _within(v, w, ab, world))]
+    detail = ""
+    if bad:  # which tensors, and how far off (on this rank's stderr too)
+        i = bad[0]
+        off = int((flat[i] != want[i]).sum().item())
+        detail = (" (rank %d: %d of %d tensors off; first %s, %d of %d elements, max |diff| "
+                  "%.3g, equal to own input: %s)" % (
+                      rank, len(bad), len(flat), names[i], off, flat[i].numel(),
+                      (flat[i] - want[i]).abs().max().item(),
+                      bool(torch.equal(flat[i], inp[i]))))
+        print("[bench] c4_named" + detail, file=sys.stderr, flush=True)
+    del want, absums, inp
     gbs.clear()
-    if not _agree(ok, dev):
-        return {"error": "C4 named parity check failed (N<=2 bit-exact / N>2 bound)"}
+    if not _agree(not bad, dev):
+        return {"error": "C4 named parity check failed (N<=2 bit-exact / N>2 bound)" + detail}
     s_bytes = sum(sizes) * 4
     step_s = _timed(step, steps, warmup, dev, world)
     busbw = 2 * (world - 1) / world * s_bytes / step_s / 1e9

@@ -569,7 +569,14 @@ int streamed(kf_ingest_t *g, int fd, uint32_t len, void *stream, void *wait_stre
         t_ingest_error = "streamed receive: kernel launch failed";
         return rc;
     }
-    ING_HIP(hipEventRecord(g->done[slot], ks));
+    if (hipError_t e = hipEventRecord(g->done[slot], ks); e != hipSuccess) {
+        // the kernel is queued and would wait for a body nobody reads: tell
+        // it to stop and let it drain before the caller may free its words
+        // (its stream is not the one the caller synchronises when ks != cs)
+        kf_stream::abort_wait(ctl);
+        (void)hipStreamSynchronize(ks);
+        return hip_fail(e, "hipEventRecord after a streamed launch");
+    }
     {
         std::lock_guard<std::mutex> lock(g->mu);
         g->armed[slot] = true;

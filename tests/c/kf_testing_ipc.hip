@@ -64,6 +64,11 @@ struct Slot {
     char handle[kHandleBytes];  // this rank's staging buffer
     uint64_t cap;
     int32_t color, key;  // split
+    // the call this rank is in (checked by every rank after rendezvous A: a
+    // rank whose call differs is a caller bug, failed loudly instead of
+    // moving mismatched bytes)
+    uint64_t seq, bytes;
+    int32_t kind, root;
 };
 
 struct Seg {
@@ -86,6 +91,7 @@ struct IpcComm {
     size_t cap     = 0;
     std::vector<void *> peer;  // every rank's staging buffer as mapped here
     uint64_t nsplit = 0;
+    uint64_t ncalls = 0;
 };
 
 Seg *map_segment(const std::string &name)
@@ -177,23 +183,46 @@ int ensure(IpcComm *c, size_t need)
         if (c->seg->slot[j].cap != cap) return fail(c, IPC_ARG, "ipc transport: ranks disagree on a size");
         hipIpcMemHandle_t ph;
         std::memcpy(&ph, c->seg->slot[j].handle, sizeof(ph));
-        e = hipIpcOpenMemHandle(&c->peer[j], ph, hipIpcMemLazyEnablePeerAccess);
-        if (e != hipSuccess) return hip_fail(c, e, "hipIpcOpenMemHandle");
+        // an import right after the export has been refused now and then
+        // with 4 processes on one GPU (r06d); a few short retries, counted
+        // in the error if they all fail
+        int tries = 0;
+        do {
+            e = hipIpcOpenMemHandle(&c->peer[j], ph, hipIpcMemLazyEnablePeerAccess);
+            if (e == hipSuccess) break;
+            (void)hipGetLastError();
+            struct timespec ts = {0, 2000000};
+            nanosleep(&ts, nullptr);
+        } while (++tries < 10);
+        if (e != hipSuccess) {
+            return fail(c, IPC_HIP, std::string("hipIpcOpenMemHandle of rank ") + std::to_string(j) +
+                                        "'s staging (" + std::to_string(tries) + " tries): " +
+                                        hipGetErrorString(e));
+        }
     }
     return barrier(c);  // the slots are read before the next growth rewrites them
 }
 
+enum { K_RS = 1, K_AG = 2, K_A2A = 3, K_BC = 4 };
+
 template <typename Pull>
-int collective(void *comm, const void *send, size_t in_bytes, bool stage_mine, void *stream, Pull pull)
+int collective(void *comm, int kind, int root, const void *send, size_t in_bytes, bool stage_mine,
+               void *stream, Pull pull)
 {
     auto *c        = static_cast<IpcComm *>(comm);
     hipStream_t st = static_cast<hipStream_t>(stream);
+    t_err.clear();
     if (c->seg->broken.load(std::memory_order_acquire)) {
         t_err = "ipc transport: the group failed earlier";
         return IPC_BROKEN;
     }
     int rc = ensure(c, in_bytes);
     if (rc != IPC_OK) return rc;
+    Slot &me = c->seg->slot[c->rank];
+    me.seq   = c->ncalls++;
+    me.bytes = in_bytes;
+    me.kind  = kind;
+    me.root  = root;
     if (stage_mine && in_bytes) {
         hipError_t e = hipMemcpyAsync(c->stage, send, in_bytes, hipMemcpyDeviceToDevice, st);
         if (e != hipSuccess) return hip_fail(c, e, "ipc transport: staging copy");
@@ -201,6 +230,17 @@ int collective(void *comm, const void *send, size_t in_bytes, bool stage_mine, v
     hipError_t e = hipStreamSynchronize(st);
     if (e != hipSuccess) return hip_fail(c, e, "ipc transport: stream sync");
     if ((rc = barrier(c)) != IPC_OK) return rc;
+    for (int j = 0; j < c->world; ++j) {
+        const Slot &p = c->seg->slot[j];
+        if (p.seq != me.seq || p.kind != kind || p.bytes != in_bytes || p.root != root) {
+            return fail(c, IPC_ARG,
+                        "ipc transport: rank " + std::to_string(j) + " is in call #" +
+                            std::to_string(p.seq) + " (kind " + std::to_string(p.kind) + ", " +
+                            std::to_string(p.bytes) + " B), rank " + std::to_string(c->rank) +
+                            " in #" + std::to_string(me.seq) + " (kind " + std::to_string(kind) +
+                            ", " + std::to_string(in_bytes) + " B)");
+        }
+    }
     if ((rc = pull(c, st)) != IPC_OK) return fail(c, rc, t_err.empty() ? "ipc transport: pull" : t_err);
     e = hipStreamSynchronize(st);
     if (e != hipSuccess) return hip_fail(c, e, "ipc transport: stream sync");
@@ -299,7 +339,8 @@ int ipc_reduce_scatter(const void *send, void *recv, size_t count, KungFu_Dataty
         return IPC_DTYPE;  // refused before any rendezvous, on every rank alike
     }
     const size_t sz = dsize(dt);
-    return collective(comm, send, count * c->world * sz, true, stream, [&](IpcComm *cc, hipStream_t st) {
+    return collective(comm, K_RS, o, send, count * c->world * sz, true, stream,
+                      [&](IpcComm *cc, hipStream_t st) {
         FoldIn in{};
         for (int j = 0; j < cc->world; ++j) in.p[j] = cc->peer[j];
         const size_t off = static_cast<size_t>(cc->rank) * count;
@@ -329,7 +370,7 @@ int copy(void *dst, const void *src, size_t b, hipStream_t st)
 
 int ipc_all_gather(const void *send, void *recv, size_t b, void *comm, void *stream)
 {
-    return collective(comm, send, b, true, stream, [&](IpcComm *c, hipStream_t st) {
+    return collective(comm, K_AG, 0, send, b, true, stream, [&](IpcComm *c, hipStream_t st) {
         for (int j = 0; j < c->world; ++j) {
             int rc = copy(static_cast<char *>(recv) + j * b, c->peer[j], b, st);
             if (rc != IPC_OK) return rc;
@@ -341,7 +382,8 @@ int ipc_all_gather(const void *send, void *recv, size_t b, void *comm, void *str
 int ipc_all_to_all(const void *send, void *recv, size_t b, void *comm, void *stream)
 {
     auto *c = static_cast<IpcComm *>(comm);
-    return collective(comm, send, b * c->world, true, stream, [&](IpcComm *cc, hipStream_t st) {
+    return collective(comm, K_A2A, 0, send, b * c->world, true, stream,
+                      [&](IpcComm *cc, hipStream_t st) {
         for (int j = 0; j < cc->world; ++j) {
             int rc = copy(static_cast<char *>(recv) + j * b,
                           static_cast<const char *>(cc->peer[j]) + cc->rank * b, b, st);
@@ -355,7 +397,8 @@ int ipc_broadcast(const void *send, void *recv, size_t b, int root, void *comm, 
 {
     auto *c = static_cast<IpcComm *>(comm);
     if (root < 0 || root >= c->world) return IPC_ARG;
-    return collective(comm, send, b, c->rank == root, stream, [&](IpcComm *cc, hipStream_t st) {
+    return collective(comm, K_BC, root, send, b, c->rank == root, stream,
+                      [&](IpcComm *cc, hipStream_t st) {
         return copy(recv, cc->peer[root], b, st);
     });
 }
@@ -368,6 +411,7 @@ int ipc_split(void *comm, int color, int key, void **newcomm)
 {
     auto *c  = static_cast<IpcComm *>(comm);
     *newcomm = nullptr;
+    t_err.clear();
     if (c->seg->broken.load(std::memory_order_acquire)) return IPC_BROKEN;
     c->seg->slot[c->rank].color = color;
     c->seg->slot[c->rank].key   = key;
@@ -438,6 +482,13 @@ void ipc_destroy(void *comm)
 }
 const char *ipc_error_string(int code)
 {
+    // the failing call's own message when this thread has one (the exchange
+    // asks right after the failed call, on the same thread)
+    thread_local std::string msg;
+    if (!t_err.empty() && code != IPC_OK) {
+        msg = t_err;
+        return msg.c_str();
+    }
     switch (code) {
     case IPC_HIP: return "ipc transport: a HIP call failed";
     case IPC_DTYPE: return "ipc transport: no reduce-scatter for this dtype";
