@@ -161,7 +161,11 @@ void drop_peers(IpcComm *c)
 int ensure(IpcComm *c, size_t need)
 {
     if (need <= c->cap) return IPC_OK;
-    size_t cap = size_t(1) << 20;
+    // at least 64 MiB: a smaller hipMalloc may be carved out of a shared
+    // fragment, and exporting one failed now and then with "invalid argument"
+    // (r06d, 4 processes on one GPU). The buffer must be the whole
+    // allocation its handle describes.
+    size_t cap = size_t(64) << 20;
     while (cap < need) cap <<= 1;
     drop_peers(c);
     if (c->stage) (void)hipFree(c->stage);
@@ -169,9 +173,16 @@ int ensure(IpcComm *c, size_t need)
     c->cap   = 0;
     hipError_t e = hipMalloc(&c->stage, cap);
     if (e != hipSuccess) return hip_fail(c, e, "ipc transport: hipMalloc of the staging buffer");
+    void *base  = nullptr;
+    size_t span = 0;
+    e           = hipMemGetAddressRange(&base, &span, c->stage);
+    if (e != hipSuccess) return hip_fail(c, e, "hipMemGetAddressRange of the staging buffer");
+    if (base != c->stage) {
+        return fail(c, IPC_HIP, "ipc transport: the staging buffer is not the base of its allocation");
+    }
     hipIpcMemHandle_t h;
     e = hipIpcGetMemHandle(&h, c->stage);
-    if (e != hipSuccess) return hip_fail(c, e, "hipIpcGetMemHandle");
+    if (e != hipSuccess) return hip_fail(c, e, "hipIpcGetMemHandle of the staging buffer");
     std::memcpy(c->seg->slot[c->rank].handle, &h, sizeof(h));
     c->seg->slot[c->rank].cap = cap;
     c->cap                    = cap;

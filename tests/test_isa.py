@@ -153,3 +153,70 @@ def test_runtime_k_fold_keeps_one_vector_in_flight(kernels):
     assert len(ks) >= 20, len(ks)
     bad = [(k, _serial_loads(v)) for k, v in ks.items() if _serial_loads(v) < 4]
     assert not bad, bad[:5]
+
+
+READELF = "/opt/rocm/lib/llvm/bin/llvm-readelf"
+
+
+@pytest.fixture(scope="module")
+def kernel_meta(tmp_path_factory):
+    """name -> {vgpr_count, private_segment_fixed_size, vgpr_spill_count}
+    from the code objects' amdhsa metadata notes."""
+    if not (os.path.exists(OBJDUMP) and os.path.exists(READELF)):
+        pytest.skip("llvm tools not found")
+    d = tmp_path_factory.mktemp("meta")
+    lib = d / "lib.so"
+    shutil.copy(LIB, lib)
+    subprocess.run([OBJDUMP, "--offloading", str(lib)], check=True, capture_output=True)
+    meta = {}
+    for o in sorted(p for p in d.iterdir() if p.name.endswith("gfx950")):
+        notes = subprocess.run([READELF, "--notes", str(o)], check=True, capture_output=True,
+                               text=True).stdout
+        cur = {}
+        for line in notes.splitlines():
+            m = re.match(r"^\s+-?\s*\.(\w+):\s+(\S+)\s*$", line)
+            if not m:
+                continue
+            k, v = m.groups()
+            if k == "agpr_count" and line.lstrip().startswith("-"):
+                cur = {}
+            if k == "name":
+                meta[v] = cur
+            elif k in ("vgpr_count", "private_segment_fixed_size", "vgpr_spill_count"):
+                cur[k] = int(v)
+    return meta
+
+
+def test_streaming_kernels_never_spill(kernel_meta):
+    """No product streaming kernel touches scratch: a spill would put private
+    memory traffic beside the HBM streams every launch pays for."""
+    ks = {k: v for k, v in kernel_meta.items()
+          if (PRODUCT_REDUCE.match(k) and not TUNING_ONLY.match(k)) or k.startswith(STREAMING)}
+    assert len(ks) >= 100, len(ks)
+    bad = [(k, v) for k, v in ks.items()
+           if v.get("private_segment_fixed_size", 0) or v.get("vgpr_spill_count", 0)]
+    assert not bad, bad[:5]
+
+
+def test_sma_kernels_keep_eight_waves(kernel_meta):
+    """The SMA blends (C5's blend step) stay within 64 VGPRs — 8 waves per
+    SIMD, two 256-thread blocks per SIMD of loads in flight. The packed-fp32
+    bf16 blend took 68 (7 waves) in one formulation before it was rewritten
+    on 32-bit words (DESIGN.md §3, C5's two kernels)."""
+    ks = {k: v for k, v in kernel_meta.items() if k.startswith(STREAMING[1]) or
+          k.startswith(STREAMING[3])}
+    assert len(ks) == 8, sorted(ks)
+    bad = [(k, v["vgpr_count"]) for k, v in ks.items() if v["vgpr_count"] > 64]
+    assert not bad, bad
+
+
+def test_bf16_sma_blend_is_packed(kernels):
+    """The bf16 blend runs on pairs of lanes in packed fp32 (v_pk_mul_f32 /
+    v_pk_add_f32): same IEEE operations as the scalar form, bit-identical
+    (tests/test_gpu_parity.py), a quarter fewer VALU instructions."""
+    ks = [k for k in kernels if k.startswith(("_ZN2kf10sma_kernelINS_6bf16_t",
+                                              "_ZN2kf16sma_batch_kernelINS_6bf16_t"))]
+    assert len(ks) == 2, ks
+    for k in ks:
+        assert sum(1 for ins in kernels[k] if ins.startswith("v_pk_mul_f32")) >= 48, k
+        assert sum(1 for ins in kernels[k] if ins.startswith("v_pk_add_f32")) >= 16, k
