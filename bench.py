@@ -1104,6 +1104,14 @@ def main():
                  ("c3_ar", lambda: bench_c3_ar(world, rank, dev, steps_x, 5, n, x)))
         # last: the experimental peer-to-peer paths, in child processes
         extra += tuple(_p2p_runs(world, rank, dev, steps_x, n, x).items())
+        child_keys = P2P_KEYS
+        if args.test_transport == "ipc":
+            # the ranks already share one GPU: c4_named runs in these
+            # processes, on an exchange of its own (a child group would put
+            # 2N processes' queues on the GPU, which then time-slices them)
+            child_keys = tuple(k for k in P2P_KEYS if k != "c4_named")
+            extra = tuple((k, (lambda: _named_ipc(world, rank, dev, steps_x)) if k == "c4_named"
+                           else fn) for k, fn in extra)
         # The primary number is measured by now: a sub-benchmark that hangs
         # (a peer mapping refused in a way that blocks, a stuck collective)
         # must not take it down. Past --extras-timeout every rank dumps its
@@ -1120,7 +1128,7 @@ def main():
         for key, fn in extra:
             if args.no_extra:
                 break
-            if key not in wanted or key in P2P_KEYS:
+            if key not in wanted or key in child_keys:
                 continue
             _progress(rank, "sub-benchmark %s" % key)
             out["_running"] = key
@@ -1135,7 +1143,7 @@ def main():
                 res = {"error": err or "failed on another rank"}
             res["wall_s"] = round(time.perf_counter() - t0, 2)
             out[key] = res
-        p2p = [k for k, _ in extra if k in P2P_KEYS and k in wanted and not args.no_extra]
+        p2p = [k for k, _ in extra if k in child_keys and k in wanted and not args.no_extra]
         if p2p:
             _progress(rank, "sub-benchmarks %s (child processes)" % ",".join(p2p))
             out["_running"] = "p2p children"
@@ -1360,14 +1368,23 @@ def _named_in_child(world, rank, dev, steps):
     name negotiation's first over RCCL (a split-off control communicator and
     a negotiation thread), so it is isolated like the P2P paths — a hang or
     fault there ends the child, not the line."""
-    if "ex" not in _NATIVE and _OPTS.get("test_transport") == "ipc":
-        _NATIVE["ex"] = _ipc_exchange(rank, world, dev, "auto")
     if "ex" not in _NATIVE:
         if dist.get_backend() != "nccl":
             raise RuntimeError("the name-keyed path needs the native exchange (nccl backend)")
         from kungfu_amd.exchange import NativeExchange
         _NATIVE["ex"] = NativeExchange(algo="auto", device=dev)
     return bench_c4_named(world, rank, dev, steps, 5)
+
+
+def _named_ipc(world, rank, dev, steps):
+    """c4_named under --test-transport ipc, in this process, over an ipc
+    exchange of its own (the name-keyed path must not interleave with the
+    primary's ordered calls on one exchange)."""
+    ex = _ipc_exchange(rank, world, dev, "auto")
+    try:
+        return bench_c4_named(world, rank, dev, steps, 5, ex=ex)
+    finally:
+        ex.close()
 
 
 def p2p_extras(args, rank, world, local_rank, dev, keys, seconds):
@@ -1802,7 +1819,7 @@ def _rs_avg_verdict(got, ref, spans, world):
             "transport": kind, "inputs": "N(0,1) fp32, no subnormal x / world"}
 
 
-def bench_c4_named(world, rank, dev, steps, warmup):
+def bench_c4_named(world, rank, dev, steps, warmup, ex=None):
     """C4's 214 ResNet-50 gradient tensors one by one through the name-keyed
     all-reduce (kf_exchange_all_reduce_named, the torch op's path:
     all_reduce_cuda_async keyed by tensor name), every rank starting them in
@@ -1812,7 +1829,7 @@ def bench_c4_named(world, rank, dev, steps, warmup):
     from kungfu_amd import ops
     from kungfu_amd.collective import GradBuckets
     sizes = _models()["resnet50-imagenet"]
-    ex = _NATIVE.get("ex")
+    ex = _NATIVE.get("ex") if ex is None else ex
     if ex is None:
         raise RuntimeError("native exchange unavailable (see collective.native_exchange_error)")
     gbs = [GradBuckets(sizes, torch.float32, dev, world, n_buckets=16) for _ in range(world)]
