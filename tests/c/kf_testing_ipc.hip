@@ -453,6 +453,7 @@ int ipc_split(void *comm, int color, int key, void **newcomm)
     rc = barrier(c);
     if (rc != IPC_OK) {
         if (n) {
+            shm_unlink(n->name.c_str());
             munmap(n->seg, sizeof(Seg));
             delete n;
         }
@@ -542,7 +543,8 @@ kf_exchange_t *kf_exchange_create_ipc(const char *name, int rank, int world, int
         return nullptr;
     }
     // every rank has mapped the segment before its name is removed
-    if (barrier(c) != IPC_OK) {
+    if (barrier(c) != IPC_OK) {  // a rank never came: leave no segment behind
+        shm_unlink(name);
         munmap(c->seg, sizeof(Seg));
         delete c;
         return nullptr;
