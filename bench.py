@@ -1735,7 +1735,8 @@ def bench_c3_torch(world, dev, steps, n, x, nb, fused):
                 nb, "coalesced into one RS -> /np -> AG" if fused else
                 "one RS -> HIP /np -> AG per bucket"),
             "ms_per_step": round(per_s * 1e3, 4),
-            "busbw_GBps": round(2 * (world - 1) / world * s_bytes / per_s / 1e9, 2)}
+            "busbw_GBps": round(2 * (world - 1) / world * s_bytes / per_s / 1e9, 2),
+            "correct": True}
 
 
 def bench_c4(world, rank, dev, steps, warmup, exchange="native"):
@@ -1911,7 +1912,7 @@ def bench_c3_ar(world, rank, dev, steps, warmup, n, x):
             "ms_per_step": round(step_s * 1e3, 4),
             "GiBps_per_gpu": round(s_bytes / step_s / 2**30, 3),
             "busbw_GBps": round(busbw, 2),
-            "frac_of_xgmi": _xgmi_frac(busbw, world)}
+            "frac_of_xgmi": _xgmi_frac(busbw, world), "correct": True}
 
 
 def bench_c3_p2p(world, rank, dev, steps, warmup, n, x, mode="pull", barrier="device"):
@@ -1970,7 +1971,8 @@ def bench_c3_p2p(world, rank, dev, steps, warmup, n, x, mode="pull", barrier="de
             "busbw_GBps": round(busbw, 2),
             "frac_of_xgmi": _xgmi_frac(busbw, world),
             "parity": "bit-exact vs rank-order fold before timing: yes; after timing, "
-                      "two fresh inputs: %s" % ("yes" if after else "NO")}
+                      "two fresh inputs: %s" % ("yes" if after else "NO"),
+            "correct": bool(after)}
 
 
 def bench_c5(world, rank, dev, steps, warmup, alpha=0.1, exchange="native"):
@@ -2100,7 +2102,8 @@ def bench_c4_overlap(world, rank, dev, steps, warmup):
             "serial_ms": round(t_s * 1e3, 4), "overlapped_ms": round(t_o * 1e3, 4),
             "ms_per_step": round(t_o * 1e3, 4),
             "hidden_frac": round(hidden, 3) if hidden is not None else None,
-            "parity": "N=2 bit-exact / N>2 order bound vs the rank-order average"}
+            "parity": "N=2 bit-exact / N>2 order bound vs the rank-order average",
+            "correct": True}
 
 
 def bench_c5_overlap(world, rank, dev, steps, warmup, alpha=0.1):
@@ -2165,7 +2168,8 @@ def bench_c5_overlap(world, rank, dev, steps, warmup, alpha=0.1):
             "serial_ms": round(t_s * 1e3, 4), "overlapped_ms": round(t_o * 1e3, 4),
             "ms_per_step": round(t_o * 1e3, 4),
             "hidden_frac": round(hidden, 3) if hidden is not None else None,
-            "parity": "overlapped blend == synchronous sma_ bit for bit"}
+            "parity": "overlapped blend == synchronous sma_ bit for bit",
+            "correct": True}
 
 
 if __name__ == "__main__":
