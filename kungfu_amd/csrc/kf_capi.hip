@@ -612,14 +612,30 @@ struct Staging {
     hipStream_t s = nullptr;
     void *dev     = nullptr;  // 3 regions: x | y | z
     size_t cap    = 0;        // bytes per region
+    void *bounce  = nullptr;  // page-locked, one region: for mixed host ranges
+    size_t bcap   = 0;
 
     void release()
     {
         if (dev) (void)hipFree(dev);
+        if (bounce) (void)hipHostFree(bounce);
         if (s) (void)hipStreamDestroy(s);
-        dev = nullptr;
-        s   = nullptr;
-        cap = 0;
+        dev    = nullptr;
+        bounce = nullptr;
+        s      = nullptr;
+        cap    = 0;
+        bcap   = 0;
+    }
+
+    int ensure_bounce(size_t bytes)
+    {
+        if (bytes <= bcap) return KF_OK;
+        if (bounce) KF_HIP(hipHostFree(bounce));
+        bounce = nullptr;
+        bcap   = 0;
+        KF_HIP(hipHostMalloc(&bounce, bytes, hipHostMallocDefault));
+        bcap = bytes;
+        return KF_OK;
     }
 
     int ensure_stream()
@@ -731,24 +747,31 @@ int registered(const void *p, size_t bytes, const void **dev)
 }
 
 // Where a host-API pointer lives: 0 pageable (or unknown to HIP), 1 page-locked
-// host memory (hipHostMalloc / kf_host_register), 2 device memory. `dev` is the
-// address a kernel uses for it. The whole range must be one kind.
+// host memory (hipHostMalloc / kf_host_register), 2 device memory, 3 a host
+// range that is page-locked only in part (e.g. a chunk running past the end
+// of a registered pool): HIP's own copies refuse those ("invalid argument",
+// profiles/r06/partial_register_r06i.txt), so they go through a page-locked
+// bounce buffer. `dev` is the address a kernel uses for kinds 1 and 2.
+constexpr int kMixed = 3;
+
+int host_kind(const void *p, hipPointerAttribute_t *a)
+{
+    if (hipPointerGetAttributes(a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return a->type == hipMemoryTypeHost ? 1 : a->type == hipMemoryTypeDevice ? 2 : 0;
+}
+
 int classify(const void *p, size_t bytes, const void **dev)
 {
     if (registered(p, bytes, dev)) return 1;
-    hipPointerAttribute_t a;
-    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
-        (void)hipGetLastError();
-        return 0;
-    }
-    int kind = a.type == hipMemoryTypeHost ? 1 : a.type == hipMemoryTypeDevice ? 2 : 0;
-    if (kind == 0 || !a.devicePointer) return 0;
+    hipPointerAttribute_t a, b;
+    const int kind   = host_kind(p, &a);
     const void *last = static_cast<const char *>(p) + bytes - 1;
-    hipPointerAttribute_t b;
-    if (hipPointerGetAttributes(&b, last) != hipSuccess) {
-        (void)hipGetLastError();
-        return 0;
-    }
+    const int klast  = host_kind(last, &b);
+    if (kind != 2 && klast != 2 && (kind == 1) != (klast == 1)) return kMixed;
+    if (kind == 0 || !a.devicePointer) return 0;
     if (b.type != a.type) return 0;
     if (kind == 2) {  // HBM of another GPU: leave it to the runtime's copies
         int cur = -1;
@@ -774,9 +797,10 @@ int transform2_host(const void *x, const void *y, void *out, size_t n,
     Staging &st = *lease;
     const void *gx = nullptr, *gy = nullptr, *gz = nullptr;
     const int kx = classify(x, bytes, &gx);
-    const int ky = kx ? classify(y, bytes, &gy) : 0;
-    const int kz = ky ? classify(out, bytes, &gz) : 0;
-    if (kx && ky && kz) {
+    const int ky = classify(y, bytes, &gy);
+    const int kz = classify(out, bytes, &gz);
+    const auto direct = [](int k) { return k == 1 || k == 2; };
+    if (direct(kx) && direct(ky) && direct(kz)) {
         int rc = st.ensure_stream();
         if (rc != KF_OK) return rc;
         const bool host_link = kx == 1 || ky == 1 || kz == 1;
@@ -792,11 +816,34 @@ int transform2_host(const void *x, const void *y, void *out, size_t n,
     char *dx = static_cast<char *>(st.dev);
     char *dy = dx + st.cap;
     char *dz = dy + st.cap;
-    KF_HIP(hipMemcpyAsync(dx, x, bytes, hipMemcpyHostToDevice, st.s));
-    KF_HIP(hipMemcpyAsync(dy, y, bytes, hipMemcpyHostToDevice, st.s));
+    // a mixed range is copied through the bounce buffer one at a time (the
+    // CPU copy, then the DMA, then a sync before the bounce is reused)
+    auto h2d = [&](char *dst, const void *src, int kind) -> int {
+        if (kind != kMixed) {
+            KF_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st.s));
+            return KF_OK;
+        }
+        int r = st.ensure_bounce(bytes);
+        if (r != KF_OK) return r;
+        KF_HIP(hipStreamSynchronize(st.s));
+        std::memcpy(st.bounce, src, bytes);
+        KF_HIP(hipMemcpyAsync(dst, st.bounce, bytes, hipMemcpyHostToDevice, st.s));
+        return KF_OK;
+    };
+    rc = h2d(dx, x, kx);
+    if (rc == KF_OK) rc = h2d(dy, y, ky);
+    if (rc != KF_OK) return rc;
     const void *ins[2] = {dx, dy};
     rc                 = dispatch_none(ins, 2, dz, n, dt, op, st.s);
     if (rc != KF_OK) return rc;
+    if (kz == kMixed) {
+        rc = st.ensure_bounce(bytes);
+        if (rc != KF_OK) return rc;
+        KF_HIP(hipMemcpyAsync(st.bounce, dz, bytes, hipMemcpyDeviceToHost, st.s));
+        KF_HIP(hipStreamSynchronize(st.s));
+        std::memcpy(out, st.bounce, bytes);
+        return KF_OK;
+    }
     KF_HIP(hipMemcpyAsync(out, dz, bytes, hipMemcpyDeviceToHost, st.s));
     KF_HIP(hipStreamSynchronize(st.s));
     return KF_OK;

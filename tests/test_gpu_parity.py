@@ -481,6 +481,24 @@ def test_host_paths_pageable_and_pinned(lib, orc):
     finally:
         for a in (x, y, z2):
             lib.kf_host_unregister(a.ctypes.data)
+    # buffers page-locked only in part (a chunk running past the end of a
+    # registered pool): HIP's own copies refuse them, so the library bounces
+    # them through page-locked memory of its own (profiles/r06/
+    # partial_register_r06i.txt: "invalid argument" before)
+    half = n // 2
+    z3 = np.zeros_like(x)
+    assert lib.kf_host_register(x.ctypes.data, half * 4) == 0
+    assert lib.kf_host_register(z3.ctypes.data, half * 4) == 0
+    try:
+        assert lib.kf_transform2_host(x.ctypes.data, y.ctypes.data, z3.ctypes.data, n,
+                                      0x20408, 0) == 0, lib.kf_last_error()
+        assert np.array_equal(z3, want)
+        z3[:] = 0
+        lib.std_transform_2(x.ctypes.data, y.ctypes.data, z3.ctypes.data, n, 0x20408, 0)
+        assert np.array_equal(z3, want)
+    finally:
+        lib.kf_host_unregister(x.ctypes.data)
+        lib.kf_host_unregister(z3.ctypes.data)
 
 
 @pytest.mark.parametrize("dt", ["f32", "f16", "i32", "f64", "u8", "bf16"])
