@@ -403,6 +403,8 @@ def test_session_device_ops(dt, op):
 
 
 @pytest.mark.gpu
+@pytest.mark.gpu_slow  # a stress case (40 chunks, 4 KiB pieces); the streamed
+# stages keep their default-tier cases in test_session_device_streamed_*
 def test_session_device_streamed_stress():
     """the streamed kernels write page-locked memory the
     host sender reads after per-block flags. Every byte of a 40-chunk bucket
@@ -418,7 +420,8 @@ def test_session_device_streamed_stress():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("strategy", ["RING", "BINARY_TREE"])
+@pytest.mark.parametrize("strategy", ["RING", pytest.param("BINARY_TREE",
+                                                           marks=pytest.mark.gpu_slow)])
 def test_session_device_streamed_launch_race(strategy):
     """rank 2 of [RING-3-4-rand-0] aborted in the HIP
     runtime ("Cannot create GlobalVar Obj for symbol ... g_seen") when the
