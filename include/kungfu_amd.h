@@ -189,7 +189,9 @@ int kf_bucket_reduce_peers(const void *const *inputs, int k, void *out, size_t n
 
 /* Page-lock / release a host range so std_transform_2 and
  * kf_transform2_host can DMA it directly (e.g. a receive-buffer pool the
- * transport reuses, srcs/go/rchannel/connection/byte_slice_pool.go:28-60). */
+ * transport reuses, srcs/go/rchannel/connection/byte_slice_pool.go:28-60).
+ * The library remembers the range (a chunk inside it needs no pointer
+ * queries); release it with kf_host_unregister(p), p the registered base. */
 int kf_host_register(void *p, size_t bytes);
 int kf_host_unregister(void *p);
 

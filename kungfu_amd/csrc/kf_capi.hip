@@ -16,7 +16,6 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <iterator>
 #include <map>
 #include <mutex>
 #include <shared_mutex>
@@ -712,11 +711,12 @@ class StagingLease
 
 // Host ranges page-locked through kf_host_register, with the address a kernel
 // uses for each: std_transform_2 finds a chunk of one of them with one lookup
-// under a shared lock instead of two hipPointerGetAttributes per buffer (six
-// per call, about 1 us each: a third of the call at the reference's 64 KiB
-// chunks, tools/explore/b1_floor.hip). Only ranges the library registered
-// itself are remembered — it also sees them unregistered — so a lookup is
-// never stale. Never destroyed (see Staging).
+// under a shared lock instead of two hipPointerGetAttributes per buffer. (The
+// six queries take 0.34 us together, tools/explore/b1_floor.hip: the call's
+// cost is the GPU round trip) Only ranges the library
+// registered itself are remembered, and kf_host_unregister forgets them, so a
+// lookup is never stale as long as the host releases them through it (not
+// through hipHostUnregister). Never destroyed (see Staging).
 struct Registered {
     size_t bytes;
     char *dev;
