@@ -1137,6 +1137,10 @@ def main():
                 res, err = fn(), None
             except Exception as e:  # keep the primary line; say what failed
                 res, err = None, repr(e)[:300]
+                # every rank names its own failure (the line carries rank 0's,
+                # which may only be "failed earlier" after another rank's)
+                print("[bench] rank %d: sub-benchmark %s failed: %s" % (rank, key, err),
+                      file=sys.stderr, flush=True)
             # every rank learns whether every rank got through, before any
             # starts the next sub-benchmark's collectives
             if not _agree(err is None, dev):
@@ -1569,8 +1573,10 @@ def _ipc_exchange(rank, world, dev, algo):
     if tests not in sys.path:
         sys.path.insert(0, tests)
     from loopback import ipc_exchange
+    # a rendezvous may wait out the other ranks' time slices on the shared
+    # GPU; the line's own watchdog (--extras-timeout) bounds the whole run
     return ipc_exchange("/kf_bench_ipc_%x" % int(tok.item()), rank, world, algo=algo,
-                        device=dev.index, timeout_s=60.0)
+                        device=dev.index, timeout_s=300.0)
 
 
 def _rccl_report(native, world, fallback):

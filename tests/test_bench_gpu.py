@@ -257,8 +257,9 @@ def test_bench_native_branch_over_ipc_transport(world):
     assert "native_exchange_error" not in c and c["exchange"].startswith("native"), c
     assert c["correct"] is True, c
     assert sorted(c["schedule_trial_ms"]) == ["a2a", "fused", "grouped", "pipelined"], c
+    why = "\n".join(l for l in r.stderr.splitlines() if "failed" in l)[-3000:]
     for k in _IPC_EXTRAS:
-        assert "error" not in d[k] and d[k]["correct"] is True, (k, d[k])
+        assert "error" not in d[k] and d[k]["correct"] is True, (k, d[k], why)
         assert d[k]["ms_per_step"] > 0, (k, d[k])
     # the phase windows account for the un-pipelined timed steps: their sum
     # is the step minus the host's gaps between calls
