@@ -69,6 +69,7 @@ struct Slot {
     // moving mismatched bytes)
     uint64_t seq, bytes;
     int32_t kind, root;
+    int32_t grow_ok[2];  // this rank's export / import of a growth attempt
 };
 
 struct Seg {
@@ -157,61 +158,107 @@ void drop_peers(IpcComm *c)
     }
 }
 
-// every rank calls with the same `need` (the collectives are symmetric)
-int ensure(IpcComm *c, size_t need)
+// this rank's half of one growth attempt: a fresh staging buffer of `cap`
+// bytes, exported into its slot; false with *why on failure
+bool stage_export(IpcComm *c, size_t cap, std::string *why)
 {
-    if (need <= c->cap) return IPC_OK;
-    // at least 64 MiB: a smaller hipMalloc may be carved out of a shared
-    // fragment, and exporting one failed now and then with "invalid argument"
-    // (r06d, 4 processes on one GPU). The buffer must be the whole
-    // allocation its handle describes.
-    size_t cap = size_t(64) << 20;
-    while (cap < need) cap <<= 1;
     drop_peers(c);
     if (c->stage) (void)hipFree(c->stage);
     c->stage = nullptr;
     c->cap   = 0;
     hipError_t e = hipMalloc(&c->stage, cap);
-    if (e != hipSuccess) return hip_fail(c, e, "ipc transport: hipMalloc of the staging buffer");
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        c->stage = nullptr;
+        *why     = std::string("hipMalloc of the staging buffer: ") + hipGetErrorString(e);
+        return false;
+    }
     void *base  = nullptr;
     size_t span = 0;
     e           = hipMemGetAddressRange(&base, &span, c->stage);
-    if (e != hipSuccess) return hip_fail(c, e, "hipMemGetAddressRange of the staging buffer");
-    if (base != c->stage) {
-        return fail(c, IPC_HIP, "ipc transport: the staging buffer is not the base of its allocation");
+    if (e != hipSuccess || base != c->stage) {
+        (void)hipGetLastError();
+        *why = "the staging buffer is not the base of its allocation";
+        return false;
     }
     hipIpcMemHandle_t h;
     e = hipIpcGetMemHandle(&h, c->stage);
-    if (e != hipSuccess) return hip_fail(c, e, "hipIpcGetMemHandle of the staging buffer");
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        *why = std::string("hipIpcGetMemHandle of the staging buffer: ") + hipGetErrorString(e);
+        return false;
+    }
     std::memcpy(c->seg->slot[c->rank].handle, &h, sizeof(h));
     c->seg->slot[c->rank].cap = cap;
     c->cap                    = cap;
-    int rc = barrier(c);
-    if (rc != IPC_OK) return rc;
+    return true;
+}
+
+// the other half: map every peer's exported buffer
+bool stage_import(IpcComm *c, size_t cap, std::string *why)
+{
     c->peer[c->rank] = c->stage;
     for (int j = 0; j < c->world; ++j) {
         if (j == c->rank) continue;
-        if (c->seg->slot[j].cap != cap) return fail(c, IPC_ARG, "ipc transport: ranks disagree on a size");
+        if (c->seg->slot[j].cap != cap) {
+            *why = "ranks disagree on a size";
+            return false;
+        }
         hipIpcMemHandle_t ph;
         std::memcpy(&ph, c->seg->slot[j].handle, sizeof(ph));
-        // an import right after the export has been refused now and then
-        // with 4 processes on one GPU (r06d); a few short retries, counted
-        // in the error if they all fail
-        int tries = 0;
-        do {
-            e = hipIpcOpenMemHandle(&c->peer[j], ph, hipIpcMemLazyEnablePeerAccess);
-            if (e == hipSuccess) break;
-            (void)hipGetLastError();
-            struct timespec ts = {0, 2000000};
-            nanosleep(&ts, nullptr);
-        } while (++tries < 10);
+        hipError_t e = hipIpcOpenMemHandle(&c->peer[j], ph, hipIpcMemLazyEnablePeerAccess);
         if (e != hipSuccess) {
-            return fail(c, IPC_HIP, std::string("hipIpcOpenMemHandle of rank ") + std::to_string(j) +
-                                        "'s staging (" + std::to_string(tries) + " tries): " +
-                                        hipGetErrorString(e));
+            (void)hipGetLastError();
+            c->peer[j] = nullptr;
+            *why = std::string("hipIpcOpenMemHandle of rank ") + std::to_string(j) +
+                   "'s staging: " + hipGetErrorString(e);
+            return false;
         }
     }
-    return barrier(c);  // the slots are read before the next growth rewrites them
+    return true;
+}
+
+bool all_ok(IpcComm *c, int which)
+{
+    for (int j = 0; j < c->world; ++j) {
+        if (!c->seg->slot[j].grow_ok[which]) return false;
+    }
+    return true;
+}
+
+// Every rank calls with the same `need` (the collectives are symmetric), so
+// they grow together, and every rank takes the same decision from the flags
+// all of them post: an export or import refused on any rank (seen now and
+// then with 4 and 8 processes on one GPU, r06d and r06zz) makes every rank
+// drop the attempt and try again with fresh buffers, up to four times. At
+// least 64 MiB: a smaller hipMalloc may be carved out of a shared block, and
+// exporting such a piece was refused (r06d); the buffer must be the whole
+// allocation its handle describes.
+int ensure(IpcComm *c, size_t need)
+{
+    if (need <= c->cap) return IPC_OK;
+    size_t cap = size_t(64) << 20;
+    while (cap < need) cap <<= 1;
+    std::string why;
+    for (int attempt = 0;; ++attempt) {
+        Slot &me      = c->seg->slot[c->rank];
+        me.grow_ok[0] = stage_export(c, cap, &why) ? 1 : 0;
+        int rc        = barrier(c);
+        if (rc != IPC_OK) return rc;
+        bool ok       = all_ok(c, 0);
+        me.grow_ok[1] = ok && stage_import(c, cap, &why) ? 1 : 0;
+        if ((rc = barrier(c)) != IPC_OK) return rc;
+        ok = all_ok(c, 1);
+        // the flags and handles are read before any rank rewrites them
+        if ((rc = barrier(c)) != IPC_OK) return rc;
+        if (ok) return IPC_OK;
+        if (attempt == 3) {
+            return fail(c, IPC_HIP, "ipc transport: staging buffers not shared after 4 attempts" +
+                                        (why.empty() ? std::string() : " (this rank: " + why + ")"));
+        }
+        struct timespec ts = {0, 5000000};
+        nanosleep(&ts, nullptr);
+    }
 }
 
 enum { K_RS = 1, K_AG = 2, K_A2A = 3, K_BC = 4 };
@@ -550,6 +597,12 @@ kf_exchange_t *kf_exchange_create_ipc(const char *name, int rank, int world, int
         return nullptr;
     }
     if (rank == 0) shm_unlink(name);
+    // staging for calls of up to 256 MiB from the start (every shape the
+    // bench and the tests use), so no growth falls in the middle of a run
+    if (ensure(c, size_t(256) << 20) != IPC_OK) {
+        ipc_destroy(c);
+        return nullptr;
+    }
     kf_exchange_t *ex = kf_exchange_create_transport(&kIpcOps, c, rank, world, device);
     if (!ex) {
         t_err = kf_exchange_last_error();
