@@ -277,15 +277,19 @@ def kernel_families(lib, dev):
            "kf_bucket_reduce_batch: 16 buckets of 4 MiB (C3's size), z = x + y, one launch")
     del sets
     torch.cuda.empty_cache()
-    # C5's blend step: BERT-base bf16 in the bench's buckets, one batched launch
-    from kungfu_amd.collective import GradBuckets
+    # C5's blend step: BERT-base bf16 in the bench's buckets, one batched
+    # launch; the sum workspaces laid out as the exchange lays them out
+    # (collective.workspace_like: flat, so the launch merges the buckets)
+    from kungfu_amd.collective import GradBuckets, workspace_like
     bert = _models()["bert"][:201]
     sets = []
     for _ in range(3):
         gbv = GradBuckets(bert, torch.bfloat16, dev, 8, bucket_bytes=16 << 20)
         for b in gbv.buckets:
             b.copy_(torch.randn(b.numel(), device=dev, generator=g).bfloat16())
-        sums = [torch.randn(b.numel(), device=dev, generator=g).bfloat16() for b in gbv.buckets]
+        sums = workspace_like(gbv.buckets)
+        for t in sums:
+            t.copy_(torch.randn(t.numel(), device=dev, generator=g).bfloat16())
         sets.append((_lib.ptr_array([b.data_ptr() for b in gbv.buckets]),
                      _lib.ptr_array([t.data_ptr() for t in sums]),
                      (ctypes.c_size_t * len(sums))(*[t.numel() for t in sums]), gbv, sums))
@@ -300,7 +304,9 @@ def kernel_families(lib, dev):
                                                 8, 0.1, sp), 3)
     report("sma_batch_c5_bf16", 3 * 2 * sum(t.numel() for t in sets[0][4]), us, ok,
            "kf_sma_blend_batch: C5's SMA blend step, BERT-base bf16 in %d buckets, one launch "
-           "(bit-identical to one kf_sma_blend per bucket)" % nbs)
+           "(the buckets and their sum workspaces are contiguous, as the exchange lays them "
+           "out, so they blend as one range; bit-identical to one kf_sma_blend per bucket)"
+           % nbs)
     del sets, v0
     torch.cuda.empty_cache()
     out.update(exchange_phase2(lib, dev, g))

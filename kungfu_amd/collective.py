@@ -92,6 +92,25 @@ def coalesce_runs(buckets):
     return runs
 
 
+def workspace_like(buckets):
+    """One workspace tensor per bucket (e.g. SMA's sum of each variable
+    bucket). When the buckets are one contiguous run (GradBuckets' flat
+    layout), the workspaces are views of ONE flat allocation in the same
+    order, so a kernel over (bucket, workspace) pairs sees two contiguous
+    ranges and launches once over them (kf_sma_blend_batch merges such
+    buckets)."""
+    buckets = list(buckets)
+    if len(buckets) > 1 and len(coalesce_runs(buckets)) == 1:
+        flat = torch.empty(sum(b.numel() for b in buckets), dtype=buckets[0].dtype,
+                           device=buckets[0].device)
+        out, off = [], 0
+        for b in buckets:
+            out.append(flat[off:off + b.numel()].view_as(b))
+            off += b.numel()
+        return out
+    return [torch.empty_like(b) for b in buckets]
+
+
 def resolve_algo(algo, dtype, op, world):
     """"rs" (RCCL reduce-scatter) or "a2a" (all-to-all + HIP rank-order fold)
     for one bucket dtype; "auto" keeps RCCL's reduce-scatter where its order

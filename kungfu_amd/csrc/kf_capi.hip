@@ -542,11 +542,32 @@ int launch_sma_batch(void *const *vs, const void *const *sums, const size_t *cou
         if (e != hipSuccess) return hip_fail(e, "sma batch kernel launch");
         return KF_OK;
     };
+    // Buckets that sit back to back in v AND in the sums (GradBuckets' flat
+    // layout with a flat sum workspace, collective.workspace_like) blend as
+    // ONE range: one tile grid with no ragged edge and no bucket search per
+    // bucket. Element-wise, so the bits are the per-bucket blend's.
+    struct Run {
+        void *v;
+        const void *s;
+        size_t n;
+    };
+    std::vector<Run> runs;
     for (int b = 0; b < nb; ++b) {
-        const size_t n = counts[b];
-        if (n == 0) continue;
-        const void *ins[1] = {sums[b]};
-        const Plan p       = make_plan(ins, 1, vs[b], n, sizeof(S));
+        if (counts[b] == 0) continue;
+        if (!runs.empty()) {
+            Run &r = runs.back();
+            if (static_cast<char *>(r.v) + r.n * sizeof(S) == vs[b] &&
+                static_cast<const char *>(r.s) + r.n * sizeof(S) == sums[b]) {
+                r.n += counts[b];
+                continue;
+            }
+        }
+        runs.push_back(Run{vs[b], sums[b], counts[b]});
+    }
+    for (const Run &run : runs) {
+        const size_t n     = run.n;
+        const void *ins[1] = {run.s};
+        const Plan p       = make_plan(ins, 1, run.v, n, sizeof(S));
         size_t nblk;
         if (p.vec_ok) {
             const size_t ned = p.head + (n - p.head - p.nvec * V);
@@ -560,8 +581,8 @@ int launch_sma_batch(void *const *vs, const void *const *sums, const size_t *cou
             if (rc != KF_OK) return rc;
         }
         const int j = a.nseg;
-        a.v[j]      = vs[b];
-        a.s[j]      = sums[b];
+        a.v[j]      = run.v;
+        a.s[j]      = run.s;
         a.n[j]      = n;
         a.head[j]   = p.head;
         a.nvec[j]   = p.nvec;

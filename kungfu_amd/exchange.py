@@ -236,7 +236,8 @@ class NativeExchange:
         key = tuple((b.data_ptr(), b.numel()) for b in buckets)
         sums = self._sums.get(key)
         if sums is None:
-            sums = [torch.empty_like(b) for b in buckets]
+            from .collective import workspace_like
+            sums = workspace_like(buckets)  # flat when the buckets are
             self._sums[key] = sums
         vp = [b.data_ptr() for b in buckets]
         sp = [s.data_ptr() for s in sums]

@@ -217,9 +217,8 @@ class _SMA(_Bucketed):
     # result is the same bit for bit.
     def _kf_start_sums(self):
         if self._kf_sums is None:
-            import torch
-            self._kf_sums = [[torch.empty_like(b) for b in gb.buckets]
-                             for _, gb in self._kf_groups]
+            from .collective import workspace_like
+            self._kf_sums = [workspace_like(gb.buckets) for _, gb in self._kf_groups]
         self._kf_pending = []
         into = getattr(self._kf_ex, "start_into_", None)
         for gi, ((_, gb), sums) in enumerate(zip(self._kf_groups, self._kf_sums)):

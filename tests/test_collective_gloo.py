@@ -300,6 +300,22 @@ def test_coalesce_runs():
     assert len(coalesce_runs(gb.buckets[::-1])) == 3
 
 
+def test_workspace_like_mirrors_a_contiguous_run():
+    """SMA's sum workspaces: for GradBuckets' contiguous buckets, views of ONE
+    flat allocation in the same order (so the blend launches once over both
+    ranges); otherwise one tensor per bucket."""
+    from kungfu_amd.collective import GradBuckets, workspace_like
+    gb = GradBuckets([1000, 3000, 5000], torch.float32, torch.device("cpu"), 2, n_buckets=3)
+    ws = workspace_like(gb.buckets)
+    assert [w.shape for w in ws] == [b.shape for b in gb.buckets]
+    for w0, w1 in zip(ws, ws[1:]):
+        assert w1.data_ptr() == w0.data_ptr() + w0.numel() * w0.element_size()
+    assert all(w.data_ptr() != b.data_ptr() for w, b in zip(ws, gb.buckets))
+    ws2 = workspace_like(gb.buckets[::-1])  # not one run: separate tensors
+    assert [w.shape for w in ws2] == [b.shape for b in gb.buckets[::-1]]
+    assert len({w.untyped_storage().data_ptr() for w in ws2}) == 3
+
+
 def body_coalesced_equals_per_bucket(rank, world, use_gpu):
     from kungfu_amd.collective import Exchange, GradBuckets
     ex = Exchange(epilogue=_epilogue(use_gpu))

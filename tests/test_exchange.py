@@ -1009,6 +1009,43 @@ def test_sma_blend_batch_matches_single(name, np_):
             assert np.array_equal(_to_np(a[j], name), want), j
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,np_", [("f32", 8), ("bf16", 8), ("bf16", 3), ("f16", 2),
+                                      ("f64", 5)])
+def test_sma_blend_batch_contiguous_runs(name, np_):
+    """Buckets back to back in v AND in the sums (GradBuckets' flat layout,
+    collective.workspace_like) are blended by kf_sma_blend_batch as merged
+    ranges — here three runs: 5 ragged buckets, then a bucket whose sum is
+    elsewhere (breaks the run), then 4 more, 20 k elements in the middle of a
+    run starting at an odd offset — bit-identical to one kf_sma_blend per
+    bucket and to the oracle."""
+    import torch
+    from kungfu_amd import ops
+    from oracle import oracle
+    dev = _gpu()
+    sizes = [7, 4099, 1 << 18, 33, 262147, 1000, 3, 20001, 65536, 5]
+    total = sum(sizes)
+    v_np = _rand(name, total + 1, 31)[1:]  # the flat v starts one element in
+    s_np = _rand(name, total + 1, 77)[1:]
+    vflat = _to_dev(_rand(name, total + 1, 31), name, dev)[1:]
+    sflat = _to_dev(_rand(name, total + 1, 77), name, dev)[1:]
+    offs = np.cumsum([0] + sizes)
+    a = [vflat[offs[i]:offs[i + 1]] for i in range(len(sizes))]
+    s = [sflat[offs[i]:offs[i + 1]] for i in range(len(sizes))]
+    s[5] = s[5].clone()  # its sum elsewhere: the run breaks around it
+    b = [t.clone() for t in a]
+    ops.sma_blend_batch_(a, s, np_, 0.1)
+    for v, x in zip(b, s):
+        ops.sma_blend_(v, x, np_, 0.1)
+    torch.cuda.synchronize()
+    for j, n in enumerate(sizes):
+        assert np.array_equal(_to_np(a[j], name), _to_np(b[j], name)), j
+        if name in ("f32", "bf16"):
+            want = oracle.sma_blend(v_np[offs[j]:offs[j + 1]], s_np[offs[j]:offs[j + 1]], name,
+                                    np_, 0.1)
+            assert np.array_equal(_to_np(a[j], name), want), j
+
+
 # ---- name-keyed all-reduce and splits ----------------------------------------
 
 @pytest.mark.gpu

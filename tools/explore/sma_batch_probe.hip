@@ -12,6 +12,9 @@
 //   xor_u4_late  the same, every store after the last xor (stores grouped)
 //   sma_u4_late  the shipped blend with its stores grouped after all math
 //   oop_u4       the shipped blend written to a third buffer (out of place)
+//   xor_flat_u4  the xor over the same bytes as ONE flat range: since round
+//                6 the shipped launch merges buckets that are contiguous in v
+//                and in the sums (as here), so this is its ceiling
 //
 // Each blend variant's bits are checked against the shipped kernel's.
 // 3 rotating sets, median of 7 x 24 launches.
@@ -111,6 +114,30 @@ __global__ void __launch_bounds__(BLOCK) probe(Args a, float c1, float c2, Div n
     }
 }
 
+// the same bytes as ONE flat range (what the shipped launch does since
+// round 6 when the buckets and the sums are both contiguous): the ceiling of
+// the merged launch
+__global__ void __launch_bounds__(BLOCK) xor_flat(u32x4 *v, const u32x4 *s, size_t nvec)
+{
+    const size_t v0 = static_cast<size_t>(blockIdx.x) * (BLOCK * U) + threadIdx.x;
+    u32x4 x[U], y[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const size_t vi = v0 + u * BLOCK;
+        x[u] = vi < nvec ? __builtin_nontemporal_load(v + vi) : u32x4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const size_t vi = v0 + u * BLOCK;
+        y[u] = vi < nvec ? __builtin_nontemporal_load(s + vi) : u32x4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const size_t vi = v0 + u * BLOCK;
+        if (vi < nvec) __builtin_nontemporal_store(x[u] ^ y[u], v + vi);
+    }
+}
+
 __global__ void fill(uint32_t *p, size_t n, uint32_t seed)
 {
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
@@ -186,6 +213,11 @@ int main()
         {"xor_u4_late", [&](int k) { probe<1><<<grid, BLOCK>>>(args[k], c1, c2, np); }},
         {"sma_u4_late", [&](int k) { probe<2><<<grid, BLOCK>>>(args[k], c1, c2, np); }},
         {"oop_u4", [&](int k) { probe<3><<<grid, BLOCK>>>(args[k], c1, c2, np); }},
+        {"xor_flat_u4", [&](int k) {
+             const size_t nv = total / 8;
+             xor_flat<<<static_cast<unsigned>((nv + BLOCK * U - 1) / (BLOCK * U)), BLOCK>>>(
+                 reinterpret_cast<u32x4 *>(V[k]), reinterpret_cast<const u32x4 *>(S[k]), nv);
+         }},
     };
     // bits (set 0): the blend variants against the shipped kernel
     {

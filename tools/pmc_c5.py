@@ -51,7 +51,10 @@ def run():
         gbv = GradBuckets(bert, torch.bfloat16, dev, 8, bucket_bytes=16 << 20)
         for b in gbv.buckets:
             b.copy_(torch.randn(b.numel(), device=dev, generator=g).bfloat16())
-        sums = [torch.randn(b.numel(), device=dev, generator=g).bfloat16() for b in gbv.buckets]
+        from kungfu_amd.collective import workspace_like
+        sums = workspace_like(gbv.buckets)  # as the exchange lays them out (flat)
+        for t in sums:
+            t.copy_(torch.randn(t.numel(), device=dev, generator=g).bfloat16())
         sets.append((_lib.ptr_array([b.data_ptr() for b in gbv.buckets]),
                      _lib.ptr_array([t.data_ptr() for t in sums]),
                      (ctypes.c_size_t * len(sums))(*[t.numel() for t in sums]), gbv, sums))
