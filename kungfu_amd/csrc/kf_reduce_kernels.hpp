@@ -843,6 +843,20 @@ template <> struct SmaMath<bf16_t> {
     }
 };
 
+// The full tile's load schedule. Held to 64 VGPRs, the compiler issued the
+// bf16 and fp16 blends' eight 16-B loads as three, a wait for the first two,
+// then five: fewer loads in flight per wave than the add kernels of the same
+// bytes. A scheduling barrier after the loads keeps all eight in flight
+// (57 VGPRs, no spill; tests/test_isa.py): 256 MiB bf16 0.793 -> 0.816 of
+// 8 TB/s, fp16 0.794 -> 0.822, fp32 0.807 -> 0.823, fp64 0.807 -> 0.820,
+// C5's batch 0.775 -> 0.794, the same bits (tools/ab_sma_sched.py,
+// profiles/r06/ab_sma_sched_r06p.jsonl). 0: the compiler's order; 1: the
+// barrier (shipped); 2: the loads interleaved (v0, s0, v1, s1, ...) and the
+// barrier, so each vector waits for its own two (0.79-0.81: behind 1).
+#ifndef KF_SMA_SCHED
+#define KF_SMA_SCHED 1
+#endif
+
 // One block `blk` of `nblk` working on one variable bucket (sma_kernel: the
 // grid; sma_batch_kernel: the bucket's share of it).
 template <typename T, typename C, int BLOCK, int UNROLL, bool P2>
@@ -876,10 +890,21 @@ __device__ __forceinline__ void sma_body(void *v, const void *s, size_t n, size_
         if (v0 + (UNROLL - 1) * BLOCK < nvec) {
             // full tile: every load issued before the first use
             Vec<S> a[UNROLL], b[UNROLL];
+#if KF_SMA_SCHED == 2
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u) {
+                a[u] = ld_vec<S, 1>(vb, v0 + u * BLOCK);
+                b[u] = ld_vec<S, 1>(sb, v0 + u * BLOCK);
+            }
+#else
 #pragma unroll
             for (int u = 0; u < UNROLL; ++u) a[u] = ld_vec<S, 1>(vb, v0 + u * BLOCK);
 #pragma unroll
             for (int u = 0; u < UNROLL; ++u) b[u] = ld_vec<S, 1>(sb, v0 + u * BLOCK);
+#endif
+#if KF_SMA_SCHED >= 1
+            __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
             for (int u = 0; u < UNROLL; ++u) {
                 st_vec<S>(vb, v0 + u * BLOCK,

@@ -220,3 +220,23 @@ def test_bf16_sma_blend_is_packed(kernels):
     for k in ks:
         assert sum(1 for ins in kernels[k] if ins.startswith("v_pk_mul_f32")) >= 48, k
         assert sum(1 for ins in kernels[k] if ins.startswith("v_pk_add_f32")) >= 16, k
+
+
+def test_sma_full_tile_issues_all_loads_first(kernels):
+    """Every SMA kernel's full tile (4 vectors of v and 4 of the sum per lane)
+    issues its eight 16-B loads back to back, before the first wait on them:
+    held to 64 VGPRs the compiler had split the bf16 and fp16 blends' loads
+    3 + 5 around a wait, one wave then keeping fewer loads in flight
+    (kf_reduce_kernels.hpp KF_SMA_SCHED; profiles/r06/ab_sma_sched_r06p.jsonl:
+    0.793 -> 0.816 of 8 TB/s for bf16, same bits)."""
+    ks = [k for k in kernels if k.startswith(("_ZN2kf10sma_kernelI", "_ZN2kf16sma_batch_kernelI"))]
+    assert len(ks) == 8, ks  # f32 f64 f16 bf16, single and batch
+    for k in ks:
+        run, best = 0, 0
+        for ins in kernels[k]:
+            if ins.startswith("global_load_dwordx4"):
+                run += 1
+                best = max(best, run)
+            elif ins.startswith("s_waitcnt") and "vmcnt" in ins:
+                run = 0
+        assert best >= 8, (k, best)
