@@ -279,7 +279,9 @@ def kernel_families(lib, dev):
     torch.cuda.empty_cache()
     # C5's blend step: BERT-base bf16 in the bench's buckets, one batched
     # launch; the sum workspaces laid out as the exchange lays them out
-    # (collective.workspace_like: flat, so the launch merges the buckets)
+    # (collective.workspace_like). In this 16 MiB-bucket layout every bucket
+    # is its own allocation, so the launch blends 13 ranges (buckets of one
+    # flat buffer, C4's layout, would merge into one)
     from kungfu_amd.collective import GradBuckets, workspace_like
     bert = _models()["bert"][:201]
     sets = []
@@ -304,8 +306,8 @@ def kernel_families(lib, dev):
                                                 8, 0.1, sp), 3)
     report("sma_batch_c5_bf16", 3 * 2 * sum(t.numel() for t in sets[0][4]), us, ok,
            "kf_sma_blend_batch: C5's SMA blend step, BERT-base bf16 in %d buckets, one launch "
-           "(the buckets and their sum workspaces are contiguous, as the exchange lays them "
-           "out, so they blend as one range; bit-identical to one kf_sma_blend per bucket)"
+           "(the exchange's 16 MiB-bucket layout, every bucket its own allocation; "
+           "bit-identical to one kf_sma_blend per bucket)"
            % nbs)
     del sets, v0
     torch.cuda.empty_cache()

@@ -12,6 +12,7 @@
 #   bash tools/gpu_r06.sh <tag> prof      # rocprofv3 stats + PMC traffic of the C2 kernel
 #   bash tools/gpu_r06.sh <tag> stream    # streamed-chunk session tests + C1 A/B against whole chunks
 #   bash tools/gpu_r06.sh <tag> c5        # C5's two kernels: rocprofv3 durations (tools/pmc_c5.py)
+#   bash tools/gpu_r06.sh <tag> c5pmc     # their PMC bytes (after c5, which it summarizes)
 set -u
 TAG=${1:?tag}
 shift
@@ -101,6 +102,14 @@ or hier_all_reduce or fake_agent or rehearsal or branch_single_rank"
   c5)
     step c5_trace 300 rocprofv3 --kernel-trace --stats -T -d "$OUT/c5" -o t --output-format csv -- \
         python3 tools/pmc_c5.py run || exit $? ;;
+  c5pmc)
+    # the same two kernels' HBM bytes, one counter per pass, then the summary
+    for c in FETCH_SIZE WRITE_SIZE; do
+      step c5_pmc_$c 120 rocprofv3 --pmc $c -T -d "$OUT/c5_$c" -o pmc --output-format csv -- \
+          python3 tools/pmc_c5.py run || exit $?
+    done
+    python3 tools/pmc_c5.py summarize "$OUT/c5" "$OUT/c5_FETCH_SIZE" "$OUT/c5_WRITE_SIZE" \
+        > "$OUT/pmc_c5.jsonl" && cat "$OUT/pmc_c5.jsonl" ;;
   *) echo "unknown stage $stage"; exit 2 ;;
   esac
 done

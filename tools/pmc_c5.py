@@ -29,7 +29,13 @@ ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 sys.path.insert(0, ROOT)
 
 LAUNCHES = 12
-KERNELS = {"sma_batch": "void kf::sma_batch_kernel", "a2a_fold": "void kf::reduce_batch_kernel"}
+# full names, or the short ones rocprofv3 -T (--truncate-kernels) writes
+KERNELS = {"sma_batch": ("void kf::sma_batch_kernel", "sma_batch_kernel"),
+           "a2a_fold": ("void kf::reduce_batch_kernel", "reduce_batch_kernel")}
+
+
+def _is(name, prefix):
+    return name.startswith(prefix[0]) or name == prefix[1]
 
 
 def shapes():
@@ -100,7 +106,7 @@ def _rows(d, pattern):
 def per_dispatch(d, counter, prefix):
     rows = {}
     for r in _rows(d, "*counter_collection.csv"):
-        if r["Counter_Name"] == counter and r["Kernel_Name"].startswith(prefix):
+        if r["Counter_Name"] == counter and _is(r["Kernel_Name"], prefix):
             key = int(r["Dispatch_Id"])
             rows[key] = rows.get(key, 0.0) + float(r["Counter_Value"])
     return [rows[k] for k in sorted(rows)]
@@ -109,7 +115,7 @@ def per_dispatch(d, counter, prefix):
 def durations(d, prefix):
     ts = []
     for r in _rows(d, "*kernel_trace.csv"):
-        if r["Kernel_Name"].startswith(prefix):
+        if _is(r["Kernel_Name"], prefix):
             ts.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
     return [dt for _, dt in sorted(ts)]
 
