@@ -390,6 +390,20 @@ fold_scalar(const InPtrs &in, int k, size_t i, const Div &np)
 // The body of one block, `blk` of `nblk` working on one bucket: reduce_kernel
 // runs it with (blockIdx.x, gridDim.x); the batch kernel below with the block's
 // index inside its bucket's share of the grid.
+// KF_REDUCE_SCHED: a scheduling barrier after the compile-time-k full tile's
+// loads, as for the SMA blend (KF_SMA_SCHED below). Left to itself the
+// compiler split several k = 2 instantiations' eight loads around a wait
+// (7 + 1 for fp16 and integer sums, 4 + 4 for bf16 min/max, 6 + 2 for the
+// bf16 average batch) and spread the waits of the rest over the adds. With
+// the barrier, in one process on the same 256 MiB buffers
+// (tools/ab_reduce_sched.py, profiles/r06/ab_reduce_sched_r06s.jsonl), same
+// bits: C2's fp32 sum 0.824 / 0.823 (unchanged), bf16 sum 0.816 -> 0.824,
+// fp16 0.813 -> 0.826, i32 0.805 -> 0.822, bf16 max 0.799 -> 0.820, fp32 min
+// 0.807 -> 0.822, (x + y) / 3 fp32 0.792 -> 0.802, bf16 / 8 0.785 -> 0.791,
+// the 16 x 4 MiB batch 0.770 / 0.767 (unchanged).
+#ifndef KF_REDUCE_SCHED
+#define KF_REDUCE_SCHED 1
+#endif
 template <typename T, int OP, int EPI, int KC, int BLOCK, int UNROLL, int LOADNT,
           int STPLAIN = 0>
 __device__ __forceinline__ void reduce_body(const InPtrs &in, int k, void *out, size_t n,
@@ -435,6 +449,9 @@ __device__ __forceinline__ void reduce_body(const InPtrs &in, int k, void *out, 
 #pragma unroll
                     for (int u = 0; u < UNROLL; ++u) v[j][u] = ld_vec<W, LOADNT>(sj, v0 + u * BLOCK);
                 }
+#if KF_REDUCE_SCHED
+                __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
                 for (int u = 0; u < UNROLL; ++u) {
 #pragma unroll
