@@ -404,6 +404,13 @@ fold_scalar(const InPtrs &in, int k, size_t i, const Div &np)
 #ifndef KF_REDUCE_SCHED
 #define KF_REDUCE_SCHED 1
 #endif
+// KF_FOLD_SCHED: the same barrier after the runtime-k fold's first two
+// inputs' loads. No effect (k = 3 / 4 / 8 fp32, k = 4 bf16 and C5's k = 8
+// batch all within 0.3 %, same bits; tools/ab_fold_sched.py,
+// profiles/r06/ab_fold_sched_r06x.jsonl), so it stays off.
+#ifndef KF_FOLD_SCHED
+#define KF_FOLD_SCHED 0
+#endif
 template <typename T, int OP, int EPI, int KC, int BLOCK, int UNROLL, int LOADNT,
           int STPLAIN = 0>
 __device__ __forceinline__ void reduce_body(const InPtrs &in, int k, void *out, size_t n,
@@ -478,6 +485,9 @@ __device__ __forceinline__ void reduce_body(const InPtrs &in, int k, void *out, 
 #pragma unroll
                     for (int u = 0; u < UNROLL; ++u) b[u] = ld_vec<W, LOADNT>(s1, v0 + u * BLOCK);
                 }
+#if KF_FOLD_SCHED
+                __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
                 for (int u = 0; u < UNROLL; ++u) {
 #pragma unroll
