@@ -752,7 +752,9 @@ Registry &registry()
     return *r;
 }
 
-// 1 with *dev set if [p, p + bytes) lies in one registered range
+// 1 with *dev set if [p, p + bytes) lies in one registered range; -1 if it
+// overlaps a registered range without lying inside it (page-locked in part);
+// 0 if it overlaps none
 int registered(const void *p, size_t bytes, const void **dev)
 {
     Registry &r = registry();
@@ -760,9 +762,13 @@ int registered(const void *p, size_t bytes, const void **dev)
     if (r.ranges.empty()) return 0;
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
     auto it           = r.ranges.upper_bound(a);
-    if (it == r.ranges.begin()) return 0;
+    // a registered range starting inside [a, a + bytes)
+    const bool later = it != r.ranges.end() && it->first < a + bytes;
+    if (it == r.ranges.begin()) return later ? -1 : 0;
     --it;
-    if (a + bytes > it->first + it->second.bytes) return 0;
+    const uintptr_t end = it->first + it->second.bytes;
+    if (a >= end) return later ? -1 : 0;
+    if (a + bytes > end) return -1;
     *dev = it->second.dev + (a - it->first);
     return 1;
 }
@@ -786,7 +792,9 @@ int host_kind(const void *p, hipPointerAttribute_t *a)
 
 int classify(const void *p, size_t bytes, const void **dev)
 {
-    if (registered(p, bytes, dev)) return 1;
+    const int reg = registered(p, bytes, dev);
+    if (reg == 1) return 1;
+    if (reg < 0) return kMixed;  // straddles the edge of a kf_host_register range
     hipPointerAttribute_t a, b;
     const int kind   = host_kind(p, &a);
     const void *last = static_cast<const char *>(p) + bytes - 1;
@@ -794,6 +802,11 @@ int classify(const void *p, size_t bytes, const void **dev)
     if (kind != 2 && klast != 2 && (kind == 1) != (klast == 1)) return kMixed;
     if (kind == 0 || !a.devicePointer) return 0;
     if (b.type != a.type) return 0;
+    // page-locked at both ends but through two registrations whose device
+    // addresses are not one run: no single pointer covers it
+    if (kind == 1 && static_cast<const char *>(b.devicePointer) !=
+                         static_cast<const char *>(a.devicePointer) + (bytes - 1))
+        return kMixed;
     if (kind == 2) {  // HBM of another GPU: leave it to the runtime's copies
         int cur = -1;
         if (hipGetDevice(&cur) != hipSuccess || cur != a.device) return 0;

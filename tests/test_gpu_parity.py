@@ -499,6 +499,25 @@ def test_host_paths_pageable_and_pinned(lib, orc):
     finally:
         lib.kf_host_unregister(x.ctypes.data)
         lib.kf_host_unregister(z3.ctypes.data)
+    # x page-locked by two registrations that meet at a page boundary (two
+    # pools back to back): no single device pointer need cover a call that
+    # straddles them, so it is bounced too; and y page-locked only in its
+    # middle (both ends pageable), found through the registry
+    page = 4096
+    cut = (-x.ctypes.data) % page + page * ((n * 4 // 2) // page)
+    mid0 = (-y.ctypes.data) % page + page * 16
+    mid1 = mid0 + page * ((n * 4 // 2) // page)
+    z4 = np.zeros_like(x)
+    assert lib.kf_host_register(x.ctypes.data, cut) == 0
+    assert lib.kf_host_register(x.ctypes.data + cut, n * 4 - cut) == 0, lib.kf_last_error()
+    assert lib.kf_host_register(y.ctypes.data + mid0, mid1 - mid0) == 0, lib.kf_last_error()
+    try:
+        lib.std_transform_2(x.ctypes.data, y.ctypes.data, z4.ctypes.data, n, 0x20408, 0)
+        assert np.array_equal(z4, want)
+    finally:
+        lib.kf_host_unregister(x.ctypes.data)
+        lib.kf_host_unregister(x.ctypes.data + cut)
+        lib.kf_host_unregister(y.ctypes.data + mid0)
 
 
 @pytest.mark.parametrize("dt", ["f32", "f16", "i32", "f64", "u8", "bf16"])
