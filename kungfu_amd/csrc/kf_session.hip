@@ -2267,7 +2267,8 @@ int kf_session::run(SessOp *one)
                                  (uint32_t(lb[2]) << 16) | (uint32_t(lb[3]) << 24);
             m.data.resize(len);
             rc = read_exact(fd, m.data.data(), len);
-            if (rc == KF_OK) stash.push_back(std::move(m));
+            // a broken session starts no call that could take it: read and drop
+            if (rc == KF_OK && broken_rc == KF_OK) stash.push_back(std::move(m));
         }
         if (rc != KF_OK) {
             pfds[bad].fd = -1;  // no message boundary left on it
