@@ -307,6 +307,14 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 // Load policy: LOADNT=1 marks the read streams non-temporal (each byte is read
 // once); chosen by measurement (tools/tune_reduce.py), see DESIGN.md.
+template <int LOADNT>
+__device__ __forceinline__ u32x4 ld_u4(const void *base, size_t vi)
+{
+    const u32x4 *p = reinterpret_cast<const u32x4 *>(base) + vi;
+    if constexpr (LOADNT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+
 template <typename S, int LOADNT>
 __device__ __forceinline__ Vec<S> ld_vec(const void *base, size_t vi)
 {
@@ -404,6 +412,12 @@ fold_scalar(const InPtrs &in, int k, size_t i, const Div &np)
 #ifndef KF_REDUCE_SCHED
 #define KF_REDUCE_SCHED 1
 #endif
+// KF_REDUCE_PIN: an empty asm on each loaded word after the barrier, so the
+// 8-bit min/max kernels' byte unpacking cannot be placed among the loads
+// (the barrier alone leaves them 5 + 3; A/B: tools/ab_reduce_sched.py p0/p1)
+#ifndef KF_REDUCE_PIN
+#define KF_REDUCE_PIN 0
+#endif
 // KF_FOLD_SCHED: the same barrier after the runtime-k fold's first two
 // inputs' loads. No effect (k = 3 / 4 / 8 fp32, k = 4 bf16 and C5's k = 8
 // batch all within 0.3 %, same bits; tools/ab_fold_sched.py,
@@ -450,14 +464,35 @@ __device__ __forceinline__ void reduce_body(const InPtrs &in, int k, void *out, 
             if constexpr (KC > 0) {
                 // compile-time k: all KC x UNROLL loads issued before any use
                 Vec<W> v[KC][UNROLL];
+#if KF_REDUCE_SCHED
+                // raw 16-B words up to the barrier, so no unpacking of a
+                // loaded word (the 8-bit lanes' byte extracts) is placed
+                // among the loads with a wait of its own
+                u32x4 raw[KC][UNROLL];
+#pragma unroll
+                for (int j = 0; j < KC; ++j) {
+                    const char *sj = src(j);
+#pragma unroll
+                    for (int u = 0; u < UNROLL; ++u) raw[j][u] = ld_u4<LOADNT>(sj, v0 + u * BLOCK);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int j = 0; j < KC; ++j) {
+#pragma unroll
+                    for (int u = 0; u < UNROLL; ++u) {
+#if KF_REDUCE_PIN
+                        asm volatile("" : "+v"(raw[j][u]));  // pins the unpack below here
+#endif
+                        __builtin_memcpy(&v[j][u], &raw[j][u], 16);
+                    }
+                }
+#else
 #pragma unroll
                 for (int j = 0; j < KC; ++j) {
                     const char *sj = src(j);
 #pragma unroll
                     for (int u = 0; u < UNROLL; ++u) v[j][u] = ld_vec<W, LOADNT>(sj, v0 + u * BLOCK);
                 }
-#if KF_REDUCE_SCHED
-                __builtin_amdgcn_sched_barrier(0);
 #endif
 #pragma unroll
                 for (int u = 0; u < UNROLL; ++u) {

@@ -9,10 +9,15 @@ adds, which for the SMA blend measured slower than one wait.
 
   r0  the compiler's order
   r1  a scheduling barrier after the loads
+  p0  r1 (the shipped schedule since r06s), loads kept as raw 16-B words
+  p1  p0 with an empty asm on each word after the barrier (KF_REDUCE_PIN),
+      which keeps the 8-bit min/max unpacking behind it
+  (AB_VARIANTS=p0,p1 selects a pair)
 
 Cases (3 rotating sets, 15 interleaved rounds, median), bits compared:
   c2_f32            kf_bucket_reduce f32 SUM, 256 MiB (the headline kernel)
-  sum_bf16 / sum_f16 / sum_i32 / max_bf16 / min_f32   the same shape
+  sum_bf16 / sum_f16 / sum_i32 / max_bf16 / min_f32 / max_u8 / min_i8
+                    the same shape
   avg_np3_f32       kf_bucket_reduce_avg (x + y) / 3 (IEEE division)
   avg_np8_bf16      (x + y) / 8 in bf16 (multiply by 1/8)
   batch16_f32       kf_bucket_reduce_batch k = 2 SUM, 16 x 4 MiB
@@ -30,8 +35,14 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 OUT = os.path.join(ROOT, "tools", "ab_lib")
-VARIANTS = ("r0", "r1")
-DT = {"f32": 0x20408, "bf16": 0x20209, "f16": 0x20208, "i32": 0x10408}
+# r0 / r1: KF_REDUCE_SCHED 0 / 1 (r06s); p0 / p1: KF_REDUCE_PIN 0 / 1 with the
+# barrier on (r06z5)
+VARIANTS = tuple(os.environ.get("AB_VARIANTS", "r0,r1").split(","))
+FLAGS = {"r0": ["-DKF_REDUCE_SCHED=0"], "r1": ["-DKF_REDUCE_SCHED=1"],
+         "p0": ["-DKF_REDUCE_SCHED=1", "-DKF_REDUCE_PIN=0"],
+         "p1": ["-DKF_REDUCE_SCHED=1", "-DKF_REDUCE_PIN=1"]}
+DT = {"f32": 0x20408, "bf16": 0x20209, "f16": 0x20208, "i32": 0x10408, "u8": 0x00108,
+      "i8": 0x10108}
 SUM, MIN, MAX = 0, 1, 2
 
 
@@ -45,7 +56,7 @@ def build():
     for name in VARIANTS:
         subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
                         "-fPIC", "-shared", "-ffp-contract=off", "-fvisibility=hidden",
-                        "-DKF_REDUCE_SCHED=%s" % name[1:],
+                        *FLAGS[name],
                         "-I" + os.path.join(ROOT, "include"), "-o", lib_path(name), src],
                        check=True)
         print("built", lib_path(name), flush=True)
@@ -71,16 +82,17 @@ def run():
     g = torch.Generator(device=dev).manual_seed(17)
     sp = torch.cuda.current_stream().cuda_stream
     tdt = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16,
-           "i32": torch.int32}
+           "i32": torch.int32, "u8": torch.uint8, "i8": torch.int8}
+    lims = {"i32": (-1 << 20, 1 << 20), "u8": (0, 256), "i8": (-128, 128)}
 
     def bufs(dt, nbytes):
         t = tdt[dt]
         n = nbytes // torch.empty((), dtype=t).element_size()
         out = []
         for _ in range(3):
-            if dt == "i32":
-                x = torch.randint(-1 << 20, 1 << 20, (n,), device=dev, generator=g, dtype=t)
-                y = torch.randint(-1 << 20, 1 << 20, (n,), device=dev, generator=g, dtype=t)
+            if dt in lims:
+                x = torch.randint(*lims[dt], (n,), device=dev, generator=g, dtype=t)
+                y = torch.randint(*lims[dt], (n,), device=dev, generator=g, dtype=t)
             else:
                 x = torch.randn(n, device=dev, generator=g).to(t)
                 y = torch.randn(n, device=dev, generator=g).to(t)
@@ -91,7 +103,8 @@ def run():
     cases = {}
     for name, dt, op in (("c2_f32", "f32", SUM), ("sum_bf16", "bf16", SUM),
                          ("sum_f16", "f16", SUM), ("sum_i32", "i32", SUM),
-                         ("max_bf16", "bf16", MAX), ("min_f32", "f32", MIN)):
+                         ("max_bf16", "bf16", MAX), ("min_f32", "f32", MIN),
+                         ("max_u8", "u8", MAX), ("min_i8", "i8", MIN)):
         sets = bufs(dt, 256 << 20)
         cases[name] = (lambda lib, i, sets=sets, dt=dt, op=op: lib.kf_bucket_reduce(
             sets[i][0], 2, sets[i][1].data_ptr(), sets[i][4], DT[dt], op, sp),
@@ -121,7 +134,7 @@ def run():
             _lib.check(launch(lib, 0), name + " " + v)
             torch.cuda.synchronize()
             outs[v] = snap()
-        same[name] = bool(torch.equal(outs["r0"], outs["r1"]))
+        same[name] = bool(torch.equal(outs[VARIANTS[0]], outs[VARIANTS[1]]))
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ts = {(c, v): [] for c in cases for v in libs}
     for r in range(15):
