@@ -414,9 +414,11 @@ fold_scalar(const InPtrs &in, int k, size_t i, const Div &np)
 #endif
 // KF_REDUCE_PIN: an empty asm on each loaded word after the barrier, so the
 // 8-bit min/max kernels' byte unpacking cannot be placed among the loads
-// (the barrier alone leaves them 5 + 3; A/B: tools/ab_reduce_sched.py p0/p1)
+// (the barrier alone left them 5 + 3): u8 max 0.799 -> 0.822, i8 min
+// 0.803 -> 0.820, every other case unchanged, same bits
+// (tools/ab_reduce_sched.py p0/p1, profiles/r06/ab_reduce_pin_r06z5.jsonl)
 #ifndef KF_REDUCE_PIN
-#define KF_REDUCE_PIN 0
+#define KF_REDUCE_PIN 1
 #endif
 // KF_FOLD_SCHED: the same barrier after the runtime-k fold's first two
 // inputs' loads. No effect (k = 3 / 4 / 8 fp32, k = 4 bf16 and C5's k = 8

@@ -245,17 +245,15 @@ def test_sma_full_tile_issues_all_loads_first(kernels):
 def test_two_input_reduce_issues_all_loads_first(kernels):
     """Every compile-time k = 2 product reduce (4 vectors of each input per
     lane) issues its eight 16-B loads before the first wait on them
-    (kf_reduce_kernels.hpp KF_REDUCE_SCHED; profiles/r06/ab_reduce_sched_r06s.jsonl).
-    The 8-bit min/max kernels are left out: they still split their loads
-    with the barrier, and their rate was not measured."""
+    (kf_reduce_kernels.hpp KF_REDUCE_SCHED and KF_REDUCE_PIN, the latter for
+    the 8-bit min/max, whose byte unpacking had split their loads 5 + 3;
+    profiles/r06/ab_reduce_sched_r06s.jsonl, ab_reduce_pin_r06z5.jsonl)."""
     pat = re.compile(r"^_ZN2kf(13reduce_kernel|19reduce_batch_kernel)I(\w+?)Li(\d)ELi\d+ELi2ELi256ELi4E")
     checked = 0
     for name, lines in product_kernels(kernels).items():
         m = pat.match(name)
         if not m:
             continue
-        if m.group(2) in ("h", "a") and m.group(3) in ("1", "2"):
-            continue  # u8 / i8 MIN, MAX
         run = best = 0
         for ins in lines:
             if ins.startswith("global_load_dwordx4"):
